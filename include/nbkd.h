@@ -1,0 +1,137 @@
+/*
+ * nbkd.h — C ABI of the MI355X-native kd-tree (libnbkd.so).
+ *
+ * Drop-in boundary for the reference's kd-tree hot path (wendazhou/nbodyhpc,
+ * kdtree/ subsystem).  Plain pointers and sizes; no exceptions and no C++ or
+ * torch types cross this boundary.  The pybind11 module nbodyhpc_amd.kdtree._impl
+ * (mirror of kdtree/src/cpp/pybind.cpp) is one caller; a ctypes / cffi / JNI /
+ * cgo stub is another.
+ *
+ * Ownership: the caller owns every input and output buffer; the library owns
+ * the tree handle and everything on the device behind it.  Buffers are host
+ * memory unless the matching NBKD_*_DEVICE flag is set, in which case they are
+ * device pointers on the tree's device.  `stream` is a hipStream_t (NULL = the
+ * null stream); with host outputs the call returns after the results are
+ * copied back, with device outputs it returns once the work is enqueued.
+ *
+ * Every entry point returns an nbkd_status; on failure nbkd_last_error()
+ * (thread-local) holds a message.  Statuses NBKD_EINVAL / NBKD_EBOX /
+ * NBKD_ETOOMANY carry the reference's exact messages (kdtree/src/cpp/pybind.cpp:17,43-45,93;
+ * kdtree/src/cpp/kdtree.cpp:99).
+ */
+#ifndef NBKD_H
+#define NBKD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef int32_t nbkd_status;
+
+enum {
+    NBKD_OK = 0,
+    NBKD_EINVAL = 1,   /* bad argument: shape, k <= 0, NULL pointer, ...              */
+    NBKD_EBOX = 2,     /* periodic build: a coordinate outside [0, box_size]           */
+    NBKD_ETOOMANY = 3, /* more than UINT32_MAX (padded) points                         */
+    NBKD_ENOMEM = 4,   /* host or device allocation failed                             */
+    NBKD_EDEVICE = 5   /* HIP runtime error, no device, or kernel failure              */
+};
+
+/* flags */
+#define NBKD_INPUT_DEVICE 0x1u  /* point / query arrays are device pointers */
+#define NBKD_OUTPUT_DEVICE 0x2u /* output arrays are device pointers        */
+
+typedef struct nbkd_tree nbkd_tree;
+
+/* Node record, bit-identical to KDTree::KDTreeNode (kdtree/src/cpp/include/kdtree/kdtree.hpp:149-163). */
+typedef struct {
+    int32_t dimension; /* split axis, -1 = leaf                               */
+    float split;       /* split value (internal nodes), 0.0f for leaves       */
+    uint32_t left;     /* internal: left child id;  leaf: first point (tree order) */
+    uint32_t right;    /* internal: right child id; leaf: one past the last point  */
+} nbkd_node;
+
+/*
+ * Build a tree over n points given as an (n, 3) row-major float32 array.
+ * Replaces: PyKDTree::PyKDTree / make_positions_and_indices (kdtree/src/cpp/pybind.cpp:14-56,76-88)
+ *           and KDTree::KDTree (kdtree/src/cpp/kdtree.cpp:95-131).
+ *   leaf_size  as the caller passes it; the reference clamps to >= 16
+ *              (kdtree/src/cpp/include/kdtree/kdtree_impl.hpp:485).
+ *   periodic   0 or 1; when 1 every coordinate must lie in [0, box_size].
+ *   device     HIP device ordinal (< 0: the calling thread's current device).
+ * The node table equals the reference's for the same (points, leaf_size):
+ * preorder, left child = id + 1, split = the m-th order statistic with
+ * m = (count/2)/8*8, leaves <= max(leaf_size, 16) points, padded to a multiple
+ * of 8 with FLT_MAX coordinates and indices n..n8-1.
+ */
+nbkd_status nbkd_build(const float *xyz, uint64_t n, int32_t leaf_size, int32_t periodic,
+                       float box_size, int32_t device, uint32_t flags, void *stream,
+                       nbkd_tree **out);
+
+/*
+ * k nearest neighbours of m query points (row-major (m, 3) float32).
+ * Replaces: PyKDTree::query (kdtree/src/cpp/pybind.cpp:90-189) and
+ *           KDTree::find_closest (kdtree/src/cpp/kdtree.cpp:133-159).
+ * out_dist / out_idx are (m, k) row-major: rows sorted by squared distance,
+ * distances = sqrtf(d2); slots beyond the number of points hold
+ * (sqrtf(FLT_MAX), 0xFFFFFFFF) as in the reference.
+ */
+nbkd_status nbkd_query_knn(const nbkd_tree *tree, const float *q, uint64_t m, int32_t k,
+                           float *out_dist, uint32_t *out_idx, uint32_t flags, void *stream);
+
+/*
+ * NEW (no reference counterpart): number of points with d2 <= r*r of each
+ * query (periodic metric when the tree is periodic).  out_count is (m,) uint32.
+ */
+nbkd_status nbkd_query_ball_count(const nbkd_tree *tree, const float *q, uint64_t m, float r,
+                                  uint32_t *out_count, uint32_t flags, void *stream);
+
+/*
+ * NEW: neighbour lists within r in CSR form.  out_offsets is (m+1,) uint64
+ * (always host memory); out_idx receives offsets[m] original point indices,
+ * each row sorted ascending.  Call with out_idx == NULL first to get
+ * offsets[m] (the required capacity), then again with a buffer of that size.
+ */
+nbkd_status nbkd_query_ball_csr(const nbkd_tree *tree, const float *q, uint64_t m, float r,
+                                uint64_t *out_offsets, uint32_t *out_idx, uint64_t capacity,
+                                uint32_t flags, void *stream);
+
+/* n8 = padded point count (the reference's `n`), nodes = node count (`size`). */
+nbkd_status nbkd_tree_info(const nbkd_tree *tree, uint64_t *n8, uint64_t *nodes,
+                           int32_t *periodic, float *box_size, int32_t *device);
+
+/* Copy the node table (nodes entries) and the tree-ordered SoA points and
+ * original indices (n8 entries each) to host buffers; any may be NULL. */
+nbkd_status nbkd_export(const nbkd_tree *tree, nbkd_node *nodes, float *x, float *y, float *z,
+                        uint32_t *idx);
+
+void nbkd_free(nbkd_tree *tree);
+
+/* thread-local message of the last failure on this thread ("" if none) */
+const char *nbkd_last_error(void);
+
+/* number of visible HIP devices (0 and NBKD_OK when there are none) */
+nbkd_status nbkd_device_count(int32_t *count);
+
+/* Kernel timing with HIP events recorded on the launch stream.  While enabled,
+ * each launch of a named kernel is bracketed by events; nbkd_timing_read
+ * synchronises them and returns the summed milliseconds and launch count of
+ * every launch of `name` since the last reset. */
+nbkd_status nbkd_timing_enable(int32_t enable);
+nbkd_status nbkd_timing_reset(void);
+nbkd_status nbkd_timing_read(const char *name, double *ms, uint64_t *launches);
+
+/* per-query work counters of the last kNN call on this thread (debug builds of
+ * the statistics, KDTreeQueryStatistics kdtree/src/cpp/include/kdtree/kdtree.hpp:124-131):
+ * sums over all queries of nodes visited and points scanned by the packet
+ * traversal.  Enabled with nbkd_stats_enable(1); costs a few % when on. */
+nbkd_status nbkd_stats_enable(int32_t enable);
+nbkd_status nbkd_stats_read(uint64_t *nodes_visited, uint64_t *points_scanned);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* NBKD_H */

@@ -1,0 +1,200 @@
+"""ctypes binding of the C ABI (include/nbkd.h) — the binding a ctypes caller
+of the reference's hot path would add.  Loads the in-tree
+nbodyhpc_amd/lib/libnbkd.so and raises if it is missing: there is no fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+
+import numpy as np
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG, "lib", "libnbkd.so")
+HEADER = os.path.join(os.path.dirname(PKG), "include", "nbkd.h")
+
+NBKD_OK, NBKD_EINVAL, NBKD_EBOX, NBKD_ETOOMANY, NBKD_ENOMEM, NBKD_EDEVICE = range(6)
+NBKD_INPUT_DEVICE = 0x1
+NBKD_OUTPUT_DEVICE = 0x2
+
+NODE_DTYPE = np.dtype([("dim", "<i4"), ("split", "<f4"), ("left", "<u4"), ("right", "<u4")])
+
+
+class NbkdError(RuntimeError):
+    def __init__(self, status, msg):
+        super().__init__(msg)
+        self.status = status
+
+
+_c_p = ctypes.c_void_p
+_u64 = ctypes.c_uint64
+_i32 = ctypes.c_int32
+_u32 = ctypes.c_uint32
+
+_PROTOS = {
+    "nbkd_build": (_i32, [_c_p, _u64, _i32, _i32, ctypes.c_float, _i32, _u32, _c_p,
+                          ctypes.POINTER(_c_p)]),
+    "nbkd_query_knn": (_i32, [_c_p, _c_p, _u64, _i32, _c_p, _c_p, _u32, _c_p]),
+    "nbkd_query_ball_count": (_i32, [_c_p, _c_p, _u64, ctypes.c_float, _c_p, _u32, _c_p]),
+    "nbkd_query_ball_csr": (_i32, [_c_p, _c_p, _u64, ctypes.c_float, _c_p, _c_p, _u64, _u32,
+                                   _c_p]),
+    "nbkd_tree_info": (_i32, [_c_p, ctypes.POINTER(_u64), ctypes.POINTER(_u64),
+                              ctypes.POINTER(_i32), ctypes.POINTER(ctypes.c_float),
+                              ctypes.POINTER(_i32)]),
+    "nbkd_export": (_i32, [_c_p, _c_p, _c_p, _c_p, _c_p, _c_p]),
+    "nbkd_free": (None, [_c_p]),
+    "nbkd_last_error": (ctypes.c_char_p, []),
+    "nbkd_device_count": (_i32, [ctypes.POINTER(_i32)]),
+    "nbkd_timing_enable": (_i32, [_i32]),
+    "nbkd_timing_reset": (_i32, []),
+    "nbkd_timing_read": (_i32, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_double),
+                                ctypes.POINTER(_u64)]),
+    "nbkd_stats_enable": (_i32, [_i32]),
+    "nbkd_stats_read": (_i32, [ctypes.POINTER(_u64), ctypes.POINTER(_u64)]),
+}
+
+
+def header_symbols() -> list[str]:
+    """Function names declared in include/nbkd.h."""
+    txt = open(HEADER).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(nbkd_[a-z_]+)\s*\(", txt)))
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} not built: run `python -m nbodyhpc_amd.build`")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in _PROTOS.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def _check(st):
+    if st != NBKD_OK:
+        raise NbkdError(st, lib().nbkd_last_error().decode())
+
+
+def device_count() -> int:
+    c = _i32(0)
+    _check(lib().nbkd_device_count(ctypes.byref(c)))
+    return c.value
+
+
+def _host_f32(a):
+    return np.ascontiguousarray(a, dtype=np.float32)
+
+
+class Tree:
+    """Owning handle over an nbkd_tree*.  Inputs are numpy arrays (host) or raw
+    device pointers (int) with `device_ptrs=True`."""
+
+    def __init__(self, points=None, leafsize=128, boxsize=None, device=-1, *, n=None,
+                 dev_ptr=None, stream=None):
+        L = lib()
+        h = _c_p()
+        flags = 0
+        if dev_ptr is not None:
+            ptr, count, flags = dev_ptr, n, NBKD_INPUT_DEVICE
+        else:
+            pts = _host_f32(points)
+            if pts.ndim != 2 or pts.shape[1] != 3:
+                raise RuntimeError("positions must be a 2D array of shape (N, 3)")
+            ptr, count = pts.ctypes.data, pts.shape[0]
+            self._keep = pts
+        periodic = boxsize is not None
+        st = L.nbkd_build(ptr, count, int(leafsize), 1 if periodic else 0,
+                          float(boxsize) if periodic else 0.0, int(device), flags, stream,
+                          ctypes.byref(h))
+        _check(st)
+        self.h = h
+        self._keep = None
+        n8, nn, per, box, dev = _u64(), _u64(), _i32(), ctypes.c_float(), _i32()
+        _check(L.nbkd_tree_info(h, ctypes.byref(n8), ctypes.byref(nn), ctypes.byref(per),
+                                ctypes.byref(box), ctypes.byref(dev)))
+        self.n, self.size = n8.value, nn.value
+        self.periodic, self.boxsize, self.device = bool(per.value), box.value, dev.value
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().nbkd_free(self.h)
+            self.h = None
+
+    __del__ = close
+
+    def export(self):
+        nodes = np.empty(self.size, NODE_DTYPE)
+        x, y, z = (np.empty(self.n, np.float32) for _ in range(3))
+        idx = np.empty(self.n, np.uint32)
+        _check(lib().nbkd_export(self.h, nodes.ctypes.data, x.ctypes.data, y.ctypes.data,
+                                 z.ctypes.data, idx.ctypes.data))
+        return nodes, x, y, z, idx
+
+    def query(self, q, k):
+        q = _host_f32(q)
+        m = q.shape[0]
+        d = np.empty((m, k), np.float32)
+        i = np.empty((m, k), np.uint32)
+        _check(lib().nbkd_query_knn(self.h, q.ctypes.data, m, int(k), d.ctypes.data,
+                                    i.ctypes.data, 0, None))
+        return d, i
+
+    def query_device(self, q_ptr, m, k, d_ptr, i_ptr, stream=None, input_device=True):
+        flags = NBKD_OUTPUT_DEVICE | (NBKD_INPUT_DEVICE if input_device else 0)
+        _check(lib().nbkd_query_knn(self.h, q_ptr, int(m), int(k), d_ptr, i_ptr, flags, stream))
+
+    def ball_count(self, q, r):
+        q = _host_f32(q)
+        out = np.empty(q.shape[0], np.uint32)
+        _check(lib().nbkd_query_ball_count(self.h, q.ctypes.data, q.shape[0], float(r),
+                                           out.ctypes.data, 0, None))
+        return out
+
+    def ball_count_device(self, q_ptr, m, r, out_ptr, stream=None):
+        _check(lib().nbkd_query_ball_count(self.h, q_ptr, int(m), float(r), out_ptr,
+                                           NBKD_INPUT_DEVICE | NBKD_OUTPUT_DEVICE, stream))
+
+    def ball_csr(self, q, r):
+        q = _host_f32(q)
+        m = q.shape[0]
+        off = np.empty(m + 1, np.uint64)
+        _check(lib().nbkd_query_ball_csr(self.h, q.ctypes.data, m, float(r), off.ctypes.data,
+                                         None, 0, 0, None))
+        idx = np.empty(int(off[-1]), np.uint32)
+        _check(lib().nbkd_query_ball_csr(self.h, q.ctypes.data, m, float(r), off.ctypes.data,
+                                         idx.ctypes.data if idx.size else None, idx.size, 0,
+                                         None))
+        return off, idx
+
+
+def timing_enable(on=True):
+    _check(lib().nbkd_timing_enable(1 if on else 0))
+
+
+def timing_reset():
+    _check(lib().nbkd_timing_reset())
+
+
+def timing_read(name):
+    ms, cnt = ctypes.c_double(), _u64()
+    _check(lib().nbkd_timing_read(name.encode(), ctypes.byref(ms), ctypes.byref(cnt)))
+    return ms.value, cnt.value
+
+
+def stats_enable(on=True):
+    _check(lib().nbkd_stats_enable(1 if on else 0))
+
+
+def stats_read():
+    a, b = _u64(), _u64()
+    _check(lib().nbkd_stats_read(ctypes.byref(a), ctypes.byref(b)))
+    return a.value, b.value

@@ -1,0 +1,343 @@
+// C ABI of libnbkd.so (include/nbkd.h).  Host code only; kernels live in
+// build.hip / query.hip.  No exception crosses the boundary.
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "internal.hpp"
+
+struct nbkd_tree {
+    nbkd::Tree t;
+};
+
+namespace nbkd {
+
+namespace {
+thread_local std::string g_err;
+thread_local uint64_t g_stats[2] = {0, 0};
+
+std::mutex g_tmu;
+bool g_timing = false;
+bool g_stats_on = false;
+struct TimedLaunch {
+    std::string name;
+    hipEvent_t a, b;
+};
+std::vector<TimedLaunch> g_pending;
+std::map<std::string, std::pair<double, uint64_t>> g_acc;
+
+struct DeviceGuard {
+    int prev = -1;
+    bool ok = true;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (dev >= 0 && dev != prev) ok = hipSetDevice(dev) == hipSuccess;
+    }
+    ~DeviceGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
+void free_tree(Tree &t) {
+    if (t.x) (void)hipFree(t.x);
+    if (t.y) (void)hipFree(t.y);
+    if (t.z) (void)hipFree(t.z);
+    if (t.idx) (void)hipFree(t.idx);
+    if (t.nodes) (void)hipFree(t.nodes);
+    t.x = t.y = t.z = nullptr;
+    t.idx = nullptr;
+    t.nodes = nullptr;
+    t.ws.release();
+}
+} // namespace
+
+void set_error(const std::string &msg) { g_err = msg; }
+
+nbkd_status hip_fail(hipError_t e, const char *what) {
+    g_err = std::string("HIP error ") + hipGetErrorName(e) + " (" + hipGetErrorString(e) +
+            ") in " + what;
+    (void)hipGetLastError();
+    return e == hipErrorOutOfMemory ? NBKD_ENOMEM : NBKD_EDEVICE;
+}
+
+bool timing_enabled() { return g_timing; }
+bool stats_enabled() { return g_stats_on; }
+void stats_store(uint64_t nodes, uint64_t points) {
+    g_stats[0] = nodes;
+    g_stats[1] = points;
+}
+
+TimedScope::TimedScope(const char *name, hipStream_t s) : name_(name), s_(s) {
+    if (!g_timing) return;
+    if (hipEventCreate(&a_) != hipSuccess) {
+        a_ = nullptr;
+        return;
+    }
+    (void)hipEventRecord(a_, s_);
+}
+
+TimedScope::~TimedScope() {
+    if (!a_) return;
+    hipEvent_t b;
+    if (hipEventCreate(&b) != hipSuccess) {
+        (void)hipEventDestroy(a_);
+        return;
+    }
+    (void)hipEventRecord(b, s_);
+    std::lock_guard<std::mutex> lk(g_tmu);
+    g_pending.push_back(TimedLaunch{name_, a_, b});
+}
+
+} // namespace nbkd
+
+using namespace nbkd;
+
+#define NBKD_GUARD_BEGIN try {
+#define NBKD_GUARD_END                                                                             \
+    }                                                                                              \
+    catch (std::bad_alloc const &) {                                                               \
+        set_error("host allocation failed");                                                       \
+        return NBKD_ENOMEM;                                                                        \
+    }                                                                                              \
+    catch (std::exception const &e) {                                                              \
+        set_error(e.what());                                                                       \
+        return NBKD_EDEVICE;                                                                       \
+    }                                                                                              \
+    catch (...) {                                                                                  \
+        set_error("unknown error");                                                                \
+        return NBKD_EDEVICE;                                                                       \
+    }
+
+extern "C" {
+
+const char *nbkd_last_error(void) { return g_err.c_str(); }
+
+nbkd_status nbkd_device_count(int32_t *count) {
+    if (!count) return NBKD_EINVAL;
+    int c = 0;
+    if (hipGetDeviceCount(&c) != hipSuccess) c = 0;
+    (void)hipGetLastError();
+    *count = c;
+    return NBKD_OK;
+}
+
+nbkd_status nbkd_build(const float *xyz, uint64_t n, int32_t leaf_size, int32_t periodic,
+                       float box_size, int32_t device, uint32_t flags, void *stream,
+                       nbkd_tree **out) {
+    NBKD_GUARD_BEGIN
+    g_err.clear();
+    if (!out || (n > 0 && !xyz)) {
+        set_error("nbkd_build: NULL argument");
+        return NBKD_EINVAL;
+    }
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+        (void)hipGetLastError();
+        set_error("no HIP device available: the MI355X kd-tree requires a GPU");
+        return NBKD_EDEVICE;
+    }
+    int dev = device;
+    if (dev < 0 && hipGetDevice(&dev) != hipSuccess) dev = 0;
+    if (dev >= ndev) {
+        set_error("nbkd_build: device ordinal out of range");
+        return NBKD_EINVAL;
+    }
+    DeviceGuard g(dev);
+    if (!g.ok) {
+        set_error("hipSetDevice failed");
+        return NBKD_EDEVICE;
+    }
+    auto *h = new nbkd_tree();
+    h->t.device = dev;
+    h->t.periodic = periodic ? 1 : 0;
+    h->t.box = periodic ? box_size : 0.0f;
+    nbkd_status st = build_tree(h->t, xyz, n, leaf_size, (flags & NBKD_INPUT_DEVICE) != 0,
+                                (hipStream_t)stream);
+    if (st != NBKD_OK) {
+        (void)hipStreamSynchronize((hipStream_t)stream);
+        free_tree(h->t);
+        delete h;
+        return st;
+    }
+    *out = h;
+    return NBKD_OK;
+    NBKD_GUARD_END
+}
+
+nbkd_status nbkd_query_knn(const nbkd_tree *tree, const float *q, uint64_t m, int32_t k,
+                           float *out_dist, uint32_t *out_idx, uint32_t flags, void *stream) {
+    NBKD_GUARD_BEGIN
+    g_err.clear();
+    if (!tree) {
+        set_error("nbkd_query_knn: NULL tree");
+        return NBKD_EINVAL;
+    }
+    if (k <= 0) {
+        set_error("k must be positive integer");
+        return NBKD_EINVAL;
+    }
+    if (m > 0 && (!q || !out_dist || !out_idx)) {
+        set_error("nbkd_query_knn: NULL argument");
+        return NBKD_EINVAL;
+    }
+    DeviceGuard g(tree->t.device);
+    return query_knn(tree->t, q, m, k, out_dist, out_idx, flags, (hipStream_t)stream);
+    NBKD_GUARD_END
+}
+
+nbkd_status nbkd_query_ball_count(const nbkd_tree *tree, const float *q, uint64_t m, float r,
+                                  uint32_t *out_count, uint32_t flags, void *stream) {
+    NBKD_GUARD_BEGIN
+    g_err.clear();
+    if (!tree || (m > 0 && (!q || !out_count))) {
+        set_error("nbkd_query_ball_count: NULL argument");
+        return NBKD_EINVAL;
+    }
+    DeviceGuard g(tree->t.device);
+    return query_ball_count(tree->t, q, m, r, out_count, flags, (hipStream_t)stream);
+    NBKD_GUARD_END
+}
+
+nbkd_status nbkd_query_ball_csr(const nbkd_tree *tree, const float *q, uint64_t m, float r,
+                                uint64_t *out_offsets, uint32_t *out_idx, uint64_t capacity,
+                                uint32_t flags, void *stream) {
+    NBKD_GUARD_BEGIN
+    g_err.clear();
+    if (!tree || !out_offsets || (m > 0 && !q)) {
+        set_error("nbkd_query_ball_csr: NULL argument");
+        return NBKD_EINVAL;
+    }
+    DeviceGuard g(tree->t.device);
+    return query_ball_csr(tree->t, q, m, r, out_offsets, out_idx, capacity, flags,
+                          (hipStream_t)stream);
+    NBKD_GUARD_END
+}
+
+nbkd_status nbkd_tree_info(const nbkd_tree *tree, uint64_t *n8, uint64_t *nodes, int32_t *periodic,
+                           float *box_size, int32_t *device) {
+    if (!tree) {
+        set_error("nbkd_tree_info: NULL tree");
+        return NBKD_EINVAL;
+    }
+    if (n8) *n8 = tree->t.n8;
+    if (nodes) *nodes = tree->t.nnodes;
+    if (periodic) *periodic = tree->t.periodic;
+    if (box_size) *box_size = tree->t.box;
+    if (device) *device = tree->t.device;
+    return NBKD_OK;
+}
+
+nbkd_status nbkd_export(const nbkd_tree *tree, nbkd_node *nodes, float *x, float *y, float *z,
+                        uint32_t *idx) {
+    NBKD_GUARD_BEGIN
+    if (!tree) {
+        set_error("nbkd_export: NULL tree");
+        return NBKD_EINVAL;
+    }
+    const Tree &t = tree->t;
+    DeviceGuard g(t.device);
+    if (nodes)
+        NBKD_HIP(hipMemcpy(nodes, t.nodes, t.nnodes * sizeof(nbkd_node), hipMemcpyDeviceToHost));
+    if (x) NBKD_HIP(hipMemcpy(x, t.x, t.n8 * 4, hipMemcpyDeviceToHost));
+    if (y) NBKD_HIP(hipMemcpy(y, t.y, t.n8 * 4, hipMemcpyDeviceToHost));
+    if (z) NBKD_HIP(hipMemcpy(z, t.z, t.n8 * 4, hipMemcpyDeviceToHost));
+    if (idx) NBKD_HIP(hipMemcpy(idx, t.idx, t.n8 * 4, hipMemcpyDeviceToHost));
+    return NBKD_OK;
+    NBKD_GUARD_END
+}
+
+void nbkd_free(nbkd_tree *tree) {
+    if (!tree) return;
+    DeviceGuard g(tree->t.device);
+    (void)hipDeviceSynchronize();
+    free_tree(tree->t);
+    delete tree;
+}
+
+nbkd_status nbkd_timing_enable(int32_t enable) {
+    g_timing = enable != 0;
+    return NBKD_OK;
+}
+
+nbkd_status nbkd_timing_reset(void) {
+    std::lock_guard<std::mutex> lk(g_tmu);
+    for (auto &p : g_pending) {
+        (void)hipEventSynchronize(p.b);
+        (void)hipEventDestroy(p.a);
+        (void)hipEventDestroy(p.b);
+    }
+    g_pending.clear();
+    g_acc.clear();
+    return NBKD_OK;
+}
+
+nbkd_status nbkd_timing_read(const char *name, double *ms, uint64_t *launches) {
+    if (!name) return NBKD_EINVAL;
+    std::lock_guard<std::mutex> lk(g_tmu);
+    for (auto &p : g_pending) {
+        if (hipEventSynchronize(p.b) != hipSuccess) return hip_fail(hipGetLastError(), "timing");
+        float t = 0.0f;
+        (void)hipEventElapsedTime(&t, p.a, p.b);
+        auto &acc = g_acc[p.name];
+        acc.first += t;
+        acc.second += 1;
+        (void)hipEventDestroy(p.a);
+        (void)hipEventDestroy(p.b);
+    }
+    g_pending.clear();
+    auto it = g_acc.find(name);
+    if (ms) *ms = it == g_acc.end() ? 0.0 : it->second.first;
+    if (launches) *launches = it == g_acc.end() ? 0 : it->second.second;
+    return NBKD_OK;
+}
+
+nbkd_status nbkd_stats_enable(int32_t enable) {
+    g_stats_on = enable != 0;
+    return NBKD_OK;
+}
+
+nbkd_status nbkd_stats_read(uint64_t *nodes_visited, uint64_t *points_scanned) {
+    if (nodes_visited) *nodes_visited = g_stats[0];
+    if (points_scanned) *points_scanned = g_stats[1];
+    return NBKD_OK;
+}
+
+} // extern "C"
+
+namespace nbkd {
+
+void *Workspace::get(int slot, size_t bytes, hipStream_t s) {
+    if (bytes == 0) bytes = 16;
+    if (cap[slot] >= bytes) return p[slot];
+    if (p[slot]) {
+        (void)hipStreamSynchronize(s);
+        (void)hipFree(p[slot]);
+        p[slot] = nullptr;
+        cap[slot] = 0;
+    }
+    size_t want = bytes + bytes / 8; // some headroom for the next, slightly larger call
+    hipError_t e = hipMalloc(&p[slot], want);
+    if (e != hipSuccess) {
+        (void)hip_fail(e, "hipMalloc(workspace)");
+        p[slot] = nullptr;
+        return nullptr;
+    }
+    cap[slot] = want;
+    return p[slot];
+}
+
+void Workspace::release() {
+    for (int i = 0; i < WS_NSLOTS; ++i) {
+        if (p[i]) (void)hipFree(p[i]);
+        p[i] = nullptr;
+        cap[i] = 0;
+    }
+}
+
+} // namespace nbkd

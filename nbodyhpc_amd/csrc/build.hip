@@ -1,0 +1,705 @@
+// GPU tree builder for gfx950.
+//
+// Produces the reference's node table (KDTreeBuilder::build_node,
+// kdtree/src/cpp/include/kdtree/kdtree_impl.hpp:492-540) on the device:
+//   * leaf iff count <= max(leaf_size, 16)                       (:485, :495)
+//   * m = (count / 2) / 8 * 8; split = m-th order statistic of the
+//     segment's coordinate on axis depth % 3                      (:502-510)
+//   * preorder ids, left child = id + 1, right = id + 1 + |left subtree|
+// The tree SHAPE is a pure function of (n8, leaf); only the split VALUES and
+// the point permutation depend on the data.  The shape (ids, segment ranges)
+// is enumerated on the host down to segments of SMALL points (~2 n / SMALL
+// records), the order statistics are found on the GPU:
+//
+//   large levels (segment > SMALL points), one launch sequence per depth:
+//     4 x { hist (tiles of 4096 keys -> per-segment 256-bin histograms, LDS
+//           then global atomics) ; select (one block per segment picks the
+//           digit holding rank m) }            -> exact m-th key = split
+//     count (per tile #<, #== pivot) ; scan (per segment over tiles) ;
+//     scatter (stable three-way partition, ballot/mbcnt ranks, SoA
+//           ping-pong A <-> B)
+//   small segments (<= SMALL points): one workgroup loads the segment into
+//     LDS (SoA, 2 x 32 KB) and finishes the whole subtree there, level by
+//     level, one wave per sub-segment (wave radix select + ballot partition),
+//     writing nodes and the final tree-ordered points to buffer A.
+//
+// Memory: SoA float x,y,z + uint32 original index = 16 B/point, two copies.
+#include <algorithm>
+#include <map>
+
+#include "internal.hpp"
+
+namespace nbkd {
+namespace {
+
+constexpr int TB = 256;              // threads per block
+constexpr int TILE = 4096;           // keys per tile in large-level passes
+constexpr int PER_T = TILE / TB;     // 16 keys per thread
+constexpr int SMALL = 2048;          // segments <= SMALL points finish in LDS
+constexpr int MAX_SUB = SMALL / 8;   // max sub-segments per level inside a block
+
+struct LSeg {
+    uint32_t node, left, count, m;
+    uint32_t lchild, rchild, tile_begin, tile_end;
+};
+struct Tile {
+    uint32_t seg, begin, count, pad;
+};
+struct SelState {
+    uint32_t prefix, rank, below, eq;
+};
+struct SSeg {
+    uint32_t node, left, count, flags; // flags: dim (bits 0-1), source buffer (bit 2)
+};
+struct SubSeg {
+    uint32_t node, off, count, dim;
+};
+
+struct Soa {
+    float *x, *y, *z;
+    uint32_t *i;
+};
+
+__device__ __forceinline__ float pick(int dim, float x, float y, float z) {
+    return dim == 0 ? x : (dim == 1 ? y : z);
+}
+
+__device__ __forceinline__ uint32_t mbcnt64(uint64_t mask) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                     __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
+// ------------------------------------------------------------------ prepare
+// pybind.cpp:14-56: AoS -> SoA, periodic range check, FLT_MAX padding, iota.
+__global__ void __launch_bounds__(TB)
+prepare_kernel(const float *__restrict__ aos, uint64_t n, uint64_t n8, int periodic, float L,
+               Soa out, uint32_t *bad) {
+    uint32_t flag = 0;
+    for (uint64_t i = blockIdx.x * (uint64_t)TB + threadIdx.x; i < n8;
+         i += (uint64_t)gridDim.x * TB) {
+        float px = FLT_MAX, py = FLT_MAX, pz = FLT_MAX;
+        if (i < n) {
+            px = aos[3 * i];
+            py = aos[3 * i + 1];
+            pz = aos[3 * i + 2];
+            if (periodic && !(px >= 0.0f && px <= L && py >= 0.0f && py <= L && pz >= 0.0f &&
+                              pz <= L))
+                flag = 1;
+        }
+        out.x[i] = px;
+        out.y[i] = py;
+        out.z[i] = pz;
+        out.i[i] = (uint32_t)i;
+    }
+    if (__any(flag) && (threadIdx.x & 63) == 0) atomicOr(bad, 1u);
+}
+
+// ------------------------------------------------------------------ large levels
+template <int PASS>
+__global__ void __launch_bounds__(TB)
+hist_kernel(const Tile *__restrict__ tiles, const LSeg *__restrict__ segs,
+            const SelState *__restrict__ st, const float *__restrict__ key_src,
+            uint32_t *__restrict__ hist) {
+    __shared__ uint32_t h[256];
+    const Tile tl = tiles[blockIdx.x];
+    h[threadIdx.x] = 0;
+    __syncthreads();
+    const LSeg sg = segs[tl.seg];
+    const uint32_t prefix = PASS > 0 ? st[tl.seg].prefix : 0u;
+    constexpr int shift = 24 - 8 * PASS;
+    const float *src = key_src + sg.left + tl.begin;
+#pragma unroll
+    for (int r = 0; r < PER_T; ++r) {
+        uint32_t e = r * TB + threadIdx.x;
+        if (e < tl.count) {
+            uint32_t k = fkey(src[e]);
+            if (((uint64_t)k >> (shift + 8)) == prefix) atomicAdd(&h[(k >> shift) & 255u], 1u);
+        }
+    }
+    __syncthreads();
+    uint32_t c = h[threadIdx.x];
+    if (c) atomicAdd(&hist[(size_t)tl.seg * 256 + threadIdx.x], c);
+}
+
+// block-wide exclusive scan of one value per thread (TB threads)
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *sh, uint32_t *total) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) sh[wave] = x;
+    __syncthreads();
+    uint32_t base = 0, tot = 0;
+    for (int w = 0; w < TB / 64; ++w) {
+        uint32_t s = sh[w];
+        if (w < wave) base += s;
+        tot += s;
+    }
+    if (total) *total = tot;
+    __syncthreads();
+    return base + x - v;
+}
+
+template <int PASS>
+__global__ void __launch_bounds__(TB)
+select_kernel(const LSeg *__restrict__ segs, SelState *__restrict__ st,
+              const uint32_t *__restrict__ hist, nbkd_node *__restrict__ nodes, int dim) {
+    __shared__ uint32_t sh[TB / 64];
+    const uint32_t seg = blockIdx.x;
+    const uint32_t c = hist[(size_t)seg * 256 + threadIdx.x];
+    // read the state before the scan's barriers: the selecting thread rewrites it
+    const SelState s0 = PASS == 0 ? SelState{0u, segs[seg].m, 0u, 0u} : st[seg];
+    const uint32_t ex = block_excl_scan(c, sh, nullptr);
+    if (s0.rank >= ex && s0.rank < ex + c) {
+        SelState s;
+        s.prefix = (s0.prefix << 8) | threadIdx.x;
+        s.rank = s0.rank - ex;
+        s.below = s0.below + ex;
+        s.eq = c;
+        st[seg] = s;
+        if (PASS == 3) {
+            const LSeg sg = segs[seg];
+            nodes[sg.node] = nbkd_node{dim, fkey_inv(s.prefix), sg.lchild, sg.rchild};
+        }
+    }
+}
+
+__global__ void __launch_bounds__(TB)
+count_kernel(const Tile *__restrict__ tiles, const LSeg *__restrict__ segs,
+             const SelState *__restrict__ st, const float *__restrict__ key_src,
+             uint2 *__restrict__ tile_cnt) {
+    __shared__ uint32_t sh[TB / 64];
+    const Tile tl = tiles[blockIdx.x];
+    const LSeg sg = segs[tl.seg];
+    const uint32_t piv = st[tl.seg].prefix;
+    const float *src = key_src + sg.left + tl.begin;
+    uint32_t lt = 0, eq = 0;
+#pragma unroll
+    for (int r = 0; r < PER_T; ++r) {
+        uint32_t e = r * TB + threadIdx.x;
+        if (e < tl.count) {
+            uint32_t k = fkey(src[e]);
+            lt += k < piv;
+            eq += k == piv;
+        }
+    }
+    uint32_t tlt, teq;
+    block_excl_scan(lt, sh, &tlt);
+    block_excl_scan(eq, sh, &teq);
+    if (threadIdx.x == 0) tile_cnt[blockIdx.x] = make_uint2(tlt, teq);
+}
+
+// one block per segment: exclusive prefix of (lt, eq) over its tiles
+__global__ void __launch_bounds__(TB)
+scan_kernel(const LSeg *__restrict__ segs, const uint2 *__restrict__ tile_cnt,
+            uint2 *__restrict__ tile_off, uint32_t tile_base) {
+    __shared__ uint32_t sh[TB / 64];
+    const LSeg sg = segs[blockIdx.x];
+    const uint32_t b = sg.tile_begin - tile_base, e = sg.tile_end - tile_base;
+    const uint32_t nt = e - b;
+    const uint32_t per = (nt + TB - 1) / TB;
+    const uint32_t t0 = b + threadIdx.x * per;
+    const uint32_t t1 = min(t0 + per, e);
+    uint32_t lt = 0, eq = 0;
+    for (uint32_t t = t0; t < t1; ++t) {
+        uint2 c = tile_cnt[t];
+        lt += c.x;
+        eq += c.y;
+    }
+    uint32_t blt = block_excl_scan(lt, sh, nullptr);
+    uint32_t beq = block_excl_scan(eq, sh, nullptr);
+    for (uint32_t t = t0; t < t1; ++t) {
+        tile_off[t] = make_uint2(blt, beq);
+        uint2 c = tile_cnt[t];
+        blt += c.x;
+        beq += c.y;
+    }
+}
+
+// stable three-way partition of one tile into dst
+__global__ void __launch_bounds__(TB)
+scatter_kernel(const Tile *__restrict__ tiles, const LSeg *__restrict__ segs,
+               const SelState *__restrict__ st, const uint2 *__restrict__ tile_off, int dim,
+               Soa src, Soa dst) {
+    __shared__ uint32_t cnt[PER_T][TB / 64][3];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const Tile tl = tiles[blockIdx.x];
+    const LSeg sg = segs[tl.seg];
+    const SelState s = st[tl.seg];
+    const uint32_t piv = s.prefix;
+    const uint2 off = tile_off[blockIdx.x];
+    const uint32_t base = sg.left + tl.begin;
+
+    float vx[PER_T], vy[PER_T], vz[PER_T];
+    uint32_t vi[PER_T];
+    uint32_t cls[PER_T];
+#pragma unroll
+    for (int r = 0; r < PER_T; ++r) {
+        uint32_t e = r * TB + threadIdx.x;
+        bool valid = e < tl.count;
+        uint32_t c = 3;
+        if (valid) {
+            vx[r] = src.x[base + e];
+            vy[r] = src.y[base + e];
+            vz[r] = src.z[base + e];
+            vi[r] = src.i[base + e];
+            uint32_t k = fkey(pick(dim, vx[r], vy[r], vz[r]));
+            c = k < piv ? 0u : (k == piv ? 1u : 2u);
+        }
+        cls[r] = c;
+        uint64_t b0 = __ballot(c == 0), b1 = __ballot(c == 1), b2 = __ballot(c == 2);
+        if (lane == 0) {
+            cnt[r][wave][0] = __popcll(b0);
+            cnt[r][wave][1] = __popcll(b1);
+            cnt[r][wave][2] = __popcll(b2);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < 3) {
+        uint32_t acc = 0;
+        for (int r = 0; r < PER_T; ++r)
+            for (int w = 0; w < TB / 64; ++w) {
+                uint32_t v = cnt[r][w][threadIdx.x];
+                cnt[r][w][threadIdx.x] = acc;
+                acc += v;
+            }
+    }
+    __syncthreads();
+    const uint32_t need = sg.m - s.below; // equal keys that go left
+    const uint32_t gt_prev = tl.begin - off.x - off.y;
+#pragma unroll
+    for (int r = 0; r < PER_T; ++r) {
+        uint32_t c = cls[r];
+        uint64_t b0 = __ballot(c == 0), b1 = __ballot(c == 1), b2 = __ballot(c == 2);
+        if (c < 3) {
+            uint64_t mine = c == 0 ? b0 : (c == 1 ? b1 : b2);
+            uint32_t rk = cnt[r][wave][c] + mbcnt64(mine);
+            uint32_t d;
+            if (c == 0) {
+                d = sg.left + off.x + rk;
+            } else if (c == 1) {
+                uint32_t er = off.y + rk;
+                d = er < need ? sg.left + s.below + er : sg.left + sg.m + (er - need);
+            } else {
+                d = sg.left + sg.m + (s.eq - need) + gt_prev + rk;
+            }
+            dst.x[d] = vx[r];
+            dst.y[d] = vy[r];
+            dst.z[d] = vz[r];
+            dst.i[d] = vi[r];
+        }
+    }
+}
+
+// ------------------------------------------------------------------ small segments
+__device__ __forceinline__ uint32_t subtree_nodes(uint32_t count, uint32_t leaf,
+                                                  const uint32_t *__restrict__ tab_c,
+                                                  const uint32_t *__restrict__ tab_n, int tab_len) {
+    if (count <= leaf) return 1u;
+    int lo = 0, hi = tab_len - 1;
+    while (lo < hi) {
+        int mid = (lo + hi) >> 1;
+        if (tab_c[mid] < count)
+            lo = mid + 1;
+        else
+            hi = mid;
+    }
+    return tab_n[lo];
+}
+
+struct SmallLds {
+    float x[2][SMALL];
+    float y[2][SMALL];
+    float z[2][SMALL];
+    uint32_t i[2][SMALL];
+    uint32_t hist[TB / 64][256];
+    SubSeg list[2][MAX_SUB];
+    uint32_t nlist[2];
+};
+
+__global__ void __launch_bounds__(TB)
+small_kernel(const SSeg *__restrict__ list, uint32_t leaf, Soa bufA, Soa bufB,
+             nbkd_node *__restrict__ nodes, const uint32_t *__restrict__ tab_c,
+             const uint32_t *__restrict__ tab_n, int tab_len) {
+    extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+    SmallLds &L = *reinterpret_cast<SmallLds *>(smem_raw);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const SSeg sg = list[blockIdx.x];
+    const Soa src = (sg.flags & 4u) ? bufB : bufA;
+    const Soa out = bufA;
+
+    if (sg.count > SMALL) { // a leaf larger than SMALL (leaf_size > SMALL): move it to A
+        if (threadIdx.x == 0) nodes[sg.node] = nbkd_node{-1, 0.0f, sg.left, sg.left + sg.count};
+        if (src.x != out.x)
+            for (uint32_t e = threadIdx.x; e < sg.count; e += TB) {
+                out.x[sg.left + e] = src.x[sg.left + e];
+                out.y[sg.left + e] = src.y[sg.left + e];
+                out.z[sg.left + e] = src.z[sg.left + e];
+                out.i[sg.left + e] = src.i[sg.left + e];
+            }
+        return;
+    }
+    for (uint32_t e = threadIdx.x; e < sg.count; e += TB) {
+        L.x[0][e] = src.x[sg.left + e];
+        L.y[0][e] = src.y[sg.left + e];
+        L.z[0][e] = src.z[sg.left + e];
+        L.i[0][e] = src.i[sg.left + e];
+    }
+    if (threadIdx.x == 0) {
+        L.list[0][0] = SubSeg{sg.node, 0u, sg.count, sg.flags & 3u};
+        L.nlist[0] = 1;
+        L.nlist[1] = 0;
+    }
+    __syncthreads();
+    int cur = 0, lc = 0;
+    while (L.nlist[lc] > 0) {
+        const uint32_t nsub = L.nlist[lc];
+        for (uint32_t s = wave; s < nsub; s += TB / 64) {
+            const SubSeg ss = L.list[lc][s];
+            if (ss.count <= leaf) {
+                if (lane == 0)
+                    nodes[ss.node] =
+                        nbkd_node{-1, 0.0f, sg.left + ss.off, sg.left + ss.off + ss.count};
+                for (uint32_t e = lane; e < ss.count; e += 64) {
+                    uint32_t g = sg.left + ss.off + e;
+                    out.x[g] = L.x[cur][ss.off + e];
+                    out.y[g] = L.y[cur][ss.off + e];
+                    out.z[g] = L.z[cur][ss.off + e];
+                    out.i[g] = L.i[cur][ss.off + e];
+                }
+                continue;
+            }
+            const float *kx = ss.dim == 0 ? L.x[cur] : (ss.dim == 1 ? L.y[cur] : L.z[cur]);
+            const uint32_t m = (ss.count / 2) / 8 * 8;
+            // wave radix select of rank m, 4 x 8-bit digits
+            uint32_t rank = m, prefix = 0, below = 0, eqc = 0;
+            uint32_t *h = L.hist[wave];
+#pragma unroll 1
+            for (int pass = 0; pass < 4; ++pass) {
+                const int shift = 24 - 8 * pass;
+                for (int j = 0; j < 4; ++j) h[lane * 4 + j] = 0;
+                wave_sync();
+                // 64-bit shift: a 32-bit shift by 32 (pass 0) is poison in LLVM IR
+                for (uint32_t e = lane; e < ss.count; e += 64) {
+                    uint32_t k = fkey(kx[ss.off + e]);
+                    if (((uint64_t)k >> (shift + 8)) == prefix)
+                        atomicAdd(&h[(k >> shift) & 255u], 1u);
+                }
+                wave_sync();
+                uint32_t c0 = h[lane * 4], c1 = h[lane * 4 + 1], c2 = h[lane * 4 + 2],
+                         c3 = h[lane * 4 + 3];
+                uint32_t sum = c0 + c1 + c2 + c3, x = sum;
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) {
+                    uint32_t y = __shfl_up(x, o, 64);
+                    if (lane >= o) x += y;
+                }
+                uint32_t ex = x - sum;
+                bool hit = rank >= ex && rank < x;
+                uint64_t bal = __ballot(hit);
+                int sel = __ffsll((unsigned long long)bal) - 1;
+                uint32_t r = rank - ex, j = 0, acc = 0, cc = c0;
+                if (r >= c0) {
+                    acc = c0;
+                    j = 1;
+                    cc = c1;
+                    if (r >= c0 + c1) {
+                        acc = c0 + c1;
+                        j = 2;
+                        cc = c2;
+                        if (r >= c0 + c1 + c2) {
+                            acc = c0 + c1 + c2;
+                            j = 3;
+                            cc = c3;
+                        }
+                    }
+                }
+                uint32_t digit = 4u * (uint32_t)sel + __shfl(j, sel, 64);
+                uint32_t before = __shfl(ex + acc, sel, 64);
+                eqc = __shfl(cc, sel, 64);
+#ifdef NBKD_DEBUG
+                if (blockIdx.x == 0 && lane == 0 && ss.node < 2)
+                    printf("node %u cnt %u m %u pass %d sel %d digit %u before %u eqc %u tot %u rank %u\n",
+                           ss.node, ss.count, m, pass, sel, digit, before, eqc, __shfl(x, 63, 64), rank);
+#endif
+                prefix = (prefix << 8) | digit;
+                below += before;
+                rank -= before;
+                wave_sync();
+            }
+            const uint32_t piv = prefix, need = m - below;
+            // stable three-way partition into the other buffer
+            uint32_t nlt = 0, neq = 0, ngt = 0;
+            for (uint32_t e0 = 0; e0 < ss.count; e0 += 64) {
+                uint32_t e = e0 + lane;
+                bool valid = e < ss.count;
+                uint32_t c = 3;
+                float px = 0, py = 0, pz = 0;
+                uint32_t pi = 0;
+                if (valid) {
+                    px = L.x[cur][ss.off + e];
+                    py = L.y[cur][ss.off + e];
+                    pz = L.z[cur][ss.off + e];
+                    pi = L.i[cur][ss.off + e];
+                    uint32_t k = fkey(pick(ss.dim, px, py, pz));
+                    c = k < piv ? 0u : (k == piv ? 1u : 2u);
+                }
+                uint64_t b0 = __ballot(c == 0), b1 = __ballot(c == 1), b2 = __ballot(c == 2);
+                if (valid) {
+                    uint32_t d;
+                    if (c == 0) {
+                        d = nlt + mbcnt64(b0);
+                    } else if (c == 1) {
+                        uint32_t er = neq + mbcnt64(b1);
+                        d = er < need ? below + er : m + (er - need);
+                    } else {
+                        d = m + (eqc - need) + ngt + mbcnt64(b2);
+                    }
+                    L.x[cur ^ 1][ss.off + d] = px;
+                    L.y[cur ^ 1][ss.off + d] = py;
+                    L.z[cur ^ 1][ss.off + d] = pz;
+                    L.i[cur ^ 1][ss.off + d] = pi;
+                }
+                nlt += __popcll(b0);
+                neq += __popcll(b1);
+                ngt += __popcll(b2);
+            }
+            const uint32_t rid = ss.node + 1 + subtree_nodes(m, leaf, tab_c, tab_n, tab_len);
+            if (lane == 0) {
+                nodes[ss.node] = nbkd_node{(int32_t)ss.dim, fkey_inv(piv), ss.node + 1, rid};
+                uint32_t slot = atomicAdd(&L.nlist[lc ^ 1], 2u);
+                uint32_t nd = (ss.dim + 1) % 3;
+                L.list[lc ^ 1][slot] = SubSeg{ss.node + 1, ss.off, m, nd};
+                L.list[lc ^ 1][slot + 1] = SubSeg{rid, ss.off + m, ss.count - m, nd};
+            }
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) L.nlist[lc] = 0;
+        cur ^= 1;
+        lc ^= 1;
+        __syncthreads();
+    }
+}
+
+// ------------------------------------------------------------------ host side
+struct Skeleton {
+    std::map<uint64_t, uint32_t> memo; // count -> subtree node count
+    std::map<uint64_t, int> dmemo;     // count -> subtree depth
+    uint32_t leaf;
+    int max_depth = 0;
+    std::vector<std::vector<LSeg>> levels;
+    std::vector<SSeg> small;
+
+    uint32_t nodes(uint64_t c) {
+        if (c <= leaf) return 1;
+        auto it = memo.find(c);
+        if (it != memo.end()) return it->second;
+        uint64_t m = (c / 2) / 8 * 8;
+        uint64_t r = 1 + (uint64_t)nodes(m) + nodes(c - m);
+        memo[c] = (uint32_t)r;
+        return (uint32_t)r;
+    }
+    int depth_of(uint64_t c) {
+        if (c <= leaf) return 0;
+        auto it = dmemo.find(c);
+        if (it != dmemo.end()) return it->second;
+        uint64_t m = (c / 2) / 8 * 8;
+        int d = 1 + std::max(depth_of(m), depth_of(c - m));
+        dmemo[c] = d;
+        return d;
+    }
+    void rec(uint32_t node, uint32_t left, uint32_t count, int depth) {
+        const uint32_t dim = depth % 3;
+        if (count <= SMALL || count <= leaf) {
+            small.push_back(SSeg{node, left, count, dim | ((uint32_t)(depth & 1) << 2)});
+            return;
+        }
+        uint32_t m = (count / 2) / 8 * 8;
+        uint32_t l = node + 1, r = node + 1 + nodes(m);
+        if ((int)levels.size() <= depth) levels.resize(depth + 1);
+        levels[depth].push_back(LSeg{node, left, count, m, l, r, 0, 0});
+        rec(l, left, m, depth + 1);
+        rec(r, left + m, count - m, depth + 1);
+    }
+};
+
+} // namespace
+
+nbkd_status build_tree(Tree &t, const float *xyz, uint64_t n, int32_t leaf_size, bool input_dev,
+                       hipStream_t s) {
+    const uint64_t n8 = (n + 7) / 8 * 8;
+    if (n8 > (uint64_t)UINT32_MAX) {
+        set_error("More than uint32_t points are not supported.");
+        return NBKD_ETOOMANY;
+    }
+    // leaf_size_ = max(leaf_size, 2 * block_size): size_t comparison, so a
+    // negative int becomes huge (kdtree_impl.hpp:485)
+    uint64_t leaf64 = leaf_size < 0 ? (uint64_t)(int64_t)leaf_size : (uint64_t)leaf_size;
+    leaf64 = std::max<uint64_t>(leaf64, 16);
+    const uint32_t leaf = (uint32_t)std::min<uint64_t>(leaf64, UINT32_MAX);
+
+    Skeleton sk;
+    sk.leaf = leaf;
+    t.n = n;
+    t.n8 = n8;
+    t.leaf = (int)std::min<uint64_t>(leaf, INT32_MAX);
+    t.nnodes = sk.nodes(n8);
+    t.depth = sk.depth_of(n8);
+
+    const size_t pbytes = (size_t)std::max<uint64_t>(n8, 1) * 4;
+    NBKD_HIP(hipMalloc(&t.x, pbytes));
+    NBKD_HIP(hipMalloc(&t.y, pbytes));
+    NBKD_HIP(hipMalloc(&t.z, pbytes));
+    NBKD_HIP(hipMalloc(&t.idx, pbytes));
+    NBKD_HIP(hipMalloc(&t.nodes, t.nnodes * sizeof(nbkd_node)));
+    Soa A{t.x, t.y, t.z, t.idx};
+
+    DevBuf bx, by, bz, bi, dev_in, bad;
+    NBKD_HIP(bx.alloc(pbytes, s));
+    NBKD_HIP(by.alloc(pbytes, s));
+    NBKD_HIP(bz.alloc(pbytes, s));
+    NBKD_HIP(bi.alloc(pbytes, s));
+    Soa B{bx.as<float>(), by.as<float>(), bz.as<float>(), bi.as<uint32_t>()};
+
+    const float *aos = xyz;
+    if (!input_dev && n > 0) {
+        NBKD_HIP(dev_in.alloc(n * 3 * sizeof(float), s));
+        NBKD_HIP(hipMemcpyAsync(dev_in.p, xyz, n * 3 * sizeof(float), hipMemcpyHostToDevice, s));
+        NBKD_HIP(hipStreamSynchronize(s));
+        aos = dev_in.as<float>();
+    }
+    NBKD_HIP(bad.alloc(sizeof(uint32_t), s));
+    NBKD_HIP(hipMemsetAsync(bad.p, 0, sizeof(uint32_t), s));
+    {
+        TimedScope ts("prepare", s);
+        uint64_t blocks = std::min<uint64_t>((n8 + TB - 1) / TB, 8192);
+        if (blocks == 0) blocks = 1;
+        prepare_kernel<<<(unsigned)blocks, TB, 0, s>>>(aos, n, n8, t.periodic, t.box, A,
+                                                        bad.as<uint32_t>());
+        NBKD_HIP(hipGetLastError());
+    }
+    if (t.periodic) {
+        uint32_t hbad = 0;
+        NBKD_HIP(hipMemcpyAsync(&hbad, bad.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+        NBKD_HIP(hipStreamSynchronize(s));
+        if (hbad) {
+            set_error("When using periodic boundary conditions, all points must be within the "
+                      "box (0 <= x <= box_size).");
+            return NBKD_EBOX;
+        }
+    }
+
+    // enumerate the shape down to SMALL-point segments
+    sk.rec(0, 0, (uint32_t)n8, 0);
+    std::vector<uint32_t> tab_c, tab_n;
+    for (auto &kv : sk.memo) {
+        tab_c.push_back((uint32_t)kv.first);
+        tab_n.push_back(kv.second);
+    }
+    if (tab_c.empty()) {
+        tab_c.push_back(0);
+        tab_n.push_back(1);
+    }
+
+    // flatten large levels and their tiles
+    std::vector<LSeg> segs;
+    std::vector<Tile> tiles;
+    struct LevelInfo {
+        uint32_t seg0, nseg, tile0, ntile;
+    };
+    std::vector<LevelInfo> info;
+    size_t max_seg = 0, max_tile = 0;
+    for (auto &lv : sk.levels) {
+        LevelInfo li{(uint32_t)segs.size(), (uint32_t)lv.size(), (uint32_t)tiles.size(), 0};
+        for (uint32_t si = 0; si < lv.size(); ++si) {
+            LSeg g = lv[si];
+            g.tile_begin = (uint32_t)tiles.size();
+            for (uint32_t b = 0; b < g.count; b += TILE)
+                tiles.push_back(Tile{si, b, std::min<uint32_t>(TILE, g.count - b), 0});
+            g.tile_end = (uint32_t)tiles.size();
+            segs.push_back(g);
+        }
+        li.ntile = (uint32_t)tiles.size() - li.tile0;
+        max_seg = std::max<size_t>(max_seg, li.nseg);
+        max_tile = std::max<size_t>(max_tile, li.ntile);
+        info.push_back(li);
+    }
+
+    DevBuf d_segs, d_tiles, d_st, d_hist, d_cnt, d_off, d_small, d_tabc, d_tabn;
+    if (!segs.empty()) {
+        NBKD_HIP(d_segs.alloc(segs.size() * sizeof(LSeg), s));
+        NBKD_HIP(d_tiles.alloc(tiles.size() * sizeof(Tile), s));
+        NBKD_HIP(d_st.alloc(max_seg * sizeof(SelState), s));
+        NBKD_HIP(d_hist.alloc(max_seg * 256 * sizeof(uint32_t), s));
+        NBKD_HIP(d_cnt.alloc(max_tile * sizeof(uint2), s));
+        NBKD_HIP(d_off.alloc(max_tile * sizeof(uint2), s));
+        NBKD_HIP(hipMemcpyAsync(d_segs.p, segs.data(), segs.size() * sizeof(LSeg),
+                                hipMemcpyHostToDevice, s));
+        NBKD_HIP(hipMemcpyAsync(d_tiles.p, tiles.data(), tiles.size() * sizeof(Tile),
+                                hipMemcpyHostToDevice, s));
+        NBKD_HIP(hipStreamSynchronize(s));
+    }
+    NBKD_HIP(d_small.alloc(sk.small.size() * sizeof(SSeg), s));
+    NBKD_HIP(hipMemcpyAsync(d_small.p, sk.small.data(), sk.small.size() * sizeof(SSeg),
+                            hipMemcpyHostToDevice, s));
+    NBKD_HIP(d_tabc.alloc(tab_c.size() * 4, s));
+    NBKD_HIP(d_tabn.alloc(tab_n.size() * 4, s));
+    NBKD_HIP(hipMemcpyAsync(d_tabc.p, tab_c.data(), tab_c.size() * 4, hipMemcpyHostToDevice, s));
+    NBKD_HIP(hipMemcpyAsync(d_tabn.p, tab_n.data(), tab_n.size() * 4, hipMemcpyHostToDevice, s));
+    NBKD_HIP(hipStreamSynchronize(s));
+
+    {
+        TimedScope ts("build_levels", s);
+        for (size_t d = 0; d < info.size(); ++d) {
+            const LevelInfo &li = info[d];
+            if (li.nseg == 0) continue;
+            const int dim = (int)(d % 3);
+            const Soa src = (d & 1) ? B : A;
+            const Soa dst = (d & 1) ? A : B;
+            const float *key = dim == 0 ? src.x : (dim == 1 ? src.y : src.z);
+            const LSeg *lsegs = d_segs.as<LSeg>() + li.seg0;
+            const Tile *ltiles = d_tiles.as<Tile>() + li.tile0;
+            SelState *st = d_st.as<SelState>();
+            uint32_t *hist = d_hist.as<uint32_t>();
+#define NBKD_PASS(P)                                                                               \
+    NBKD_HIP(hipMemsetAsync(hist, 0, (size_t)li.nseg * 256 * 4, s));                              \
+    hist_kernel<P><<<li.ntile, TB, 0, s>>>(ltiles, lsegs, st, key, hist);                         \
+    select_kernel<P><<<li.nseg, TB, 0, s>>>(lsegs, st, hist, t.nodes, dim);
+            NBKD_PASS(0)
+            NBKD_PASS(1)
+            NBKD_PASS(2)
+            NBKD_PASS(3)
+#undef NBKD_PASS
+            count_kernel<<<li.ntile, TB, 0, s>>>(ltiles, lsegs, st, key, d_cnt.as<uint2>());
+            scan_kernel<<<li.nseg, TB, 0, s>>>(lsegs, d_cnt.as<uint2>(), d_off.as<uint2>(),
+                                               li.tile0);
+            scatter_kernel<<<li.ntile, TB, 0, s>>>(ltiles, lsegs, st, d_off.as<uint2>(), dim,
+                                                   src, dst);
+            NBKD_HIP(hipGetLastError());
+        }
+    }
+    {
+        TimedScope ts("build_small", s);
+        if (!sk.small.empty()) {
+            NBKD_HIP(hipFuncSetAttribute((const void *)small_kernel,
+                                         hipFuncAttributeMaxDynamicSharedMemorySize,
+                                         (int)sizeof(SmallLds)));
+            small_kernel<<<(unsigned)sk.small.size(), TB, sizeof(SmallLds), s>>>(
+                d_small.as<SSeg>(), leaf, A, B, t.nodes, d_tabc.as<uint32_t>(),
+                d_tabn.as<uint32_t>(), (int)tab_c.size());
+            NBKD_HIP(hipGetLastError());
+        }
+    }
+    NBKD_HIP(hipStreamSynchronize(s));
+    return NBKD_OK;
+}
+
+} // namespace nbkd

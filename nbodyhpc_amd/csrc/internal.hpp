@@ -1,0 +1,131 @@
+// Internal declarations of libnbkd.so (MI355X / gfx950).  Not part of the ABI.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cfloat>
+#include <cstdint>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/nbkd.h"
+
+namespace nbkd {
+
+// Grow-only per-tree scratch for queries (one query at a time per tree:
+// Workspace::mu is held for the whole call).
+enum WsSlot {
+    WS_Q = 0, WS_KEYS, WS_KEYS2, WS_ORDER, WS_TMP, WS_HIST, WS_SUMS, WS_OUTD, WS_OUTI,
+    WS_COUNT, WS_OFF, WS_IDX, WS_STATS, WS_LIST, WS_LT, WS_NSLOTS
+};
+struct Workspace {
+    std::mutex mu;
+    void *p[WS_NSLOTS] = {};
+    size_t cap[WS_NSLOTS] = {};
+    // returns nullptr on failure (hip error recorded via set_error)
+    void *get(int slot, size_t bytes, hipStream_t s);
+    void release();
+};
+
+// Device-resident tree.  Points are SoA in tree order (the reference layout,
+// kdtree/src/cpp/include/kdtree/position_array.hpp:166-271): x, y, z, original
+// index; leaves are contiguous ranges.  Nodes are the reference's 16-B records.
+struct Tree {
+    int device = 0;
+    uint64_t n = 0;  // caller's point count
+    uint64_t n8 = 0; // padded to a multiple of 8
+    uint64_t nnodes = 0;
+    int periodic = 0;
+    float box = 0.0f;
+    int leaf = 16; // effective leaf size max(leaf_size, 16)
+    int depth = 0; // max node depth (root = 0)
+    float *x = nullptr, *y = nullptr, *z = nullptr;
+    uint32_t *idx = nullptr;
+    nbkd_node *nodes = nullptr;
+    mutable Workspace ws;
+};
+
+// plain-value view passed to kernels
+struct DevTree {
+    const float *__restrict__ x;
+    const float *__restrict__ y;
+    const float *__restrict__ z;
+    const uint32_t *__restrict__ idx;
+    const nbkd_node *__restrict__ nodes;
+    uint32_t n8;
+    uint32_t nnodes;
+    float box;
+};
+
+inline DevTree view(const Tree &t) {
+    return DevTree{t.x, t.y, t.z, t.idx, t.nodes, (uint32_t)t.n8, (uint32_t)t.nnodes, t.box};
+}
+
+// error plumbing (api.cpp)
+void set_error(const std::string &msg);
+nbkd_status hip_fail(hipError_t e, const char *what);
+
+#define NBKD_HIP(call)                                                                     \
+    do {                                                                                   \
+        hipError_t e_ = (call);                                                            \
+        if (e_ != hipSuccess) return ::nbkd::hip_fail(e_, #call);                          \
+    } while (0)
+
+// event timing (api.cpp)
+struct TimedScope {
+    TimedScope(const char *name, hipStream_t s);
+    ~TimedScope();
+    const char *name_;
+    hipStream_t s_;
+    hipEvent_t a_ = nullptr;
+};
+bool timing_enabled();
+bool stats_enabled();
+void stats_store(uint64_t nodes, uint64_t points);
+
+// RAII device allocation (plain hipMalloc; freed after the stream drained).
+// The stream-ordered pool (hipMallocAsync) is deliberately not used: mixing it
+// with hipMalloc'd tree storage and pageable copies produced corrupted inputs.
+struct DevBuf {
+    void *p = nullptr;
+    hipStream_t s = nullptr;
+    DevBuf() = default;
+    DevBuf(const DevBuf &) = delete;
+    DevBuf &operator=(const DevBuf &) = delete;
+    ~DevBuf() {
+        if (p) {
+            (void)hipStreamSynchronize(s);
+            (void)hipFree(p);
+        }
+    }
+    hipError_t alloc(size_t bytes, hipStream_t stream) {
+        s = stream;
+        return hipMalloc(&p, bytes ? bytes : 16);
+    }
+    template <typename T> T *as() const { return static_cast<T *>(p); }
+};
+
+// build.hip
+nbkd_status build_tree(Tree &t, const float *xyz, uint64_t n, int32_t leaf_size, bool input_dev,
+                       hipStream_t s);
+
+// query.hip
+nbkd_status query_knn(const Tree &t, const float *q, uint64_t m, int k, float *out_d,
+                      uint32_t *out_i, uint32_t flags, hipStream_t s);
+nbkd_status query_ball_count(const Tree &t, const float *q, uint64_t m, float r,
+                             uint32_t *out_count, uint32_t flags, hipStream_t s);
+nbkd_status query_ball_csr(const Tree &t, const float *q, uint64_t m, float r, uint64_t *offsets,
+                           uint32_t *out_idx, uint64_t capacity, uint32_t flags, hipStream_t s);
+
+// order-preserving float -> uint32 key (IEEE-754 total order of non-NaN values)
+__host__ __device__ inline uint32_t fkey(float f) {
+    uint32_t u = __builtin_bit_cast(uint32_t, f);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__host__ __device__ inline float fkey_inv(uint32_t k) {
+    uint32_t u = (k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k;
+    return __builtin_bit_cast(float, u);
+}
+
+} // namespace nbkd

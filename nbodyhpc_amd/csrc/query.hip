@@ -1,0 +1,979 @@
+// Batched kNN / radius queries for gfx950.
+//
+// Reference semantics (what the results must equal):
+//   traversal       KDTreeQuery::compute   kdtree/src/cpp/include/kdtree/kdtree_impl.hpp:620-662
+//   point metric    L2 / L2Periodic        kdtree/src/cpp/include/kdtree/kdtree.hpp:23-31, 72-84
+//   box metric      box_distance           kdtree/src/cpp/include/kdtree/kdtree.hpp:35-45, 89-107
+//   insertion       d2 < current k-th      kdtree/src/cpp/kdtree_asm_systemv.asm:148-188
+//   finalisation    sort by d2, sqrtf      kdtree/src/cpp/kdtree.cpp:149-156
+//
+// MI355X mapping ("packet traversal"):
+//   1. every query is bucketed by the leaf it falls in (one thread per query
+//      descends the tree), and the (leaf, query) pairs are radix-sorted, so
+//      consecutive queries are spatially adjacent in the kd order;
+//   2. one wave64 owns a PACKET of 64 consecutive queries, one per lane, and
+//      walks the tree ONCE for all of them: the stack (node id + 6-float box)
+//      lives in the wave's VGPRs, one entry per lane (v_writelane / v_readlane);
+//      a node is entered iff any lane's box distance <= its own k-th distance;
+//   3. a leaf's points are wave-uniform: their SoA coordinates come through the
+//      scalar cache (s_load), and every lane computes its own d2 against them;
+//   4. each lane keeps its top-k as a sorted register array (K_CAP = 8..64,
+//      with K_CAP-k -inf sentinels so the k-th is always element K_CAP-1) and
+//      appends candidates (d2 < k-th) to a per-lane LDS buffer of 16 slots; when
+//      any lane's buffer is full the wave merges: bitonic sort of the buffer +
+//      bitonic merge into the top-k.  No per-candidate divergence.
+//   d2 is evaluated exactly as the reference ((dx^2 + dy^2) + dz^2, periodic
+//   per-axis min of the three images; min of squares == square of the min |.|),
+//   compiled with -ffp-contract=off, so distances are bit-identical.
+#include <algorithm>
+
+#include "internal.hpp"
+
+namespace nbkd {
+namespace {
+
+constexpr int TB = 256;
+constexpr int WPB = TB / 64; // waves per block
+
+__device__ __forceinline__ uint32_t mbcnt64(uint64_t mask) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                     __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+
+__device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ float unif(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(uint32_t, v)));
+}
+
+// ------------------------------------------------------------------ metrics
+template <bool PER>
+__device__ __forceinline__ float point_d2(float qx, float qy, float qz, float px, float py, float pz,
+                                          float L) {
+    float dx = px - qx, dy = py - qy, dz = pz - qz;
+    if constexpr (PER) {
+        // min(d^2, (d-L)^2, (d+L)^2) == (min(|d|, |d-L|, |d+L|))^2 exactly
+        dx = fminf(fminf(fabsf(dx), fabsf(dx - L)), fabsf(dx + L));
+        dy = fminf(fminf(fabsf(dy), fabsf(dy - L)), fabsf(dy + L));
+        dz = fminf(fminf(fabsf(dz), fabsf(dz - L)), fabsf(dz + L));
+    }
+    float a = dx * dx, b = dy * dy, c = dz * dz;
+    return (a + b) + c;
+}
+
+template <bool PER>
+__device__ __forceinline__ float box_axis(float p, float lo, float hi, float L) {
+    if constexpr (PER) {
+        // kdtree.hpp:93-103
+        float below = fminf(lo - p, (p + L) - hi);
+        float above = fminf(p - hi, (lo + L) - p);
+        float m = p < lo ? below : (p > hi ? above : 0.0f);
+        return m * m;
+    } else {
+        // kdtree.hpp:39-41
+        float dl = fmaxf(lo - p, 0.0f), dr = fmaxf(p - hi, 0.0f);
+        float a = dl * dl, b = dr * dr;
+        return a + b;
+    }
+}
+
+template <bool PER>
+__device__ __forceinline__ float box_d2(float qx, float qy, float qz, const float b[6], float L) {
+    float r = box_axis<PER>(qx, b[0], b[1], L);
+    r += box_axis<PER>(qy, b[2], b[3], L);
+    r += box_axis<PER>(qz, b[4], b[5], L);
+    return r;
+}
+
+// ------------------------------------------------------------------ register sorting networks
+template <int N>
+__device__ __forceinline__ void ce(float (&d)[N], uint32_t (&i)[N], int a, int b) {
+    // ascending: d[a] <= d[b]
+    float da = d[a], db = d[b];
+    bool sw = db < da;
+    d[a] = sw ? db : da;
+    d[b] = sw ? da : db;
+    uint32_t ia = i[a], ib = i[b];
+    i[a] = sw ? ib : ia;
+    i[b] = sw ? ia : ib;
+}
+
+template <int N>
+__device__ __forceinline__ void bitonic_sort(float (&d)[N], uint32_t (&i)[N]) {
+#pragma unroll
+    for (int size = 2; size <= N; size <<= 1) {
+#pragma unroll
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+#pragma unroll
+            for (int a = 0; a < N; ++a) {
+                int b = a ^ stride;
+                if (b > a) {
+                    if ((a & size) == 0)
+                        ce<N>(d, i, a, b);
+                    else
+                        ce<N>(d, i, b, a);
+                }
+            }
+        }
+    }
+}
+
+template <int N>
+__device__ __forceinline__ void bitonic_merge(float (&d)[N], uint32_t (&i)[N]) {
+#pragma unroll
+    for (int stride = N >> 1; stride > 0; stride >>= 1) {
+#pragma unroll
+        for (int a = 0; a < N; ++a) {
+            int b = a ^ stride;
+            if (b > a) ce<N>(d, i, a, b);
+        }
+    }
+}
+
+// ------------------------------------------------------------------ query bucketing
+__global__ void __launch_bounds__(TB)
+leaf_key_kernel(DevTree t, const float *__restrict__ q, uint32_t m, uint32_t *__restrict__ keys,
+                uint32_t *__restrict__ vals) {
+    uint32_t i = blockIdx.x * TB + threadIdx.x;
+    if (i >= m) return;
+    float p[3] = {q[3 * (size_t)i], q[3 * (size_t)i + 1], q[3 * (size_t)i + 2]};
+    uint32_t node = 0;
+    nbkd_node nd = t.nodes[0];
+    while (nd.dimension >= 0) {
+        float v = p[nd.dimension];
+        node = v > nd.split ? nd.right : nd.left; // near child, kdtree_impl.hpp:633
+        nd = t.nodes[node];
+    }
+    keys[i] = nd.left >> 3;
+    vals[i] = i;
+}
+
+// ------------------------------------------------------------------ LSD radix sort (keys + values)
+constexpr int RS_ITEMS = 8;
+constexpr int RS_TILE = TB * RS_ITEMS; // 2048
+
+__global__ void __launch_bounds__(TB)
+rs_hist_kernel(const uint32_t *__restrict__ keys, uint32_t n, int shift, uint32_t ntiles,
+               uint32_t *__restrict__ hist) {
+    __shared__ uint32_t h[256];
+    h[threadIdx.x] = 0;
+    __syncthreads();
+    const uint32_t base = blockIdx.x * RS_TILE;
+#pragma unroll
+    for (int r = 0; r < RS_ITEMS; ++r) {
+        uint32_t e = base + r * TB + threadIdx.x;
+        if (e < n) atomicAdd(&h[(keys[e] >> shift) & 255u], 1u);
+    }
+    __syncthreads();
+    hist[(size_t)threadIdx.x * ntiles + blockIdx.x] = h[threadIdx.x];
+}
+
+__global__ void __launch_bounds__(TB)
+rs_scatter_kernel(const uint32_t *__restrict__ kin, const uint32_t *__restrict__ vin, uint32_t n,
+                  int shift, uint32_t ntiles, const uint32_t *__restrict__ hist_scanned,
+                  uint32_t *__restrict__ kout, uint32_t *__restrict__ vout) {
+    __shared__ uint16_t cnt[RS_ITEMS][WPB][256];
+    __shared__ uint32_t gofs[256];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (int j = threadIdx.x; j < RS_ITEMS * WPB * 256; j += TB) (&cnt[0][0][0])[j] = 0;
+    gofs[threadIdx.x] = hist_scanned[(size_t)threadIdx.x * ntiles + blockIdx.x];
+    __syncthreads();
+    const uint32_t base = blockIdx.x * RS_TILE;
+    uint32_t kk[RS_ITEMS], vv[RS_ITEMS], rk[RS_ITEMS];
+#pragma unroll
+    for (int r = 0; r < RS_ITEMS; ++r) {
+        uint32_t e = base + r * TB + threadIdx.x;
+        bool valid = e < n;
+        kk[r] = valid ? kin[e] : 0u;
+        vv[r] = valid ? vin[e] : 0u;
+        uint32_t d = (kk[r] >> shift) & 255u;
+        uint64_t same = __ballot(valid);
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+            uint64_t bb = __ballot((d >> b) & 1u);
+            same &= ((d >> b) & 1u) ? bb : ~bb;
+        }
+        uint32_t below = mbcnt64(same);
+        rk[r] = below;
+        if (valid && below == 0) cnt[r][wave][d] = (uint16_t)__popcll(same);
+    }
+    __syncthreads();
+    { // per digit: exclusive prefix over (round, wave) in element order
+        uint32_t acc = 0;
+        const int d = threadIdx.x;
+        for (int r = 0; r < RS_ITEMS; ++r)
+            for (int w = 0; w < WPB; ++w) {
+                uint32_t v = cnt[r][w][d];
+                cnt[r][w][d] = (uint16_t)acc;
+                acc += v;
+            }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < RS_ITEMS; ++r) {
+        uint32_t e = base + r * TB + threadIdx.x;
+        if (e < n) {
+            uint32_t d = (kk[r] >> shift) & 255u;
+            uint32_t dst = gofs[d] + cnt[r][wave][d] + rk[r];
+            kout[dst] = kk[r];
+            vout[dst] = vv[r];
+        }
+    }
+    (void)lane;
+}
+
+// exclusive scan of a uint32 array, 3 kernels
+constexpr int SC_ITEMS = 16;
+constexpr int SC_TILE = TB * SC_ITEMS;
+
+__device__ __forceinline__ uint32_t block_scan_excl(uint32_t v, uint32_t *sh, uint32_t *total) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int nw = blockDim.x / 64;
+    uint32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) sh[wave] = x;
+    __syncthreads();
+    uint32_t base = 0, tot = 0;
+    for (int w = 0; w < nw; ++w) {
+        uint32_t s = sh[w];
+        if (w < wave) base += s;
+        tot += s;
+    }
+    if (total) *total = tot;
+    __syncthreads();
+    return base + x - v;
+}
+
+__global__ void __launch_bounds__(TB)
+scan_up_kernel(const uint32_t *__restrict__ a, uint64_t n, uint32_t *__restrict__ sums) {
+    __shared__ uint32_t sh[WPB];
+    const uint64_t base = (uint64_t)blockIdx.x * SC_TILE + (uint64_t)threadIdx.x * SC_ITEMS;
+    uint32_t s = 0;
+#pragma unroll
+    for (int j = 0; j < SC_ITEMS; ++j)
+        if (base + j < n) s += a[base + j];
+    uint32_t tot;
+    block_scan_excl(s, sh, &tot);
+    if (threadIdx.x == 0) sums[blockIdx.x] = tot;
+}
+
+__global__ void __launch_bounds__(1024) scan_mid_kernel(uint32_t *__restrict__ sums, uint32_t nb) {
+    __shared__ uint32_t sh[16];
+    const uint32_t per = (nb + 1023) / 1024;
+    const uint32_t b0 = threadIdx.x * per, b1 = min(b0 + per, nb);
+    uint32_t s = 0;
+    for (uint32_t b = b0; b < b1; ++b) s += sums[b];
+    uint32_t ex = block_scan_excl(s, sh, nullptr);
+    for (uint32_t b = b0; b < b1; ++b) {
+        uint32_t v = sums[b];
+        sums[b] = ex;
+        ex += v;
+    }
+}
+
+__global__ void __launch_bounds__(TB)
+scan_down_kernel(uint32_t *__restrict__ a, uint64_t n, const uint32_t *__restrict__ sums) {
+    __shared__ uint32_t sh[WPB];
+    const uint64_t base = (uint64_t)blockIdx.x * SC_TILE + (uint64_t)threadIdx.x * SC_ITEMS;
+    uint32_t v[SC_ITEMS], s = 0;
+#pragma unroll
+    for (int j = 0; j < SC_ITEMS; ++j) {
+        v[j] = base + j < n ? a[base + j] : 0u;
+        s += v[j];
+    }
+    uint32_t ex = block_scan_excl(s, sh, nullptr) + sums[blockIdx.x];
+#pragma unroll
+    for (int j = 0; j < SC_ITEMS; ++j) {
+        if (base + j < n) a[base + j] = ex;
+        ex += v[j];
+    }
+}
+
+nbkd_status device_excl_scan(Workspace &ws, uint32_t *a, uint64_t n, hipStream_t s) {
+    if (n == 0) return NBKD_OK;
+    uint64_t nb = (n + SC_TILE - 1) / SC_TILE;
+    uint32_t *sums = (uint32_t *)ws.get(WS_SUMS, nb * 4, s);
+    if (!sums) return NBKD_ENOMEM;
+    scan_up_kernel<<<(unsigned)nb, TB, 0, s>>>(a, n, sums);
+    scan_mid_kernel<<<1, 1024, 0, s>>>(sums, (uint32_t)nb);
+    scan_down_kernel<<<(unsigned)nb, TB, 0, s>>>(a, n, sums);
+    NBKD_HIP(hipGetLastError());
+    return NBKD_OK;
+}
+
+// sorts (keys, vals) by the low `nbits` of keys; result in (k0, v0)
+nbkd_status radix_sort(Workspace &ws, uint32_t *k0, uint32_t *v0, uint32_t *k1, uint32_t *v1,
+                       uint32_t n, int nbits, hipStream_t s) {
+    if (n <= 1) return NBKD_OK;
+    const uint32_t ntiles = (n + RS_TILE - 1) / RS_TILE;
+    uint32_t *hist = (uint32_t *)ws.get(WS_HIST, (size_t)256 * ntiles * 4, s);
+    if (!hist) return NBKD_ENOMEM;
+    int passes = (nbits + 7) / 8;
+    if (passes & 1) ++passes; // even number of passes: the result lands back in (k0, v0)
+    for (int p = 0; p < passes; ++p) {
+        const int shift = 8 * p;
+        uint32_t *ki = (p & 1) ? k1 : k0, *vi = (p & 1) ? v1 : v0;
+        uint32_t *ko = (p & 1) ? k0 : k1, *vo = (p & 1) ? v0 : v1;
+        rs_hist_kernel<<<ntiles, TB, 0, s>>>(ki, n, shift, ntiles, hist);
+        nbkd_status st = device_excl_scan(ws, hist, (uint64_t)256 * ntiles, s);
+        if (st) return st;
+        rs_scatter_kernel<<<ntiles, TB, 0, s>>>(ki, vi, n, shift, ntiles, hist, ko, vo);
+        NBKD_HIP(hipGetLastError());
+    }
+    return NBKD_OK;
+}
+
+// ------------------------------------------------------------------ packet traversal
+constexpr int STACK = 64; // one entry per lane
+
+struct WaveStack {
+    uint32_t node;
+    float b0, b1, b2, b3, b4, b5;
+};
+
+// push: the lane whose id equals the stack pointer takes the entry
+#define NBKD_PUSH(SP, NODE, BX)                                                                    \
+    do {                                                                                           \
+        const bool me_ = lane == (SP);                                                             \
+        stk.node = me_ ? (NODE) : stk.node;                                                        \
+        stk.b0 = me_ ? (BX)[0] : stk.b0;                                                           \
+        stk.b1 = me_ ? (BX)[1] : stk.b1;                                                           \
+        stk.b2 = me_ ? (BX)[2] : stk.b2;                                                           \
+        stk.b3 = me_ ? (BX)[3] : stk.b3;                                                           \
+        stk.b4 = me_ ? (BX)[4] : stk.b4;                                                           \
+        stk.b5 = me_ ? (BX)[5] : stk.b5;                                                           \
+        ++(SP);                                                                                    \
+    } while (0)
+
+__device__ __forceinline__ float rdlane(float v, int l) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(uint32_t, v), l));
+}
+
+template <int KC, bool PER>
+__global__ void __launch_bounds__(TB)
+knn_kernel(DevTree t, const float *__restrict__ q, const uint32_t *__restrict__ order, uint32_t m,
+           int k, float *__restrict__ out_d, uint32_t *__restrict__ out_i,
+           unsigned long long *__restrict__ stats) {
+    constexpr int CAP = KC < 16 ? KC : 16;
+    __shared__ float s_bd[WPB][CAP][64];
+    __shared__ uint32_t s_bi[WPB][CAP][64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t gq = (blockIdx.x * WPB + wave) * 64u + lane;
+    const bool valid = gq < m;
+    const uint32_t qo = valid ? order[gq] : 0u;
+    const float qx = valid ? q[3 * (size_t)qo] : 0.0f;
+    const float qy = valid ? q[3 * (size_t)qo + 1] : 0.0f;
+    const float qz = valid ? q[3 * (size_t)qo + 2] : 0.0f;
+    const float L = t.box;
+    const uint32_t nvalid = (uint32_t)__popcll(__ballot(valid));
+
+    float td[KC];
+    uint32_t ti[KC];
+#pragma unroll
+    for (int j = 0; j < KC; ++j) {
+        td[j] = (j < KC - k) ? -INFINITY : FLT_MAX;
+        ti[j] = 0xFFFFFFFFu;
+    }
+    float kth = valid ? FLT_MAX : -INFINITY;
+    uint32_t cnt = 0;
+    float *bd_col = &s_bd[wave][0][lane];
+    uint32_t *bi_col = &s_bi[wave][0][lane];
+
+    auto merge = [&]() {
+        float bd[CAP];
+        uint32_t bi[CAP];
+#pragma unroll
+        for (int s = 0; s < CAP; ++s) {
+            float dv = bd_col[s * 64];
+            uint32_t iv = bi_col[s * 64];
+            bool have = (uint32_t)s < cnt;
+            bd[s] = have ? dv : INFINITY;
+            bi[s] = have ? iv : 0xFFFFFFFFu;
+        }
+        bitonic_sort<CAP>(bd, bi);
+#pragma unroll
+        for (int s = 0; s < CAP; ++s) {
+            const int pos = KC - CAP + s, o = CAP - 1 - s;
+            bool take = bd[o] < td[pos];
+            td[pos] = take ? bd[o] : td[pos];
+            ti[pos] = take ? bi[o] : ti[pos];
+        }
+        bitonic_merge<KC>(td, ti);
+        if (valid) kth = td[KC - 1];
+        cnt = 0;
+    };
+
+    uint64_t n_nodes = 0, n_pts = 0;
+    WaveStack stk;
+    stk.node = 0;
+    stk.b0 = stk.b1 = stk.b2 = stk.b3 = stk.b4 = stk.b5 = 0.0f;
+    int sp = 0;
+    {
+        float box[6];
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            box[2 * a] = PER ? 0.0f : -FLT_MAX;
+            box[2 * a + 1] = PER ? L : FLT_MAX;
+        }
+        NBKD_PUSH(sp, 0u, box);
+    }
+    while (sp > 0) {
+        --sp;
+        const uint32_t node = __builtin_amdgcn_readlane(stk.node, sp);
+        float box[6] = {rdlane(stk.b0, sp), rdlane(stk.b1, sp), rdlane(stk.b2, sp),
+                        rdlane(stk.b3, sp), rdlane(stk.b4, sp), rdlane(stk.b5, sp)};
+        const float bdist = box_d2<PER>(qx, qy, qz, box, L);
+        if (!__any(bdist <= kth)) continue;
+        ++n_nodes;
+        const nbkd_node nd = t.nodes[node];
+        const int dim = (int)uni((uint32_t)nd.dimension);
+        if (dim < 0) {
+            const uint32_t b = uni(nd.left), e = uni(nd.right);
+            n_pts += e - b;
+            for (uint32_t j = b; j < e; j += 8) {
+                float px[8], py[8], pz[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    px[u] = t.x[j + u];
+                    py[u] = t.y[j + u];
+                    pz[u] = t.z[j + u];
+                }
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const float d = point_d2<PER>(qx, qy, qz, px[u], py[u], pz[u], L);
+                    if (d < kth) {
+                        bd_col[cnt * 64] = d;
+                        bi_col[cnt * 64] = j + u;
+                        ++cnt;
+                    }
+                    if (__any(cnt == CAP)) merge();
+                }
+            }
+            continue;
+        }
+        const float split = unif(nd.split);
+        const uint32_t lchild = uni(nd.left), rchild = uni(nd.right);
+        const float qd = dim == 0 ? qx : (dim == 1 ? qy : qz);
+        const uint32_t right_votes = (uint32_t)__popcll(__ballot(valid && qd > split));
+        const bool right_first = 2 * right_votes > nvalid;
+        float lbox[6], rbox[6];
+#pragma unroll
+        for (int a = 0; a < 6; ++a) {
+            lbox[a] = box[a];
+            rbox[a] = box[a];
+        }
+        // left child: hi[dim] = split; right child: lo[dim] = split
+        if (dim == 0) {
+            lbox[1] = split;
+            rbox[0] = split;
+        } else if (dim == 1) {
+            lbox[3] = split;
+            rbox[2] = split;
+        } else {
+            lbox[5] = split;
+            rbox[4] = split;
+        }
+        if (right_first) {
+            NBKD_PUSH(sp, lchild, lbox);
+            NBKD_PUSH(sp, rchild, rbox);
+        } else {
+            NBKD_PUSH(sp, rchild, rbox);
+            NBKD_PUSH(sp, lchild, lbox);
+        }
+    }
+    if (__any(cnt > 0)) merge();
+
+    if (valid) {
+        const int skip = KC - k;
+        const size_t row = (size_t)qo * (size_t)k;
+#pragma unroll
+        for (int j = 0; j < KC; ++j) {
+            if (j >= skip) {
+                out_d[row + (j - skip)] = sqrtf(td[j]);
+                const uint32_t p = ti[j];
+                out_i[row + (j - skip)] = p == 0xFFFFFFFFu ? p : t.idx[p];
+            }
+        }
+    }
+    if (stats && lane == 0) {
+        atomicAdd(&stats[0], (unsigned long long)n_nodes * nvalid);
+        atomicAdd(&stats[1], (unsigned long long)n_pts * nvalid);
+    }
+}
+
+// radius count: same packet traversal, fixed threshold r2
+template <bool PER>
+__global__ void __launch_bounds__(TB)
+ball_count_kernel(DevTree t, const float *__restrict__ q, const uint32_t *__restrict__ order,
+                  uint32_t m, float r2, uint32_t *__restrict__ out_count,
+                  uint64_t *__restrict__ row_offsets, uint32_t *__restrict__ out_idx) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t gq = (blockIdx.x * WPB + wave) * 64u + lane;
+    const bool valid = gq < m;
+    const uint32_t qo = valid ? order[gq] : 0u;
+    const float qx = valid ? q[3 * (size_t)qo] : 0.0f;
+    const float qy = valid ? q[3 * (size_t)qo + 1] : 0.0f;
+    const float qz = valid ? q[3 * (size_t)qo + 2] : 0.0f;
+    const float L = t.box;
+    const float thr = valid ? r2 : -INFINITY;
+    uint64_t wpos = (out_idx && valid) ? row_offsets[qo] : 0;
+    uint32_t cnt = 0;
+    WaveStack stk;
+    stk.node = 0;
+    stk.b0 = stk.b1 = stk.b2 = stk.b3 = stk.b4 = stk.b5 = 0.0f;
+    int sp = 0;
+    {
+        float box[6];
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            box[2 * a] = PER ? 0.0f : -FLT_MAX;
+            box[2 * a + 1] = PER ? L : FLT_MAX;
+        }
+        NBKD_PUSH(sp, 0u, box);
+    }
+    while (sp > 0) {
+        --sp;
+        const uint32_t node = __builtin_amdgcn_readlane(stk.node, sp);
+        float box[6] = {rdlane(stk.b0, sp), rdlane(stk.b1, sp), rdlane(stk.b2, sp),
+                        rdlane(stk.b3, sp), rdlane(stk.b4, sp), rdlane(stk.b5, sp)};
+        const float bdist = box_d2<PER>(qx, qy, qz, box, L);
+        if (!__any(bdist <= thr)) continue;
+        const nbkd_node nd = t.nodes[node];
+        const int dim = (int)uni((uint32_t)nd.dimension);
+        if (dim < 0) {
+            const uint32_t b = uni(nd.left), e = uni(nd.right);
+            for (uint32_t j = b; j < e; j += 8) {
+                float px[8], py[8], pz[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    px[u] = t.x[j + u];
+                    py[u] = t.y[j + u];
+                    pz[u] = t.z[j + u];
+                }
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const float d = point_d2<PER>(qx, qy, qz, px[u], py[u], pz[u], L);
+                    const bool in = d <= thr;
+                    if (out_idx && in) out_idx[wpos + cnt] = t.idx[j + u];
+                    cnt += in;
+                }
+            }
+            continue;
+        }
+        const float split = unif(nd.split);
+        const uint32_t lchild = uni(nd.left), rchild = uni(nd.right);
+        float lbox[6], rbox[6];
+#pragma unroll
+        for (int a = 0; a < 6; ++a) {
+            lbox[a] = box[a];
+            rbox[a] = box[a];
+        }
+        if (dim == 0) {
+            lbox[1] = split;
+            rbox[0] = split;
+        } else if (dim == 1) {
+            lbox[3] = split;
+            rbox[2] = split;
+        } else {
+            lbox[5] = split;
+            rbox[4] = split;
+        }
+        NBKD_PUSH(sp, rchild, rbox);
+        NBKD_PUSH(sp, lchild, lbox);
+    }
+    if (valid && out_count) out_count[qo] = cnt;
+}
+
+// ------------------------------------------------------------------ reference-exact traversal
+// One lane per query, replaying KDTreeQuery::compute (kdtree_impl.hpp:620-662)
+// step for step: near child first (left unless q[dim] > split), near visited iff
+// box_d2 < k-th, far skipped iff k-th < box_d2 (checked after the near subtree),
+// leaf points inserted iff d2 < k-th into the reference's loser tree
+// (tournament_tree.hpp:18-105), then sorted by d2 and sqrt'd.  Used where the
+// packet traversal's result could differ from the reference's:
+//   * periodic queries outside [0, L]^3: the reference does not validate
+//     queries (pybind.cpp:90-98) and its periodic box distance is then not a
+//     lower bound, so its pruning can drop true neighbours; this replays it;
+//   * k > 64 (beyond the register top-k of the packet kernel).
+struct LtEntry {
+    float d;
+    uint32_t id;
+    uint32_t slot;
+    uint32_t win; // scratch for the initial winners
+};
+
+__device__ __forceinline__ void lt_init(LtEntry *lt, uint32_t n) {
+    for (uint32_t i = 0; i < 2 * n; ++i) {
+        lt[i].d = FLT_MAX;
+        lt[i].id = 0xFFFFFFFFu;
+    }
+    for (uint32_t i = 0; i < n; ++i) lt[i + n].win = i;
+    for (uint32_t i = n - 1; i > 0; --i) {
+        uint32_t a = lt[2 * i].win, b = lt[2 * i + 1].win;
+        lt[i].win = a > b ? a : b;
+        lt[i].slot = (a < b ? a : b) + n;
+    }
+    for (uint32_t i = n; i < 2 * n; ++i) lt[i].slot = i;
+    lt[0].slot = 2 * n - 1;
+}
+
+__device__ __forceinline__ void lt_replace_top(LtEntry *lt, float d, uint32_t id) {
+    const uint32_t s = lt[0].slot;
+    float wd = d;
+    uint32_t wid = id, wslot = s;
+    lt[s].d = d;
+    lt[s].id = id;
+    lt[s].slot = s;
+    uint32_t i = s;
+    while (i > 1) {
+        i >>= 1;
+        const float od = lt[i].d;
+        if (wd < od) {
+            const uint32_t oid = lt[i].id, oslot = lt[i].slot;
+            lt[i].d = wd;
+            lt[i].id = wid;
+            lt[i].slot = wslot;
+            wd = od;
+            wid = oid;
+            wslot = oslot;
+        }
+    }
+    lt[0].d = wd;
+    lt[0].id = wid;
+    lt[0].slot = wslot;
+}
+
+template <bool PER>
+__global__ void __launch_bounds__(TB)
+knn_exact_kernel(DevTree t, const float *__restrict__ q, const uint32_t *__restrict__ list,
+                 const uint32_t *__restrict__ list_count, uint32_t m_all, int k,
+                 LtEntry *__restrict__ scratch, float *__restrict__ out_d,
+                 uint32_t *__restrict__ out_i) {
+    const uint32_t tid = blockIdx.x * TB + threadIdx.x;
+    const uint32_t nthreads = gridDim.x * TB;
+    const uint32_t count = list_count ? *list_count : m_all;
+    const float L = t.box;
+    LtEntry *lt = scratch + (size_t)tid * 2 * (size_t)k;
+    for (uint32_t w = tid; w < count; w += nthreads) {
+        const uint32_t qi = list ? list[w] : w;
+        const float qv[3] = {q[3 * (size_t)qi], q[3 * (size_t)qi + 1], q[3 * (size_t)qi + 2]};
+        lt_init(lt, (uint32_t)k);
+        uint32_t stk_node[64];
+        float stk_box[64][6];
+        int sp = 0;
+        float box[6];
+        for (int a = 0; a < 3; ++a) {
+            box[2 * a] = PER ? 0.0f : -FLT_MAX;
+            box[2 * a + 1] = PER ? L : FLT_MAX;
+        }
+        uint32_t node = 0;
+        for (;;) {
+            const nbkd_node nd = t.nodes[node];
+            bool descend = false;
+            if (nd.dimension < 0) {
+                float top = lt[0].d;
+                for (uint32_t j = nd.left; j < nd.right; ++j) {
+                    const float d = point_d2<PER>(qv[0], qv[1], qv[2], t.x[j], t.y[j], t.z[j], L);
+                    if (d < top) {
+                        lt_replace_top(lt, d, j);
+                        top = lt[0].d;
+                    }
+                }
+            } else {
+                const int dim = nd.dimension;
+                const bool right_near = qv[dim] > nd.split;
+                float nb[6], fb[6];
+                for (int a = 0; a < 6; ++a) {
+                    nb[a] = box[a];
+                    fb[a] = box[a];
+                }
+                nb[right_near ? 2 * dim : 2 * dim + 1] = nd.split;
+                fb[right_near ? 2 * dim + 1 : 2 * dim] = nd.split;
+                stk_node[sp] = right_near ? nd.left : nd.right;
+                for (int a = 0; a < 6; ++a) stk_box[sp][a] = fb[a];
+                ++sp;
+                if (box_d2<PER>(qv[0], qv[1], qv[2], nb, L) < lt[0].d) {
+                    node = right_near ? nd.right : nd.left;
+                    for (int a = 0; a < 6; ++a) box[a] = nb[a];
+                    descend = true;
+                }
+            }
+            if (descend) continue;
+            // pop deferred far children: skip iff kth < box_d2
+            bool found = false;
+            while (sp > 0) {
+                --sp;
+                const float bd = box_d2<PER>(qv[0], qv[1], qv[2], stk_box[sp], L);
+                if (lt[0].d < bd) continue;
+                node = stk_node[sp];
+                for (int a = 0; a < 6; ++a) box[a] = stk_box[sp][a];
+                found = true;
+                break;
+            }
+            if (!found) break;
+        }
+        // copy_values + sort by d2 (stable) + sqrt, kdtree.cpp:149-156
+        LtEntry *res = lt + k;
+        for (int i = 1; i < k; ++i) {
+            const LtEntry v = res[i];
+            int j = i;
+            while (j > 0 && v.d < res[j - 1].d) {
+                res[j] = res[j - 1];
+                --j;
+            }
+            res[j] = v;
+        }
+        const size_t row = (size_t)qi * (size_t)k;
+        for (int j = 0; j < k; ++j) {
+            out_d[row + j] = sqrtf(res[j].d);
+            const uint32_t p = res[j].id;
+            out_i[row + j] = p == 0xFFFFFFFFu ? p : t.idx[p];
+        }
+    }
+}
+
+// periodic queries outside [0, L]^3 -> list (order irrelevant: rows are independent)
+__global__ void __launch_bounds__(TB)
+outside_box_kernel(const float *__restrict__ q, uint32_t m, float L, uint32_t *__restrict__ list,
+                   uint32_t *__restrict__ count) {
+    const uint32_t i = blockIdx.x * TB + threadIdx.x;
+    if (i >= m) return;
+    const float x = q[3 * (size_t)i], y = q[3 * (size_t)i + 1], z = q[3 * (size_t)i + 2];
+    const bool inside = x >= 0.0f && x <= L && y >= 0.0f && y <= L && z >= 0.0f && z <= L;
+    if (!inside) list[atomicAdd(count, 1u)] = i;
+}
+
+template <int KC>
+void launch_knn(const Tree &t, const float *q, const uint32_t *order, uint32_t m, int k,
+                float *od, uint32_t *oi, unsigned long long *stats, hipStream_t s) {
+    const unsigned blocks = (m + TB - 1) / TB;
+    if (t.periodic)
+        knn_kernel<KC, true><<<blocks, TB, 0, s>>>(view(t), q, order, m, k, od, oi, stats);
+    else
+        knn_kernel<KC, false><<<blocks, TB, 0, s>>>(view(t), q, order, m, k, od, oi, stats);
+}
+
+int key_bits(const Tree &t) {
+    uint64_t maxkey = t.n8 >> 3;
+    int b = 1;
+    while (b < 32 && (1ull << b) <= maxkey) ++b;
+    return b;
+}
+
+// bucket + sort queries by leaf: order[] = query ids in kd order
+// order[] (workspace slot WS_ORDER) = query ids sorted by leaf
+nbkd_status sort_queries(const Tree &t, const float *dq, uint32_t m, uint32_t *&order,
+                         hipStream_t s) {
+    Workspace &ws = t.ws;
+    order = (uint32_t *)ws.get(WS_ORDER, (size_t)m * 4, s);
+    uint32_t *tmp = (uint32_t *)ws.get(WS_TMP, (size_t)m * 4, s);
+    uint32_t *keys = (uint32_t *)ws.get(WS_KEYS, (size_t)m * 4, s);
+    uint32_t *keys2 = (uint32_t *)ws.get(WS_KEYS2, (size_t)m * 4, s);
+    if (!order || !tmp || !keys || !keys2) return NBKD_ENOMEM;
+    {
+        TimedScope ts("leaf_key", s);
+        leaf_key_kernel<<<(m + TB - 1) / TB, TB, 0, s>>>(view(t), dq, m, keys, order);
+        NBKD_HIP(hipGetLastError());
+    }
+    TimedScope ts("sort", s);
+    return radix_sort(ws, keys, order, keys2, tmp, m, key_bits(t), s);
+}
+
+nbkd_status stage_queries(const Tree &t, const float *q, uint64_t m, uint32_t flags,
+                          const float *&dq, hipStream_t s) {
+    if (flags & NBKD_INPUT_DEVICE) {
+        dq = q;
+        return NBKD_OK;
+    }
+    float *buf = (float *)t.ws.get(WS_Q, m * 3 * sizeof(float), s);
+    if (!buf) return NBKD_ENOMEM;
+    NBKD_HIP(hipMemcpyAsync(buf, q, m * 3 * sizeof(float), hipMemcpyHostToDevice, s));
+    NBKD_HIP(hipStreamSynchronize(s));
+    dq = buf;
+    return NBKD_OK;
+}
+
+} // namespace
+
+nbkd_status query_knn(const Tree &t, const float *q, uint64_t m, int k, float *out_d,
+                      uint32_t *out_i, uint32_t flags, hipStream_t s) {
+    if (k <= 0) {
+        set_error("k must be positive integer");
+        return NBKD_EINVAL;
+    }
+    if (m == 0) return NBKD_OK;
+    if (m >= (1ull << 32)) {
+        set_error("more than 2^32 - 1 queries per call are not supported");
+        return NBKD_EINVAL;
+    }
+    const uint32_t mm = (uint32_t)m;
+    std::lock_guard<std::mutex> lk(t.ws.mu);
+    const float *dq = nullptr;
+    nbkd_status rc = stage_queries(t, q, m, flags, dq, s);
+    if (rc) return rc;
+    uint32_t *ord = nullptr;
+    rc = sort_queries(t, dq, mm, ord, s);
+    if (rc) return rc;
+    float *dd = out_d;
+    uint32_t *di = out_i;
+    if (!(flags & NBKD_OUTPUT_DEVICE)) {
+        dd = (float *)t.ws.get(WS_OUTD, m * (size_t)k * 4, s);
+        di = (uint32_t *)t.ws.get(WS_OUTI, m * (size_t)k * 4, s);
+        if (!dd || !di) return NBKD_ENOMEM;
+    }
+    unsigned long long *stats = nullptr;
+    if (stats_enabled()) {
+        stats = (unsigned long long *)t.ws.get(WS_STATS, 16, s);
+        if (!stats) return NBKD_ENOMEM;
+        NBKD_HIP(hipMemsetAsync(stats, 0, 16, s));
+    }
+    if (k > 64) { // all queries through the reference-exact lane-per-query kernel
+        TimedScope ts("knn_exact", s);
+        uint32_t threads = (uint32_t)std::min<uint64_t>(
+            std::max<uint64_t>((512ull << 20) / (32ull * (uint64_t)k), TB), 65536ull);
+        threads = (uint32_t)std::min<uint64_t>(threads, ((uint64_t)mm + TB - 1) / TB * TB);
+        threads = std::max<uint32_t>(threads / TB * TB, TB);
+        LtEntry *lt = (LtEntry *)t.ws.get(WS_LT, (size_t)threads * 2 * k * sizeof(LtEntry), s);
+        if (!lt) return NBKD_ENOMEM;
+        if (t.periodic)
+            knn_exact_kernel<true><<<threads / TB, TB, 0, s>>>(view(t), dq, ord, nullptr, mm, k,
+                                                                lt, dd, di);
+        else
+            knn_exact_kernel<false><<<threads / TB, TB, 0, s>>>(view(t), dq, ord, nullptr, mm, k,
+                                                                 lt, dd, di);
+        NBKD_HIP(hipGetLastError());
+    } else {
+        TimedScope ts("knn", s);
+        if (k <= 8)
+            launch_knn<8>(t, dq, ord, mm, k, dd, di, stats, s);
+        else if (k <= 16)
+            launch_knn<16>(t, dq, ord, mm, k, dd, di, stats, s);
+        else if (k <= 32)
+            launch_knn<32>(t, dq, ord, mm, k, dd, di, stats, s);
+        else
+            launch_knn<64>(t, dq, ord, mm, k, dd, di, stats, s);
+        NBKD_HIP(hipGetLastError());
+    }
+    if (k <= 64 && t.periodic) {
+        // queries outside the periodic box: replay the reference traversal exactly
+        TimedScope ts("knn_outside_box", s);
+        uint32_t *list = (uint32_t *)t.ws.get(WS_LIST, (size_t)mm * 4 + 16, s);
+        const uint32_t threads = 16384;
+        LtEntry *lt = (LtEntry *)t.ws.get(WS_LT, (size_t)threads * 2 * k * sizeof(LtEntry), s);
+        if (!list || !lt) return NBKD_ENOMEM;
+        uint32_t *count = list + mm;
+        NBKD_HIP(hipMemsetAsync(count, 0, 4, s));
+        outside_box_kernel<<<(mm + TB - 1) / TB, TB, 0, s>>>(dq, mm, t.box, list, count);
+        knn_exact_kernel<true><<<threads / TB, TB, 0, s>>>(view(t), dq, list, count, mm, k, lt,
+                                                           dd, di);
+        NBKD_HIP(hipGetLastError());
+    }
+    if (stats) {
+        unsigned long long h[2];
+        NBKD_HIP(hipMemcpyAsync(h, stats, 16, hipMemcpyDeviceToHost, s));
+        NBKD_HIP(hipStreamSynchronize(s));
+        stats_store(h[0], h[1]);
+    }
+    if (!(flags & NBKD_OUTPUT_DEVICE)) {
+        NBKD_HIP(hipMemcpyAsync(out_d, dd, m * (size_t)k * 4, hipMemcpyDeviceToHost, s));
+        NBKD_HIP(hipMemcpyAsync(out_i, di, m * (size_t)k * 4, hipMemcpyDeviceToHost, s));
+        NBKD_HIP(hipStreamSynchronize(s));
+    }
+    return NBKD_OK;
+}
+
+static nbkd_status ball_common(const Tree &t, const float *q, uint64_t m, float r,
+                               uint32_t *out_count, uint64_t *offsets, uint32_t *out_idx,
+                               uint64_t capacity, uint32_t flags, hipStream_t s) {
+    if (m >= (1ull << 32)) {
+        set_error("more than 2^32 - 1 queries per call are not supported");
+        return NBKD_EINVAL;
+    }
+    if (m == 0) {
+        if (offsets) offsets[0] = 0;
+        return NBKD_OK;
+    }
+    const uint32_t mm = (uint32_t)m;
+    std::lock_guard<std::mutex> lk(t.ws.mu);
+    const float *dq = nullptr;
+    nbkd_status rc = stage_queries(t, q, m, flags, dq, s);
+    if (rc) return rc;
+    uint32_t *ord = nullptr;
+    rc = sort_queries(t, dq, mm, ord, s);
+    if (rc) return rc;
+    const float r2 = r * r;
+    const unsigned blocks = (mm + TB - 1) / TB;
+    uint32_t *cnt = out_count;
+    const bool dev_out = flags & NBKD_OUTPUT_DEVICE;
+    if (!cnt || !dev_out) {
+        cnt = (uint32_t *)t.ws.get(WS_COUNT, m * 4, s);
+        if (!cnt) return NBKD_ENOMEM;
+    }
+    {
+        TimedScope ts("ball_count", s);
+        if (t.periodic)
+            ball_count_kernel<true><<<blocks, TB, 0, s>>>(view(t), dq, ord, mm, r2, cnt, nullptr,
+                                                          nullptr);
+        else
+            ball_count_kernel<false><<<blocks, TB, 0, s>>>(view(t), dq, ord, mm, r2, cnt, nullptr,
+                                                           nullptr);
+        NBKD_HIP(hipGetLastError());
+    }
+    if (!offsets) { // count-only
+        if (!dev_out) {
+            NBKD_HIP(hipMemcpyAsync(out_count, cnt, m * 4, hipMemcpyDeviceToHost, s));
+            NBKD_HIP(hipStreamSynchronize(s));
+        }
+        return NBKD_OK;
+    }
+    // CSR: offsets on the host
+    std::vector<uint32_t> hc(m);
+    NBKD_HIP(hipMemcpyAsync(hc.data(), cnt, m * 4, hipMemcpyDeviceToHost, s));
+    NBKD_HIP(hipStreamSynchronize(s));
+    offsets[0] = 0;
+    for (uint64_t i = 0; i < m; ++i) offsets[i + 1] = offsets[i] + hc[i];
+    if (!out_idx) return NBKD_OK;
+    if (capacity < offsets[m]) {
+        set_error("query_ball_csr: capacity smaller than the number of neighbours");
+        return NBKD_EINVAL;
+    }
+    uint64_t *doff = (uint64_t *)t.ws.get(WS_OFF, (m + 1) * 8, s);
+    if (!doff) return NBKD_ENOMEM;
+    NBKD_HIP(hipMemcpyAsync(doff, offsets, (m + 1) * 8, hipMemcpyHostToDevice, s));
+    NBKD_HIP(hipStreamSynchronize(s));
+    uint32_t *di = out_idx;
+    if (!dev_out) {
+        di = (uint32_t *)t.ws.get(WS_IDX, std::max<uint64_t>(offsets[m], 1) * 4, s);
+        if (!di) return NBKD_ENOMEM;
+    }
+    {
+        TimedScope ts("ball_fill", s);
+        if (t.periodic)
+            ball_count_kernel<true><<<blocks, TB, 0, s>>>(view(t), dq, ord, mm, r2, nullptr, doff,
+                                                          di);
+        else
+            ball_count_kernel<false><<<blocks, TB, 0, s>>>(view(t), dq, ord, mm, r2, nullptr, doff,
+                                                           di);
+        NBKD_HIP(hipGetLastError());
+    }
+    if (!dev_out) {
+        NBKD_HIP(hipMemcpyAsync(out_idx, di, offsets[m] * 4, hipMemcpyDeviceToHost, s));
+    }
+    NBKD_HIP(hipStreamSynchronize(s));
+    return NBKD_OK;
+}
+
+nbkd_status query_ball_count(const Tree &t, const float *q, uint64_t m, float r,
+                             uint32_t *out_count, uint32_t flags, hipStream_t s) {
+    return ball_common(t, q, m, r, out_count, nullptr, nullptr, 0, flags, s);
+}
+
+nbkd_status query_ball_csr(const Tree &t, const float *q, uint64_t m, float r, uint64_t *offsets,
+                           uint32_t *out_idx, uint64_t capacity, uint32_t flags, hipStream_t s) {
+    return ball_common(t, q, m, r, nullptr, offsets, out_idx, capacity, flags, s);
+}
+
+} // namespace nbkd

@@ -1,0 +1,112 @@
+"""MI355X-native drop-in for ``nbodyhpc.kdtree``.
+
+Mirrors the reference wrapper kdtree/src/python/nbodyhpc/kdtree/__init__.py:11-56
+(defaults leafsize=128, max_threads=-1; unknown keyword arguments warn;
+N-D query arrays are flattened) on top of the pybind11 module ``_impl``
+(mirror of kdtree/src/cpp/pybind.cpp), which drives the HIP kernels through
+the C ABI in include/nbkd.h.  There is no CPU fallback: without the built
+extension or without a GPU the constructor raises.
+
+Additions (no reference counterpart): ``query_ball`` (scipy-style radius
+query, count or index lists), ``density`` (local number density from the k-th
+neighbour distance or from a radius count) and a ``device`` keyword.
+Deviation: the reference's N-D reshape-back (``reshape(shape[:-1], k)``,
+__init__.py:53-54) raises TypeError; here the result has shape
+``shape[:-1] + (k,)``.
+"""
+from __future__ import annotations
+
+import math
+import warnings
+from typing import Optional, Tuple
+
+import numpy as np
+
+try:
+    from ._impl import KDTree as cKDTree
+    from ._impl import device_count
+except ImportError as e:  # fail loudly: no CPU path exists
+    raise ImportError(
+        "nbodyhpc_amd.kdtree._impl is not built; run `python -m nbodyhpc_amd.build` "
+        f"(hipcc for gfx950 + pybind11). Original error: {e}") from e
+
+__all__ = ["KDTree", "cKDTree", "device_count"]
+
+
+def _flatten(points):
+    points = np.asarray(points)
+    if points.ndim != 2:
+        shape = points.shape
+        return points.reshape((-1, shape[-1])), shape
+    return points, None
+
+
+class KDTree(cKDTree):
+    """Spatial KD-tree, with optional periodic boundary conditions (GPU build and queries)."""
+
+    def __init__(self, points: np.ndarray, leafsize: int = 128, max_threads: int = -1,
+                 boxsize: Optional[float] = None, device: int = -1, **kwargs):
+        """Build a new KDTree.
+
+        Parameters
+        ----------
+        points : (N, 3) array of points (cast to float32).
+        leafsize : maximum number of points in a leaf (the reference clamps to >= 16).
+        max_threads : accepted for compatibility; the build runs on the GPU.
+        boxsize : periodic box size L (every coordinate must be in [0, L]), or None.
+        device : HIP device ordinal (-1: the current device).
+        """
+        super().__init__(points, leafsize, max_threads, boxsize, device)
+
+        if len(kwargs) > 0:
+            warnings.warn("Unrecognized keyword arguments: {}".format(kwargs))
+
+    def query(self, points: np.ndarray, k: int = 1, workers: int = 1,
+              **kwargs) -> Tuple[np.ndarray, np.ndarray]:
+        if len(kwargs) > 0:
+            warnings.warn("Unrecognized keyword arguments: {}".format(kwargs))
+
+        points, shape = _flatten(points)
+        distances, indices = super().query(points, k, workers)
+
+        if shape is not None:
+            distances = distances.reshape(tuple(shape[:-1]) + (k,))
+            indices = indices.reshape(tuple(shape[:-1]) + (k,))
+
+        return distances, indices
+
+    def query_ball(self, points: np.ndarray, r: float, return_length: bool = False,
+                   return_sorted: bool = True, workers: int = 1, **kwargs):
+        """Points within distance r (d2 <= r*r in float32, the kNN metric).
+
+        return_length=True -> uint32 counts, shape points.shape[:-1].
+        Otherwise an object array of uint32 index arrays (sorted ascending
+        unless return_sorted=False), like scipy's query_ball_point.
+        """
+        if len(kwargs) > 0:
+            warnings.warn("Unrecognized keyword arguments: {}".format(kwargs))
+        points, shape = _flatten(points)
+        out_shape = tuple(shape[:-1]) if shape is not None else (np.asarray(points).shape[0],)
+        if return_length:
+            return super().query_ball_count(points, float(r)).reshape(out_shape)
+        off, idx = super().query_ball_csr(points, float(r))
+        rows = np.empty(len(off) - 1, dtype=object)
+        for i in range(len(off) - 1):
+            row = idx[off[i]:off[i + 1]]
+            rows[i] = np.sort(row) if return_sorted else row
+        return rows.reshape(out_shape)
+
+    def density(self, points: np.ndarray, k: Optional[int] = None, r: Optional[float] = None):
+        """Local number density at each query point.
+
+        k given: k / (4/3 pi r_k^3) with r_k the k-th neighbour distance.
+        r given: count(d <= r) / (4/3 pi r^3).
+        """
+        if (k is None) == (r is None):
+            raise ValueError("give exactly one of k or r")
+        if k is not None:
+            d, _ = self.query(points, k=k)
+            rk = d[..., -1].astype(np.float64)
+            return k / (4.0 / 3.0 * math.pi * rk ** 3)
+        c = self.query_ball(points, r, return_length=True).astype(np.float64)
+        return c / (4.0 / 3.0 * math.pi * float(r) ** 3)

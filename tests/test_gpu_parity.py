@@ -1,0 +1,224 @@
+"""GPU parity: the HIP path (through the C ABI and through the pybind surface)
+against the reference's golden vectors and the oracle.  Run on an MI355X:
+    python -m pytest tests -m gpu -x -q
+"""
+import numpy as np
+import pytest
+
+from tests.golden.inputs import edge_cases, g1_inputs, g2_inputs, g3_inputs, g4_inputs, g5_inputs, sha, uniform
+from tests.parity import assert_knn_equal, check_tree_structure, d2_ref, leaf_sets
+
+pytestmark = pytest.mark.gpu
+
+
+def _kdtree():
+    from nbodyhpc import kdtree
+    return kdtree
+
+
+# ---------------------------------------------------------------- reference pytest (G1, G2)
+@pytest.mark.parametrize("name,inputs", [("g1_basic", g1_inputs), ("g2_periodic", g2_inputs)])
+def test_reference_pytest_cases(gpu, golden, name, inputs):
+    """kdtree/tests/test_kdtree.py:6-35: allclose vs scipy, exact indices."""
+    pts, q, box = inputs()
+    g = golden(name)
+    assert str(g["sha"]) == sha(pts, q)
+    tree = _kdtree().KDTree(pts, boxsize=box)
+    d, i = tree.query(q, k=4)
+    assert np.allclose(g["scipy_dist"], d)
+    assert np.all(g["scipy_idx"] == i)
+    assert_knn_equal(d, i, g["dist"], g["idx"], np.asarray(pts, np.float32), q, box)
+    assert np.array_equal(d.view(np.uint32), g["dist"].view(np.uint32))
+
+
+def test_config1_golden(gpu, golden):
+    pts, q = g3_inputs()
+    g = golden("g3_config1")
+    assert str(g["sha"]) == sha(pts, q)
+    t = gpu.Tree(pts, leafsize=128)
+    d, i = t.query(q, 8)
+    assert_knn_equal(d, i, g["dist"], g["idx"], pts, q)
+
+
+@pytest.mark.parametrize("leaf", [32, 128])
+def test_periodic_1e6_golden(gpu, golden, leaf):
+    pts, q = g4_inputs()
+    g = golden("g4_periodic_1e6")
+    assert str(g["sha"]) == sha(pts, q)
+    t = gpu.Tree(pts, leafsize=leaf, boxsize=1.0)
+    d, i = t.query(q, 32)
+    d2 = g[f"d2_leaf{leaf}"]
+    assert_knn_equal(d, i, np.sqrt(d2), g[f"idx_leaf{leaf}"], pts, q, 1.0)
+    # self queries: the point itself is the nearest neighbour (distance 0)
+    assert np.all(d[1000:, 0] == 0.0)
+
+
+def test_node_tables_match_reference(gpu, golden):
+    """G5: the GPU node table equals the reference's bit for bit."""
+    g = golden("g5_nodes")
+    for key, (pts, leaf, box) in g5_inputs().items():
+        assert str(g["sha_" + key]) == sha(pts)
+        t = gpu.Tree(pts, leafsize=leaf, boxsize=box)
+        nodes, x, y, z, idx = t.export()
+        ref = g["nodes_" + key]
+        assert t.n == int(g["n8_" + key])
+        assert t.size == ref.shape[0], key
+        assert np.array_equal(nodes.view(np.uint32).reshape(-1, 4), ref), key
+        check_tree_structure(nodes, x, y, z, idx, len(pts), leaf)
+
+
+def test_leaf_membership_matches_oracle(gpu, oracle):
+    for n, leaf, box in [(1000, 16, None), (50_000, 32, 1.0), (200_000, 128, None)]:
+        pts = uniform(n, 77 + n)
+        t = gpu.Tree(pts, leafsize=leaf, boxsize=box)
+        o = oracle.tree(pts, leaf, box)
+        gn, gx, gy, gz, gi = t.export()
+        on, ox, oy, oz, oi = o.export()
+        assert np.array_equal(gn.view(np.uint32), on.view(np.uint32))
+        assert leaf_sets(gn, gi) == leaf_sets(on, oi)
+        # coordinates travel with their index
+        pp = np.concatenate([pts, np.full(((n + 7) // 8 * 8 - n, 3), np.finfo(np.float32).max,
+                                          np.float32)])
+        assert np.array_equal(pp[gi, 0], gx) and np.array_equal(pp[gi, 1], gy)
+        assert np.array_equal(pp[gi, 2], gz)
+
+
+def test_edge_cases_golden(gpu, golden):
+    g = golden("g6_edges")
+    kd = _kdtree()
+    for key, (pts, q, k, leaf, box) in edge_cases().items():
+        t = kd.KDTree(pts, leafsize=leaf, boxsize=box)
+        assert t.n == int(g["n_" + key]), key
+        assert t.size == int(g["size_" + key]), key
+        d, i = t.query(q, k=k)
+        assert_knn_equal(d, i, g["dist_" + key], g["idx_" + key], np.asarray(pts, np.float32),
+                         np.asarray(q, np.float32), box)
+    with pytest.raises(RuntimeError, match=r"all points must be within the box"):
+        kd.KDTree(np.array([[0.5, 0.5, 1.5]], np.float32), boxsize=1.0)
+
+
+# ---------------------------------------------------------------- sweeps vs oracle
+@pytest.mark.parametrize("n,leaf,k,box", [
+    (10, 16, 4, None), (100, 16, 4, 2.0), (1000, 32, 4, None), (4096, 16, 1, 1.0),
+    (10_000, 64, 7, None), (33_333, 16, 16, 1.0), (100_000, 128, 20, None),
+    (100_000, 32, 33, 1.0), (250_000, 24, 64, None), (250_000, 200, 5, 3.0),
+    (50_000, 32, 100, 1.0), (20_000, 16, 200, None),
+])
+def test_knn_vs_oracle(gpu, oracle, n, leaf, k, box):
+    pts = uniform(n, n + leaf, L=box or 1.0)
+    rng = np.random.Generator(np.random.PCG64(n))
+    q = np.concatenate([rng.uniform(0, box or 1.0, (1500, 3)).astype(np.float32), pts[:500]])
+    t = gpu.Tree(pts, leafsize=leaf, boxsize=box)
+    o = oracle.tree(pts, leaf, box)
+    d, i = t.query(q, k)
+    dr, ir = o.query(q, k)
+    assert_knn_equal(d, i, dr, ir, pts, q, box)
+
+
+def test_knn_brute_force_small(gpu, oracle):
+    """test.cpp:43-111: tree == naive for n in {10, 100, 1000}, incl. periodic L=2."""
+    for n in (10, 100, 1000):
+        for box in (None, 2.0):
+            pts = uniform(n, 42, L=box or 1.0)
+            q = uniform(100, 43, L=box or 1.0)
+            t = gpu.Tree(pts, leafsize=32, boxsize=box)
+            d, i = t.query(q, 4)
+            db, ib = oracle.knn_brute(pts, q, 4, box)
+            assert_knn_equal(d, i, db, ib, pts, q, box)
+
+
+def test_periodic_queries_outside_box(gpu, oracle):
+    """Queries are not validated (pybind.cpp:90-98); outside [0, L]^3 the reference's
+    periodic pruning is not a lower bound and the result depends on its exact
+    traversal, which the lane-per-query path replays."""
+    pts = uniform(30_000, 21)
+    rng = np.random.Generator(np.random.PCG64(22))
+    q = rng.uniform(-0.6, 1.6, (2000, 3)).astype(np.float32)
+    t = gpu.Tree(pts, leafsize=32, boxsize=1.0)
+    o = oracle.tree(pts, 32, 1.0)
+    for k in (1, 8, 32):
+        d, i = t.query(q, k)
+        dr, ir = o.query(q, k)
+        assert_knn_equal(d, i, dr, ir, pts, q, 1.0)
+
+
+def test_duplicates_and_ties(gpu, oracle):
+    base = uniform(300, 3)
+    pts = np.concatenate([base] * 5)
+    q = np.concatenate([base[:50], uniform(50, 4)])
+    t = gpu.Tree(pts, leafsize=16)
+    d, i = t.query(q, 12)
+    db, ib = oracle.knn_brute(pts, q, 12)
+    assert_knn_equal(d, i, db, ib, pts, q)
+
+
+def test_grid_points_heavy_ties(gpu, oracle):
+    """A lattice makes exact d2 ties everywhere (and coordinate ties at every split)."""
+    g = np.arange(24, dtype=np.float32) / 24
+    pts = np.stack(np.meshgrid(g, g, g, indexing="ij"), -1).reshape(-1, 3)
+    q = pts[::37] + np.float32(0.01)
+    t = gpu.Tree(pts, leafsize=16, boxsize=1.0)
+    check_tree_structure(*t.export(), len(pts), 16)
+    d, i = t.query(q, 10)
+    db, ib = oracle.knn_brute(pts, q, 10, 1.0)
+    assert_knn_equal(d, i, db, ib, pts, q, 1.0)
+
+
+# ---------------------------------------------------------------- radius queries (NEW)
+@pytest.mark.parametrize("box", [None, 1.0])
+def test_ball_count_and_csr(gpu, oracle, box):
+    pts = uniform(20_000, 5)
+    q = uniform(700, 6)
+    r = 0.05
+    t = gpu.Tree(pts, leafsize=32, boxsize=box)
+    c = t.ball_count(q, r)
+    cb = oracle.ball_count_brute(pts, q, r, box)
+    assert np.array_equal(c, cb)
+    off, idx = t.ball_csr(q, r)
+    assert np.array_equal(np.diff(off.astype(np.int64)), cb.astype(np.int64))
+    for j in range(0, 700, 37):
+        row = np.sort(idx[off[j]:off[j + 1]])
+        d2 = d2_ref(q[j], pts, box)
+        expect = np.nonzero(d2 <= np.float32(r) * np.float32(r))[0]
+        assert np.array_equal(row, expect.astype(np.uint32))
+
+
+def test_python_surface(gpu):
+    kd = _kdtree()
+    pts = uniform(5000, 9)
+    t = kd.KDTree(pts, boxsize=1.0)
+    assert t.n == 5000 and t.periodic and t.boxsize == 1.0
+    with pytest.raises(RuntimeError, match="k must be positive integer"):
+        t.query(pts[:3], k=0)
+    with pytest.raises(RuntimeError, match=r"shape \(N, 3\)"):
+        t.query(pts[:, :2])
+    with pytest.warns(UserWarning, match="Unrecognized keyword arguments"):
+        kd.KDTree(pts, foo=1)
+    d, i = t.query(pts[:12].reshape(3, 4, 3), k=2)
+    assert d.shape == (3, 4, 2) and i.shape == (3, 4, 2)
+    rows = t.query_ball(pts[:5], 0.05)
+    counts = t.query_ball(pts[:5], 0.05, return_length=True)
+    assert [len(r) for r in rows] == counts.tolist()
+    dens = t.density(pts[:100], k=8)
+    assert np.all(np.isfinite(dens)) and np.all(dens > 0)
+
+
+def test_device_pointer_path(gpu):
+    """C ABI with device-resident inputs/outputs on a caller stream (the bench path)."""
+    from nbodyhpc_amd import hip
+    pts = uniform(100_000, 12)
+    dev = hip.DeviceArray.from_numpy(pts)
+    t = gpu.Tree(n=pts.shape[0], dev_ptr=dev.ptr, leafsize=32, boxsize=1.0)
+    k = 16
+    od = hip.DeviceArray((pts.shape[0], k), np.float32)
+    oi = hip.DeviceArray((pts.shape[0], k), np.uint32)
+    stream = hip.Stream()
+    t.query_device(dev.ptr, pts.shape[0], k, od.ptr, oi.ptr, stream.handle)
+    stream.synchronize()
+    d_host, i_host = t.query(pts, k)
+    assert np.array_equal(od.numpy(), d_host)
+    assert np.array_equal(oi.numpy(), i_host)
+    cnt = hip.DeviceArray((pts.shape[0],), np.uint32)
+    t.ball_count_device(dev.ptr, pts.shape[0], 0.02, cnt.ptr, stream.handle)
+    stream.synchronize()
+    assert np.array_equal(cnt.numpy(), t.ball_count(pts, 0.02))
