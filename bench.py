@@ -1,0 +1,263 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X kd-tree hot path: batched k=32 kNN self-queries over
+1e8 uniform periodic particles (BASELINE.json metric), plus build time.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+One step = one pass of the hot path over one batch: every local particle
+queried for its k=32 nearest neighbours (query bucketing + radix sort + packet
+kNN kernel), inputs and outputs resident in HBM.  N > 1: the particles are
+sharded by x-slab, each rank holds its slab plus a periodic halo exchanged
+over RCCL at setup, and queries its own particles (weak scaling: 1e8 per GPU).
+
+Rank 0 prints ONE JSON line.  Device plumbing goes through the same HIP
+runtime as libnbkd (nbodyhpc_amd/hip.py); torch is used only for
+torch.distributed (gloo) coordination.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "kNN queries/sec (k=32, 1e8 periodic particles)"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+# Algorithmic bytes per kNN query: B_q = 16*N + 12*P + 12 + 8k,
+# N = nodes visited, P = points scanned by the REFERENCE traversal at leafsize 32
+# (its KDTreeQueryStatistics), uniform periodic k=32 at 1e8 points: N=61.8, P=307.9.
+REF_NODES_1E8, REF_POINTS_1E8 = 61.8, 307.9
+
+
+def bytes_per_query(k, nodes=REF_NODES_1E8, points=REF_POINTS_1E8):
+    return 16.0 * nodes + 12.0 * points + 12.0 + 8.0 * k
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=5)
+    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--n", type=float, default=1e8, help="particles per GPU")
+    p.add_argument("--k", type=int, default=32)
+    p.add_argument("--leafsize", type=int, default=32)
+    p.add_argument("--box", type=float, default=1.0)
+    p.add_argument("--seed", type=int, default=20261015)
+    p.add_argument("--cpu-sample", type=int, default=500_000,
+                   help="queries timed on the CPU baseline (rank 0, N=1)")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-parity", action="store_true")
+    return p.parse_args()
+
+
+def log(*a):
+    print("[bench]", *a, file=sys.stderr, flush=True)
+
+
+def gen_uniform(n, seed, box):
+    rng = np.random.Generator(np.random.PCG64(seed))
+    out = np.empty((n, 3), np.float32)
+    chunk = 1 << 24
+    for s in range(0, n, chunk):
+        e = min(n, s + chunk)
+        out[s:e] = rng.uniform(0.0, box, size=(e - s, 3))
+    return out
+
+
+def cpu_baseline(points, k, leafsize, box, sample, gpu_d, gpu_i):
+    """The reference's own C++ (oracle/_ref) when built, else the C restatement
+    (oracle/liborc.so), timed on this host's cores on a bounded sample."""
+    from oracle.oracle import Oracle, Reference, REF_PATH
+    kind = "reference" if os.path.exists(REF_PATH) else "port"
+    lib = Reference() if kind == "reference" else Oracle()
+    cores = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+    cores = max(1, min(cores, 64))
+    t0 = time.perf_counter()
+    tree = lib.tree(points, leafsize, box)
+    build_s = time.perf_counter() - t0
+    q = points[:sample]
+    t0 = time.perf_counter()
+    d, i = tree.query(q, k, workers=cores)
+    query_s = time.perf_counter() - t0
+    parity = None
+    if gpu_d is not None:
+        from tests.parity import assert_knn_equal
+        try:
+            tie_rows = assert_knn_equal(gpu_d, gpu_i, d, i, points, q, box)
+            parity = {"rows": int(sample), "bit_exact_distances": True,
+                      "rows_with_tie_order_differences": int(tie_rows)}
+        except AssertionError as e:  # reported, never hidden
+            parity = {"rows": int(sample), "FAILED": str(e)[:500]}
+    return {"value": sample / query_s, "unit": "queries/s", "cores": cores, "kind": kind,
+            "sample": f"{sample} self-queries (first {sample} particles) of the same "
+                      f"{len(points):.0e}-point periodic tree, k={k}, leafsize={leafsize}, "
+                      f"{cores} threads; single-threaded CPU build {build_s:.2f} s",
+            "build_s": build_s}, parity
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
+    from nbodyhpc_amd import capi, hip
+
+    dist = None
+    if world > 1:
+        import torch.distributed as dist  # gloo: CPU-side coordination only
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    hip.set_device(local_rank)
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    def allmax(v):
+        if dist is None:
+            return v
+        import torch
+        t = torch.tensor([v], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    n = int(args.n)
+    k, L = args.k, args.box
+    t_gen = time.perf_counter()
+    if world == 1:
+        points = gen_uniform(n, args.seed, L)
+        own = n
+    else:
+        from nbodyhpc_amd import slab
+        points, own = slab.make_local_points(n, args.seed, L, rank, world, k)
+    log(f"rank {rank}: {own} own particles ({len(points)} with halo) generated in "
+        f"{time.perf_counter() - t_gen:.1f} s")
+
+    dev_pts = hip.DeviceArray.from_numpy(points)
+    stream = hip.Stream()
+    # build: one untimed (code-object load), then timed builds
+    capi.Tree(n=len(points), dev_ptr=dev_pts.ptr, leafsize=args.leafsize, boxsize=L,
+              device=local_rank, stream=stream.handle).close()
+    build_ms = []
+    for _ in range(2):
+        hip.synchronize()
+        t0 = time.perf_counter()
+        tree = capi.Tree(n=len(points), dev_ptr=dev_pts.ptr, leafsize=args.leafsize, boxsize=L,
+                         device=local_rank, stream=stream.handle)
+        hip.synchronize()
+        build_ms.append((time.perf_counter() - t0) * 1e3)
+        if _ == 0:
+            tree.close()
+    build_ms = min(build_ms)
+
+    od = hip.DeviceArray((own, k), np.float32)
+    oi = hip.DeviceArray((own, k), np.uint32)
+
+    def step():
+        tree.query_device(dev_pts.ptr, own, k, od.ptr, oi.ptr, stream.handle)
+
+    for _ in range(args.warmup):
+        step()
+    stream.synchronize()
+    capi.timing_enable(True)
+    capi.timing_reset()
+    barrier()
+    hip.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    hip.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    knn_ms, knn_launches = capi.timing_read("knn")
+    sort_ms, _ = capi.timing_read("sort")
+    key_ms, _ = capi.timing_read("leaf_key")
+    oob_ms, _ = capi.timing_read("knn_outside_box")
+    capi.timing_enable(False)
+    elapsed_max = allmax(elapsed)
+
+    # work counters of our own traversal (one extra, untimed pass)
+    capi.stats_enable(True)
+    step()
+    stream.synchronize()
+    nodes_vis, pts_scanned = capi.stats_read()
+    capi.stats_enable(False)
+
+    gpu_d = gpu_i = None
+    parity_rows = min(args.cpu_sample, own)
+    if rank == 0 and not args.no_parity:
+        gpu_d = od.numpy_head(parity_rows)
+        gpu_i = oi.numpy_head(parity_rows)
+
+    if rank != 0:
+        return
+    total_q = own * world * args.steps
+    value = total_q / elapsed_max
+    ms_per_step = elapsed_max / args.steps * 1e3
+    bq = bytes_per_query(k)
+    knn_avg_ms = knn_ms / max(knn_launches, 1)
+    achieved = bq * own / (knn_avg_ms * 1e-3) / 1e9
+    traffic = None
+    pmc_path = os.path.join(ROOT, "profiles", "pmc_knn.json")
+    if os.path.exists(pmc_path):
+        try:
+            traffic = json.load(open(pmc_path)).get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    cpu = None
+    parity = None
+    if world == 1 and not args.no_cpu_baseline:
+        cpu, parity = cpu_baseline(points, k, args.leafsize, L, parity_rows, gpu_d, gpu_i)
+    out = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "queries/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic: numpy PCG64 uniform [0,L)^3, L=1, float32; self-queries",
+        "config": {
+            "workload": f"kNN k={k} self-query of every particle, {n:.0e} uniform periodic "
+                        f"particles per GPU (L={L}), leafsize {args.leafsize}",
+            "n_particles_per_gpu": own, "k": k, "leafsize": args.leafsize,
+            "queries_per_step": own * world,
+            "parallelism": "single" if world == 1 else f"x-slab x{world} + RCCL halo",
+        },
+        "build_ms": build_ms,
+        "roofline": {
+            "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+            "kernel": "knn_kernel<32,periodic>",
+            "kernel_ms_per_launch": knn_avg_ms,
+            "bytes_per_query": bq,
+        },
+        "breakdown_ms_per_step": {
+            "leaf_key": key_ms / args.steps, "sort": sort_ms / args.steps,
+            "knn": knn_ms / args.steps, "outside_box_check": oob_ms / args.steps,
+        },
+        "traversal_per_query": {"nodes_visited": nodes_vis / own,
+                                "points_scanned": pts_scanned / own},
+        "cpu_baseline": None if cpu is None else {kk: cpu[kk] for kk in
+                                                  ("value", "unit", "cores", "kind", "sample")},
+        "cpu_build_ms": None if cpu is None else cpu["build_s"] * 1e3,
+        "parity_vs_cpu": parity,
+    }
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

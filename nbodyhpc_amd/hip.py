@@ -89,6 +89,13 @@ class DeviceArray:
         _ok(_hip().hipMemcpy(out.ctypes.data, self.ptr, self.nbytes, D2H), "hipMemcpy D2H")
         return out
 
+    def numpy_head(self, rows):
+        """copy only the first `rows` rows (leading dimension) to the host"""
+        rows = min(int(rows), self.shape[0])
+        out = np.empty((rows,) + self.shape[1:], self.dtype)
+        _ok(_hip().hipMemcpy(out.ctypes.data, self.ptr, out.nbytes, D2H), "hipMemcpy D2H")
+        return out
+
     def zero(self):
         _ok(_hip().hipMemset(self.ptr, 0, self.nbytes), "hipMemset")
 
