@@ -189,7 +189,8 @@ def main():
     capi.stats_enable(True)
     step()
     stream.synchronize()
-    nodes_vis, pts_scanned = capi.stats_read()
+    st = capi.stats_read_all()
+    nodes_vis, pts_scanned = st["node_lane_visits"], st["pair_evals"]
     capi.stats_enable(False)
 
     gpu_d = gpu_i = None
@@ -250,7 +251,10 @@ def main():
             "knn": knn_ms / args.steps, "outside_box_check": oob_ms / args.steps,
         },
         "traversal_per_query": {"nodes_visited": nodes_vis / own,
-                                "points_scanned": pts_scanned / own},
+                                "distance_evals": pts_scanned / own},
+        "traversal_per_packet": {kk: st[kk] / max(st["packets"], 1)
+                                 for kk in ("dense_rounds", "sparse_iters", "merges", "candidates",
+                                           "fill_merges")},
         "cpu_baseline": None if cpu is None else {kk: cpu[kk] for kk in
                                                   ("value", "unit", "cores", "kind", "sample")},
         "cpu_build_ms": None if cpu is None else cpu["build_s"] * 1e3,

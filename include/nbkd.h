@@ -129,6 +129,11 @@ nbkd_status nbkd_timing_read(const char *name, double *ms, uint64_t *launches);
  * traversal.  Enabled with nbkd_stats_enable(1); costs a few % when on. */
 nbkd_status nbkd_stats_enable(int32_t enable);
 nbkd_status nbkd_stats_read(uint64_t *nodes_visited, uint64_t *points_scanned);
+/* all counters of the last kNN call: [0] nodes entered x packet lanes,
+ * [1] (query, point) distance evaluations, [2] dense leaf rounds, [3] sparse
+ * (lane-compacted) iterations, [4] top-k merges, [5] packets (waves),
+ * [6] candidates merged (all lanes), [7] merges while some lane was still filling */
+nbkd_status nbkd_stats_read_all(uint64_t *out, int32_t n);
 
 #ifdef __cplusplus
 }

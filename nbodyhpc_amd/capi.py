@@ -52,6 +52,7 @@ _PROTOS = {
                                 ctypes.POINTER(_u64)]),
     "nbkd_stats_enable": (_i32, [_i32]),
     "nbkd_stats_read": (_i32, [ctypes.POINTER(_u64), ctypes.POINTER(_u64)]),
+    "nbkd_stats_read_all": (_i32, [ctypes.POINTER(_u64), _i32]),
 }
 
 
@@ -198,3 +199,13 @@ def stats_read():
     a, b = _u64(), _u64()
     _check(lib().nbkd_stats_read(ctypes.byref(a), ctypes.byref(b)))
     return a.value, b.value
+
+
+STATS_NAMES = ("node_lane_visits", "pair_evals", "dense_rounds", "sparse_iters", "merges",
+               "packets", "candidates", "fill_merges")
+
+
+def stats_read_all():
+    arr = (_u64 * len(STATS_NAMES))()
+    _check(lib().nbkd_stats_read_all(arr, len(STATS_NAMES)))
+    return dict(zip(STATS_NAMES, [int(v) for v in arr]))

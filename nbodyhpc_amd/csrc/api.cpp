@@ -19,7 +19,7 @@ namespace nbkd {
 
 namespace {
 thread_local std::string g_err;
-thread_local uint64_t g_stats[2] = {0, 0};
+thread_local uint64_t g_stats[NBKD_NSTATS] = {};
 
 std::mutex g_tmu;
 bool g_timing = false;
@@ -49,6 +49,11 @@ void free_tree(Tree &t) {
     if (t.z) (void)hipFree(t.z);
     if (t.idx) (void)hipFree(t.idx);
     if (t.nodes) (void)hipFree(t.nodes);
+    if (t.splits) (void)hipFree(t.splits);
+    if (t.shape_c) (void)hipFree(t.shape_c);
+    if (t.shape_n) (void)hipFree(t.shape_n);
+    t.splits = nullptr;
+    t.shape_c = t.shape_n = nullptr;
     t.x = t.y = t.z = nullptr;
     t.idx = nullptr;
     t.nodes = nullptr;
@@ -67,9 +72,8 @@ nbkd_status hip_fail(hipError_t e, const char *what) {
 
 bool timing_enabled() { return g_timing; }
 bool stats_enabled() { return g_stats_on; }
-void stats_store(uint64_t nodes, uint64_t points) {
-    g_stats[0] = nodes;
-    g_stats[1] = points;
+void stats_store(const uint64_t *v) {
+    for (int i = 0; i < NBKD_NSTATS; ++i) g_stats[i] = v[i];
 }
 
 TimedScope::TimedScope(const char *name, hipStream_t s) : name_(name), s_(s) {
@@ -305,6 +309,12 @@ nbkd_status nbkd_stats_enable(int32_t enable) {
 nbkd_status nbkd_stats_read(uint64_t *nodes_visited, uint64_t *points_scanned) {
     if (nodes_visited) *nodes_visited = g_stats[0];
     if (points_scanned) *points_scanned = g_stats[1];
+    return NBKD_OK;
+}
+
+nbkd_status nbkd_stats_read_all(uint64_t *out, int32_t n) {
+    if (!out || n < 0) return NBKD_EINVAL;
+    for (int i = 0; i < n && i < NBKD_NSTATS; ++i) out[i] = g_stats[i];
     return NBKD_OK;
 }
 

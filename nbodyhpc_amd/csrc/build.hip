@@ -489,6 +489,12 @@ small_kernel(const SSeg *__restrict__ list, uint32_t leaf, Soa bufA, Soa bufB,
     }
 }
 
+__global__ void __launch_bounds__(TB)
+extract_splits_kernel(const nbkd_node *__restrict__ nodes, uint64_t nn, float *__restrict__ splits) {
+    for (uint64_t i = blockIdx.x * (uint64_t)TB + threadIdx.x; i < nn; i += (uint64_t)gridDim.x * TB)
+        splits[i] = nodes[i].split;
+}
+
 // ------------------------------------------------------------------ host side
 struct Skeleton {
     std::map<uint64_t, uint32_t> memo; // count -> subtree node count
@@ -697,6 +703,19 @@ nbkd_status build_tree(Tree &t, const float *xyz, uint64_t n, int32_t leaf_size,
                 d_tabn.as<uint32_t>(), (int)tab_c.size());
             NBKD_HIP(hipGetLastError());
         }
+    }
+    // descent helpers for query bucketing: split per node + the shape table
+    NBKD_HIP(hipMalloc(&t.splits, std::max<uint64_t>(t.nnodes, 1) * 4));
+    NBKD_HIP(hipMalloc(&t.shape_c, tab_c.size() * 4));
+    NBKD_HIP(hipMalloc(&t.shape_n, tab_n.size() * 4));
+    t.shape_len = (int)tab_c.size();
+    NBKD_HIP(hipMemcpyAsync(t.shape_c, tab_c.data(), tab_c.size() * 4, hipMemcpyHostToDevice, s));
+    NBKD_HIP(hipMemcpyAsync(t.shape_n, tab_n.data(), tab_n.size() * 4, hipMemcpyHostToDevice, s));
+    {
+        uint64_t blocks = std::min<uint64_t>((t.nnodes + TB - 1) / TB, 4096);
+        extract_splits_kernel<<<(unsigned)std::max<uint64_t>(blocks, 1), TB, 0, s>>>(
+            t.nodes, t.nnodes, t.splits);
+        NBKD_HIP(hipGetLastError());
     }
     NBKD_HIP(hipStreamSynchronize(s));
     return NBKD_OK;

@@ -43,6 +43,11 @@ struct Tree {
     float *x = nullptr, *y = nullptr, *z = nullptr;
     uint32_t *idx = nullptr;
     nbkd_node *nodes = nullptr;
+    // descent helpers: split value per node and the shape table
+    // (count -> subtree node count, sorted by count) of this (n8, leaf)
+    float *splits = nullptr;
+    uint32_t *shape_c = nullptr, *shape_n = nullptr;
+    int shape_len = 0;
     mutable Workspace ws;
 };
 
@@ -82,7 +87,8 @@ struct TimedScope {
 };
 bool timing_enabled();
 bool stats_enabled();
-void stats_store(uint64_t nodes, uint64_t points);
+constexpr int NBKD_NSTATS = 8; // nodes*lanes, lane-point evals, dense rounds, sparse iters, merges, waves, candidates, fill merges
+void stats_store(const uint64_t *v);
 
 // RAII device allocation (plain hipMalloc; freed after the stream drained).
 // The stream-ordered pool (hipMallocAsync) is deliberately not used: mixing it
@@ -109,6 +115,10 @@ struct DevBuf {
 // build.hip
 nbkd_status build_tree(Tree &t, const float *xyz, uint64_t n, int32_t leaf_size, bool input_dev,
                        hipStream_t s);
+
+// knn_packet.hip
+void launch_knn_packet(const Tree &t, const float *q, const uint32_t *order, uint32_t m, int k,
+                       float *od, uint32_t *oi, unsigned long long *stats, hipStream_t s);
 
 // query.hip
 nbkd_status query_knn(const Tree &t, const float *q, uint64_t m, int k, float *out_d,

@@ -1,0 +1,140 @@
+// Device helpers shared by the query kernels (gfx950).  Metric formulas follow
+// the reference bit for bit: kdtree/src/cpp/include/kdtree/kdtree.hpp:23-31,
+// 35-45, 72-84, 89-107; compile with -ffp-contract=off.
+#pragma once
+
+#include "internal.hpp"
+
+namespace nbkd {
+namespace dev {
+
+__device__ __forceinline__ uint32_t mbcnt64(uint64_t mask) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                     __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+
+__device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ float unif(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(uint32_t, v)));
+}
+
+// ------------------------------------------------------------------ metrics
+template <bool PER>
+__device__ __forceinline__ float point_d2(float qx, float qy, float qz, float px, float py, float pz,
+                                          float L) {
+    float dx = px - qx, dy = py - qy, dz = pz - qz;
+    if constexpr (PER) {
+        // min(d^2, (d-L)^2, (d+L)^2) == (min(|d|, |d-L|, |d+L|))^2 exactly
+        dx = fminf(fminf(fabsf(dx), fabsf(dx - L)), fabsf(dx + L));
+        dy = fminf(fminf(fabsf(dy), fabsf(dy - L)), fabsf(dy + L));
+        dz = fminf(fminf(fabsf(dz), fabsf(dz - L)), fabsf(dz + L));
+    }
+    float a = dx * dx, b = dy * dy, c = dz * dz;
+    return (a + b) + c;
+}
+
+template <bool PER>
+__device__ __forceinline__ float box_axis(float p, float lo, float hi, float L) {
+    if constexpr (PER) {
+        // kdtree.hpp:93-103
+        float below = fminf(lo - p, (p + L) - hi);
+        float above = fminf(p - hi, (lo + L) - p);
+        float m = p < lo ? below : (p > hi ? above : 0.0f);
+        return m * m;
+    } else {
+        // kdtree.hpp:39-41
+        float dl = fmaxf(lo - p, 0.0f), dr = fmaxf(p - hi, 0.0f);
+        float a = dl * dl, b = dr * dr;
+        return a + b;
+    }
+}
+
+template <bool PER>
+__device__ __forceinline__ float box_d2(float qx, float qy, float qz, const float b[6], float L) {
+    float r = box_axis<PER>(qx, b[0], b[1], L);
+    r += box_axis<PER>(qy, b[2], b[3], L);
+    r += box_axis<PER>(qz, b[4], b[5], L);
+    return r;
+}
+
+// ------------------------------------------------------------------ register sorting networks
+template <int N>
+__device__ __forceinline__ void ce(float (&d)[N], uint32_t (&i)[N], int a, int b) {
+    // ascending: d[a] <= d[b]
+    float da = d[a], db = d[b];
+    bool sw = db < da;
+    d[a] = sw ? db : da;
+    d[b] = sw ? da : db;
+    uint32_t ia = i[a], ib = i[b];
+    i[a] = sw ? ib : ia;
+    i[b] = sw ? ia : ib;
+}
+
+template <int N>
+__device__ __forceinline__ void bitonic_sort(float (&d)[N], uint32_t (&i)[N]) {
+#pragma unroll
+    for (int size = 2; size <= N; size <<= 1) {
+#pragma unroll
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+#pragma unroll
+            for (int a = 0; a < N; ++a) {
+                int b = a ^ stride;
+                if (b > a) {
+                    if ((a & size) == 0)
+                        ce<N>(d, i, a, b);
+                    else
+                        ce<N>(d, i, b, a);
+                    if ((a & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+                }
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+}
+
+// sched_barrier between groups of compare-exchanges: without it the scheduler
+// hoists a whole stage's compares and the live masks/temporaries push the
+// kernel past the VGPR budget of the occupancy it needs
+template <int N>
+__device__ __forceinline__ void bitonic_merge(float (&d)[N], uint32_t (&i)[N]) {
+#pragma unroll
+    for (int stride = N >> 1; stride > 0; stride >>= 1) {
+#pragma unroll
+        for (int a = 0; a < N; ++a) {
+            int b = a ^ stride;
+            if (b > a) {
+                ce<N>(d, i, a, b);
+                if ((a & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+// ------------------------------------------------------------------ packet traversal
+struct WaveStack {
+    uint32_t node;
+    float b0, b1, b2, b3, b4, b5;
+};
+
+// push: the lane whose id equals the stack pointer takes the entry
+#define NBKD_PUSH(SP, NODE, BX)                                                                    \
+    do {                                                                                           \
+        const bool me_ = lane == (SP);                                                             \
+        stk.node = me_ ? (NODE) : stk.node;                                                        \
+        stk.b0 = me_ ? (BX)[0] : stk.b0;                                                           \
+        stk.b1 = me_ ? (BX)[1] : stk.b1;                                                           \
+        stk.b2 = me_ ? (BX)[2] : stk.b2;                                                           \
+        stk.b3 = me_ ? (BX)[3] : stk.b3;                                                           \
+        stk.b4 = me_ ? (BX)[4] : stk.b4;                                                           \
+        stk.b5 = me_ ? (BX)[5] : stk.b5;                                                           \
+        ++(SP);                                                                                    \
+    } while (0)
+
+__device__ __forceinline__ float rdlane(float v, int l) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(uint32_t, v), l));
+}
+
+
+} // namespace dev
+} // namespace nbkd

@@ -26,108 +26,17 @@
 //   per-axis min of the three images; min of squares == square of the min |.|),
 //   compiled with -ffp-contract=off, so distances are bit-identical.
 #include <algorithm>
+#include <cstdlib>
 
 #include "internal.hpp"
+#include "metric.hpp"
 
 namespace nbkd {
 namespace {
+using namespace dev;
 
 constexpr int TB = 256;
 constexpr int WPB = TB / 64; // waves per block
-
-__device__ __forceinline__ uint32_t mbcnt64(uint64_t mask) {
-    return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
-                                     __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
-}
-
-__device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
-__device__ __forceinline__ float unif(float v) {
-    return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(uint32_t, v)));
-}
-
-// ------------------------------------------------------------------ metrics
-template <bool PER>
-__device__ __forceinline__ float point_d2(float qx, float qy, float qz, float px, float py, float pz,
-                                          float L) {
-    float dx = px - qx, dy = py - qy, dz = pz - qz;
-    if constexpr (PER) {
-        // min(d^2, (d-L)^2, (d+L)^2) == (min(|d|, |d-L|, |d+L|))^2 exactly
-        dx = fminf(fminf(fabsf(dx), fabsf(dx - L)), fabsf(dx + L));
-        dy = fminf(fminf(fabsf(dy), fabsf(dy - L)), fabsf(dy + L));
-        dz = fminf(fminf(fabsf(dz), fabsf(dz - L)), fabsf(dz + L));
-    }
-    float a = dx * dx, b = dy * dy, c = dz * dz;
-    return (a + b) + c;
-}
-
-template <bool PER>
-__device__ __forceinline__ float box_axis(float p, float lo, float hi, float L) {
-    if constexpr (PER) {
-        // kdtree.hpp:93-103
-        float below = fminf(lo - p, (p + L) - hi);
-        float above = fminf(p - hi, (lo + L) - p);
-        float m = p < lo ? below : (p > hi ? above : 0.0f);
-        return m * m;
-    } else {
-        // kdtree.hpp:39-41
-        float dl = fmaxf(lo - p, 0.0f), dr = fmaxf(p - hi, 0.0f);
-        float a = dl * dl, b = dr * dr;
-        return a + b;
-    }
-}
-
-template <bool PER>
-__device__ __forceinline__ float box_d2(float qx, float qy, float qz, const float b[6], float L) {
-    float r = box_axis<PER>(qx, b[0], b[1], L);
-    r += box_axis<PER>(qy, b[2], b[3], L);
-    r += box_axis<PER>(qz, b[4], b[5], L);
-    return r;
-}
-
-// ------------------------------------------------------------------ register sorting networks
-template <int N>
-__device__ __forceinline__ void ce(float (&d)[N], uint32_t (&i)[N], int a, int b) {
-    // ascending: d[a] <= d[b]
-    float da = d[a], db = d[b];
-    bool sw = db < da;
-    d[a] = sw ? db : da;
-    d[b] = sw ? da : db;
-    uint32_t ia = i[a], ib = i[b];
-    i[a] = sw ? ib : ia;
-    i[b] = sw ? ia : ib;
-}
-
-template <int N>
-__device__ __forceinline__ void bitonic_sort(float (&d)[N], uint32_t (&i)[N]) {
-#pragma unroll
-    for (int size = 2; size <= N; size <<= 1) {
-#pragma unroll
-        for (int stride = size >> 1; stride > 0; stride >>= 1) {
-#pragma unroll
-            for (int a = 0; a < N; ++a) {
-                int b = a ^ stride;
-                if (b > a) {
-                    if ((a & size) == 0)
-                        ce<N>(d, i, a, b);
-                    else
-                        ce<N>(d, i, b, a);
-                }
-            }
-        }
-    }
-}
-
-template <int N>
-__device__ __forceinline__ void bitonic_merge(float (&d)[N], uint32_t (&i)[N]) {
-#pragma unroll
-    for (int stride = N >> 1; stride > 0; stride >>= 1) {
-#pragma unroll
-        for (int a = 0; a < N; ++a) {
-            int b = a ^ stride;
-            if (b > a) ce<N>(d, i, a, b);
-        }
-    }
-}
 
 // ------------------------------------------------------------------ query bucketing
 __global__ void __launch_bounds__(TB)
@@ -145,6 +54,56 @@ leaf_key_kernel(DevTree t, const float *__restrict__ q, uint32_t m, uint32_t *__
     }
     keys[i] = nd.left >> 3;
     vals[i] = i;
+}
+
+// Same descent without touching the 16-B node records: the shape is a pure
+// function of (n8, leaf) — left child = id + 1, right child = id + 1 +
+// |subtree(m)|, m = (count/2)/8*8, axis = depth % 3 — so only the 4-B split
+// values are read (a 33 MB array at 1e8 points, Infinity-Cache resident).
+constexpr int SHAPE_MAX = 256;
+__global__ void __launch_bounds__(TB)
+leaf_key2_kernel(const float *__restrict__ splits, const uint32_t *__restrict__ shape_c,
+                 const uint32_t *__restrict__ shape_n, int shape_len, uint32_t n8, uint32_t leaf,
+                 const float *__restrict__ q, uint32_t m, uint32_t *__restrict__ keys,
+                 uint32_t *__restrict__ vals) {
+    __shared__ uint32_t sc[SHAPE_MAX], sn[SHAPE_MAX];
+    for (int i = threadIdx.x; i < shape_len; i += TB) {
+        sc[i] = shape_c[i];
+        sn[i] = shape_n[i];
+    }
+    __syncthreads();
+    for (uint32_t i = blockIdx.x * TB + threadIdx.x; i < m; i += gridDim.x * TB) {
+        const float p[3] = {q[3 * (size_t)i], q[3 * (size_t)i + 1], q[3 * (size_t)i + 2]};
+        uint32_t node = 0, left = 0, count = n8;
+        int dim = 0;
+        while (count > leaf) {
+            const uint32_t mm = (count / 2) / 8 * 8;
+            const float s = splits[node];
+            if (p[dim] > s) { // near child, kdtree_impl.hpp:633
+                uint32_t sub = 1;
+                if (mm > leaf) {
+                    int lo = 0, hi = shape_len - 1;
+                    while (lo < hi) {
+                        const int mid = (lo + hi) >> 1;
+                        if (sc[mid] < mm)
+                            lo = mid + 1;
+                        else
+                            hi = mid;
+                    }
+                    sub = sn[lo];
+                }
+                node += 1 + sub;
+                left += mm;
+                count -= mm;
+            } else {
+                node += 1;
+                count = mm;
+            }
+            dim = dim == 2 ? 0 : dim + 1;
+        }
+        keys[i] = left >> 3;
+        vals[i] = i;
+    }
 }
 
 // ------------------------------------------------------------------ LSD radix sort (keys + values)
@@ -324,32 +283,6 @@ nbkd_status radix_sort(Workspace &ws, uint32_t *k0, uint32_t *v0, uint32_t *k1, 
         NBKD_HIP(hipGetLastError());
     }
     return NBKD_OK;
-}
-
-// ------------------------------------------------------------------ packet traversal
-constexpr int STACK = 64; // one entry per lane
-
-struct WaveStack {
-    uint32_t node;
-    float b0, b1, b2, b3, b4, b5;
-};
-
-// push: the lane whose id equals the stack pointer takes the entry
-#define NBKD_PUSH(SP, NODE, BX)                                                                    \
-    do {                                                                                           \
-        const bool me_ = lane == (SP);                                                             \
-        stk.node = me_ ? (NODE) : stk.node;                                                        \
-        stk.b0 = me_ ? (BX)[0] : stk.b0;                                                           \
-        stk.b1 = me_ ? (BX)[1] : stk.b1;                                                           \
-        stk.b2 = me_ ? (BX)[2] : stk.b2;                                                           \
-        stk.b3 = me_ ? (BX)[3] : stk.b3;                                                           \
-        stk.b4 = me_ ? (BX)[4] : stk.b4;                                                           \
-        stk.b5 = me_ ? (BX)[5] : stk.b5;                                                           \
-        ++(SP);                                                                                    \
-    } while (0)
-
-__device__ __forceinline__ float rdlane(float v, int l) {
-    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(uint32_t, v), l));
 }
 
 template <int KC, bool PER>
@@ -775,7 +708,14 @@ nbkd_status sort_queries(const Tree &t, const float *dq, uint32_t m, uint32_t *&
     if (!order || !tmp || !keys || !keys2) return NBKD_ENOMEM;
     {
         TimedScope ts("leaf_key", s);
-        leaf_key_kernel<<<(m + TB - 1) / TB, TB, 0, s>>>(view(t), dq, m, keys, order);
+        if (t.shape_len <= SHAPE_MAX) {
+            const unsigned blocks = (unsigned)std::min<uint64_t>((m + TB - 1) / TB, 8192);
+            leaf_key2_kernel<<<blocks, TB, 0, s>>>(t.splits, t.shape_c, t.shape_n, t.shape_len,
+                                                   (uint32_t)t.n8, (uint32_t)t.leaf, dq, m, keys,
+                                                   order);
+        } else {
+            leaf_key_kernel<<<(m + TB - 1) / TB, TB, 0, s>>>(view(t), dq, m, keys, order);
+        }
         NBKD_HIP(hipGetLastError());
     }
     TimedScope ts("sort", s);
@@ -826,9 +766,9 @@ nbkd_status query_knn(const Tree &t, const float *q, uint64_t m, int k, float *o
     }
     unsigned long long *stats = nullptr;
     if (stats_enabled()) {
-        stats = (unsigned long long *)t.ws.get(WS_STATS, 16, s);
+        stats = (unsigned long long *)t.ws.get(WS_STATS, NBKD_NSTATS * 8, s);
         if (!stats) return NBKD_ENOMEM;
-        NBKD_HIP(hipMemsetAsync(stats, 0, 16, s));
+        NBKD_HIP(hipMemsetAsync(stats, 0, NBKD_NSTATS * 8, s));
     }
     if (k > 64) { // all queries through the reference-exact lane-per-query kernel
         TimedScope ts("knn_exact", s);
@@ -847,7 +787,10 @@ nbkd_status query_knn(const Tree &t, const float *q, uint64_t m, int k, float *o
         NBKD_HIP(hipGetLastError());
     } else {
         TimedScope ts("knn", s);
-        if (k <= 8)
+        static const bool v1 = getenv("NBKD_KNN_V1") != nullptr;
+        if (!v1)
+            launch_knn_packet(t, dq, ord, mm, k, dd, di, stats, s);
+        else if (k <= 8)
             launch_knn<8>(t, dq, ord, mm, k, dd, di, stats, s);
         else if (k <= 16)
             launch_knn<16>(t, dq, ord, mm, k, dd, di, stats, s);
@@ -872,10 +815,10 @@ nbkd_status query_knn(const Tree &t, const float *q, uint64_t m, int k, float *o
         NBKD_HIP(hipGetLastError());
     }
     if (stats) {
-        unsigned long long h[2];
-        NBKD_HIP(hipMemcpyAsync(h, stats, 16, hipMemcpyDeviceToHost, s));
+        uint64_t h[NBKD_NSTATS];
+        NBKD_HIP(hipMemcpyAsync(h, stats, NBKD_NSTATS * 8, hipMemcpyDeviceToHost, s));
         NBKD_HIP(hipStreamSynchronize(s));
-        stats_store(h[0], h[1]);
+        stats_store(h);
     }
     if (!(flags & NBKD_OUTPUT_DEVICE)) {
         NBKD_HIP(hipMemcpyAsync(out_d, dd, m * (size_t)k * 4, hipMemcpyDeviceToHost, s));
