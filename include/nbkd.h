@@ -91,7 +91,7 @@ nbkd_status nbkd_query_ball_count(const nbkd_tree *tree, const float *q, uint64_
 /*
  * NEW: neighbour lists within r in CSR form.  out_offsets is (m+1,) uint64
  * (always host memory); out_idx receives offsets[m] original point indices,
- * each row sorted ascending.  Call with out_idx == NULL first to get
+ * each row in tree traversal order (unsorted; sort per row if needed).  Call with out_idx == NULL first to get
  * offsets[m] (the required capacity), then again with a buffer of that size.
  */
 nbkd_status nbkd_query_ball_csr(const nbkd_tree *tree, const float *q, uint64_t m, float r,
@@ -134,6 +134,51 @@ nbkd_status nbkd_stats_read(uint64_t *nodes_visited, uint64_t *points_scanned);
  * (lane-compacted) iterations, [4] top-k merges, [5] packets (waves),
  * [6] candidates merged (all lanes), [7] merges while some lane was still filling */
 nbkd_status nbkd_stats_read_all(uint64_t *out, int32_t n);
+
+/* ------------------------------------------------------------------ slabs (multi-GPU)
+ * NEW (the reference is single-node CPU only).  One process per
+ * GPU; the particles are cut into x-slabs [lo, hi) of the periodic box and each
+ * rank builds its tree over its own particles plus halo strips of width h
+ * received from its two ring neighbours.  All pointers here are device
+ * pointers on `device`; xyz arrays are (n, 3) row-major float32. */
+
+/* Replace the tree's point ids: idx[j] <- ids[idx[j]] for the n real points
+ * (ids has n entries; host memory unless NBKD_INPUT_DEVICE).  kNN and ball
+ * queries then return these ids (e.g. global particle ids of a slab tree). */
+nbkd_status nbkd_set_ids(nbkd_tree *tree, const uint32_t *ids, uint32_t flags, void *stream);
+
+/* Stable compaction of the points with lo <= x < hi into out_xyz / out_ids
+ * (ids may be NULL: then the row number is stored).  *count receives the
+ * number selected; with out_xyz or out_ids NULL only the count is computed. */
+nbkd_status nbkd_slab_select(const float *xyz, const uint32_t *ids, uint64_t n, float lo, float hi,
+                             float *out_xyz, uint32_t *out_ids, uint64_t capacity,
+                             uint64_t *count, int32_t device, void *stream);
+
+/* Exactness check of a slab-local kNN result: counts the queries (x in
+ * [lo, hi)) whose k-th distance (column k-1 of the (m, k) dist rows) is not
+ * strictly inside the local domain [lo - h, hi + h) along x.  Zero means every
+ * row equals the single-tree result over all particles. */
+nbkd_status nbkd_slab_violations(const float *q, const float *dist, uint64_t m, int32_t k,
+                                 float lo, float hi, float h, uint64_t *count, int32_t device,
+                                 void *stream);
+
+/* RCCL communicator (librccl.so.1 loaded on first use).  Rank 0 calls
+ * nbkd_comm_unique_id and distributes the NBKD_COMM_ID_BYTES bytes out of band
+ * (e.g. torch.distributed over gloo); every rank then calls nbkd_comm_init. */
+#define NBKD_COMM_ID_BYTES 128
+typedef struct nbkd_comm nbkd_comm;
+nbkd_status nbkd_comm_unique_id(uint8_t *out);
+nbkd_status nbkd_comm_init(const uint8_t *id, int32_t rank, int32_t world, int32_t device,
+                           nbkd_comm **out);
+/* One grouped set of point-to-point byte transfers: for each i, send
+ * send_bytes[i] from send[i] to rank send_peer[i] and receive recv_bytes[i]
+ * into recv[i] from rank recv_peer[i] (zero sizes skip).  Transfers between
+ * one pair of ranks are matched in posting order.  Enqueued on `stream`. */
+nbkd_status nbkd_comm_exchange(nbkd_comm *comm, int32_t npairs, const void *const *send,
+                               const uint64_t *send_bytes, const int32_t *send_peer,
+                               void *const *recv, const uint64_t *recv_bytes,
+                               const int32_t *recv_peer, void *stream);
+void nbkd_comm_free(nbkd_comm *comm);
 
 #ifdef __cplusplus
 }

@@ -28,7 +28,7 @@ ARCH = os.environ.get("NBKD_ARCH", "gfx950")
 # squared distances stop being bit-identical.
 HIP_FLAGS = ["--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
              "-Wall", "-Wno-unused-function", "-Wno-unused-const-variable"]
-SOURCES = ["api.cpp", "build.hip", "query.hip", "knn_packet.hip"]
+SOURCES = ["api.cpp", "build.hip", "query.hip", "knn_packet.hip", "slab.hip"]
 HEADERS = [os.path.join(CSRC, "internal.hpp"), os.path.join(CSRC, "metric.hpp"),
            os.path.join(ROOT, "include", "nbkd.h")]
 
@@ -60,7 +60,7 @@ def build_lib(force=False, verbose=True):
         if p.wait() != 0:
             raise RuntimeError("hipcc failed")
     if force or procs or _newer(LIB, objs):
-        cmd = [HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", LIB] + objs
+        cmd = [HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", LIB] + objs + ["-ldl"]
         if _run(cmd, verbose).wait() != 0:
             raise RuntimeError("link of libnbkd.so failed")
     return LIB

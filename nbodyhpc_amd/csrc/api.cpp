@@ -11,10 +11,6 @@
 
 #include "internal.hpp"
 
-struct nbkd_tree {
-    nbkd::Tree t;
-};
-
 namespace nbkd {
 
 namespace {

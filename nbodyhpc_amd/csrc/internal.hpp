@@ -139,3 +139,7 @@ __host__ __device__ inline float fkey_inv(uint32_t k) {
 }
 
 } // namespace nbkd
+
+struct nbkd_tree {
+    nbkd::Tree t;
+};

@@ -58,10 +58,15 @@ __device__ __forceinline__ float box_d2(float qx, float qy, float qz, const floa
 }
 
 // ------------------------------------------------------------------ register sorting networks
-template <int N>
+template <int N, bool IDX = true>
 __device__ __forceinline__ void ce(float (&d)[N], uint32_t (&i)[N], int a, int b) {
     // ascending: d[a] <= d[b]
     float da = d[a], db = d[b];
+    if constexpr (!IDX) { // distances only (timing experiments)
+        d[a] = fminf(da, db);
+        d[b] = fmaxf(da, db);
+        return;
+    }
     bool sw = db < da;
     d[a] = sw ? db : da;
     d[b] = sw ? da : db;
@@ -70,7 +75,7 @@ __device__ __forceinline__ void ce(float (&d)[N], uint32_t (&i)[N], int a, int b
     i[b] = sw ? ia : ib;
 }
 
-template <int N>
+template <int N, bool IDX = true>
 __device__ __forceinline__ void bitonic_sort(float (&d)[N], uint32_t (&i)[N]) {
 #pragma unroll
     for (int size = 2; size <= N; size <<= 1) {
@@ -81,9 +86,9 @@ __device__ __forceinline__ void bitonic_sort(float (&d)[N], uint32_t (&i)[N]) {
                 int b = a ^ stride;
                 if (b > a) {
                     if ((a & size) == 0)
-                        ce<N>(d, i, a, b);
+                        ce<N, IDX>(d, i, a, b);
                     else
-                        ce<N>(d, i, b, a);
+                        ce<N, IDX>(d, i, b, a);
                     if ((a & 3) == 3) __builtin_amdgcn_sched_barrier(0);
                 }
             }
@@ -95,7 +100,7 @@ __device__ __forceinline__ void bitonic_sort(float (&d)[N], uint32_t (&i)[N]) {
 // sched_barrier between groups of compare-exchanges: without it the scheduler
 // hoists a whole stage's compares and the live masks/temporaries push the
 // kernel past the VGPR budget of the occupancy it needs
-template <int N>
+template <int N, bool IDX = true>
 __device__ __forceinline__ void bitonic_merge(float (&d)[N], uint32_t (&i)[N]) {
 #pragma unroll
     for (int stride = N >> 1; stride > 0; stride >>= 1) {
@@ -103,7 +108,7 @@ __device__ __forceinline__ void bitonic_merge(float (&d)[N], uint32_t (&i)[N]) {
         for (int a = 0; a < N; ++a) {
             int b = a ^ stride;
             if (b > a) {
-                ce<N>(d, i, a, b);
+                ce<N, IDX>(d, i, a, b);
                 if ((a & 3) == 3) __builtin_amdgcn_sched_barrier(0);
             }
         }
