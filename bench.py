@@ -46,12 +46,12 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--n", type=float, default=1e8, help="particles per GPU")
+    p.add_argument("--particles", dest="n", type=float, default=1e8, help="particles per GPU")
     p.add_argument("--k", type=int, default=32)
     p.add_argument("--leafsize", type=int, default=32)
     p.add_argument("--box", type=float, default=1.0)
     p.add_argument("--seed", type=int, default=20261015)
-    p.add_argument("--cpu-sample", type=int, default=500_000,
+    p.add_argument("--cpu-sample", type=int, default=10_000_000,
                    help="queries timed on the CPU baseline (rank 0, N=1)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-parity", action="store_true")
@@ -112,10 +112,16 @@ def main():
         log(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
     from nbodyhpc_amd import capi, hip
 
+    hip.preload()  # before torch: see hip.preload
     dist = None
     if world > 1:
         import torch.distributed as dist  # gloo: CPU-side coordination only
         dist.init_process_group("gloo", rank=rank, world_size=world)
+    # rehearsal of the N > 1 path on a one-GPU box: every rank on device 0 and
+    # the halo staged over gloo (RCCL needs one GPU per rank)
+    same_dev = os.environ.get("NBKD_BENCH_SAME_DEVICE") == "1"
+    if same_dev:
+        local_rank = 0
     hip.set_device(local_rank)
 
     def barrier():
@@ -132,27 +138,47 @@ def main():
 
     n = int(args.n)
     k, L = args.k, args.box
+    stream = hip.Stream()
     t_gen = time.perf_counter()
+    ds = None
+    halo = None
     if world == 1:
         points = gen_uniform(n, args.seed, L)
         own = n
+        dev_pts = hip.DeviceArray.from_numpy(points)
+        n_local = n
     else:
         from nbodyhpc_amd import slab
-        points, own = slab.make_local_points(n, args.seed, L, rank, world, k)
-    log(f"rank {rank}: {own} own particles ({len(points)} with halo) generated in "
+        points = None
+        own_xyz, own_ids = slab.gen_slab_points(n, args.seed, L, rank, world)
+        own = n
+        comm = None if same_dev else slab.init_comm(dist, rank, world, local_rank, log)
+        ds = slab.DeviceSlab(own_xyz, own_ids, rank, world, L, local_rank, dist, comm, log)
+        del own_xyz, own_ids
+        h = slab.halo_width(n * world, k, L)
+        barrier()
+        t_x = time.perf_counter()
+        ds.exchange(h, stream.handle)
+        barrier()
+        halo = {"h": h, "exchange_ms": (time.perf_counter() - t_x) * 1e3}
+        dev_pts, n_local = ds.xyz, ds.n_local
+    log(f"rank {rank}: {own} own particles ({n_local} with halo) ready in "
         f"{time.perf_counter() - t_gen:.1f} s")
 
-    dev_pts = hip.DeviceArray.from_numpy(points)
-    stream = hip.Stream()
+    def build_tree():
+        t = capi.Tree(n=n_local, dev_ptr=dev_pts.ptr, leafsize=args.leafsize, boxsize=L,
+                      device=local_rank, stream=stream.handle)
+        if ds is not None:
+            t.set_ids(dev_ptr=ds.ids.ptr, stream=stream.handle)
+        return t
+
     # build: one untimed (code-object load), then timed builds
-    capi.Tree(n=len(points), dev_ptr=dev_pts.ptr, leafsize=args.leafsize, boxsize=L,
-              device=local_rank, stream=stream.handle).close()
+    build_tree().close()
     build_ms = []
     for _ in range(2):
         hip.synchronize()
         t0 = time.perf_counter()
-        tree = capi.Tree(n=len(points), dev_ptr=dev_pts.ptr, leafsize=args.leafsize, boxsize=L,
-                         device=local_rank, stream=stream.handle)
+        tree = build_tree()
         hip.synchronize()
         build_ms.append((time.perf_counter() - t0) * 1e3)
         if _ == 0:
@@ -168,6 +194,21 @@ def main():
     for _ in range(args.warmup):
         step()
     stream.synchronize()
+    if ds is not None:
+        # exactness of the slab-local result; widen the halo until every row is exact
+        for attempt in range(4):
+            step()
+            stream.synchronize()
+            v = int(allmax(float(ds.violations(od.ptr, k, stream.handle))))
+            halo["violations"] = v
+            if v == 0:
+                break
+            log(f"{v} rows reach past the halo (h={ds.h:.3g}); widening")
+            tree.close()
+            ds.exchange(ds.h * 2.0, stream.handle)
+            dev_pts, n_local = ds.xyz, ds.n_local
+            tree = build_tree()
+        halo.update({"h": ds.h, "local_points": n_local, "transport": ds.transport})
     capi.timing_enable(True)
     capi.timing_reset()
     barrier()
@@ -208,10 +249,15 @@ def main():
     knn_avg_ms = knn_ms / max(knn_launches, 1)
     achieved = bq * own / (knn_avg_ms * 1e-3) / 1e9
     traffic = None
-    pmc_path = os.path.join(ROOT, "profiles", "pmc_knn.json")
-    if os.path.exists(pmc_path):
+    # HBM bytes per knn launch from the newest committed rocprofv3 PMC summary
+    # (profiles/rNN_pmc_knn.json: FETCH_SIZE x2 (gfx950) + WRITE_SIZE passes)
+    import glob
+    pmcs = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_knn.json")))
+    if pmcs:
         try:
-            traffic = json.load(open(pmc_path)).get("hbm_bytes_per_launch")
+            pm = json.load(open(pmcs[-1]))
+            if pm.get("n_particles") == own and pm.get("k") == k:
+                traffic = pm.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
     cpu = None
@@ -238,11 +284,12 @@ def main():
             "queries_per_step": own * world,
             "parallelism": "single" if world == 1 else f"x-slab x{world} + RCCL halo",
         },
+        "halo": halo,
         "build_ms": build_ms,
         "roofline": {
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-            "kernel": "knn_kernel<32,periodic>",
+            "kernel": "knn4_kernel<32,periodic> (nbodyhpc_amd/csrc/knn_packet.hip)",
             "kernel_ms_per_launch": knn_avg_ms,
             "bytes_per_query": bq,
         },

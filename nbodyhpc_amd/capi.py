@@ -53,7 +53,17 @@ _PROTOS = {
     "nbkd_stats_enable": (_i32, [_i32]),
     "nbkd_stats_read": (_i32, [ctypes.POINTER(_u64), ctypes.POINTER(_u64)]),
     "nbkd_stats_read_all": (_i32, [ctypes.POINTER(_u64), _i32]),
+    "nbkd_set_ids": (_i32, [_c_p, _c_p, _u32, _c_p]),
+    "nbkd_slab_select": (_i32, [_c_p, _c_p, _u64, ctypes.c_float, ctypes.c_float, _c_p, _c_p,
+                                _u64, ctypes.POINTER(_u64), _i32, _c_p]),
+    "nbkd_slab_violations": (_i32, [_c_p, _c_p, _u64, _i32, ctypes.c_float, ctypes.c_float,
+                                    ctypes.c_float, ctypes.POINTER(_u64), _i32, _c_p]),
+    "nbkd_comm_unique_id": (_i32, [_c_p]),
+    "nbkd_comm_init": (_i32, [_c_p, _i32, _i32, _i32, ctypes.POINTER(_c_p)]),
+    "nbkd_comm_exchange": (_i32, [_c_p, _i32, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p]),
+    "nbkd_comm_free": (None, [_c_p]),
 }
+COMM_ID_BYTES = 128
 
 
 def header_symbols() -> list[str]:
@@ -153,6 +163,14 @@ class Tree:
         flags = NBKD_OUTPUT_DEVICE | (NBKD_INPUT_DEVICE if input_device else 0)
         _check(lib().nbkd_query_knn(self.h, q_ptr, int(m), int(k), d_ptr, i_ptr, flags, stream))
 
+    def set_ids(self, ids=None, *, dev_ptr=None, stream=None):
+        """Map the tree's point ids through `ids` (host array or device pointer)."""
+        if dev_ptr is not None:
+            _check(lib().nbkd_set_ids(self.h, dev_ptr, NBKD_INPUT_DEVICE, stream))
+        else:
+            a = np.ascontiguousarray(ids, dtype=np.uint32)
+            _check(lib().nbkd_set_ids(self.h, a.ctypes.data, 0, stream))
+
     def ball_count(self, q, r):
         q = _host_f32(q)
         out = np.empty(q.shape[0], np.uint32)
@@ -209,3 +227,54 @@ def stats_read_all():
     arr = (_u64 * len(STATS_NAMES))()
     _check(lib().nbkd_stats_read_all(arr, len(STATS_NAMES)))
     return dict(zip(STATS_NAMES, [int(v) for v in arr]))
+
+
+# ------------------------------------------------------------------ slabs / RCCL
+def slab_select(xyz_ptr, ids_ptr, n, lo, hi, out_xyz_ptr=None, out_ids_ptr=None, capacity=0,
+                device=0, stream=None):
+    """Device-side stable selection of points with lo <= x < hi; returns the count."""
+    c = _u64()
+    _check(lib().nbkd_slab_select(xyz_ptr, ids_ptr, int(n), float(lo), float(hi), out_xyz_ptr,
+                                  out_ids_ptr, int(capacity), ctypes.byref(c), int(device), stream))
+    return c.value
+
+
+def slab_violations(q_ptr, dist_ptr, m, k, lo, hi, h, device=0, stream=None):
+    c = _u64()
+    _check(lib().nbkd_slab_violations(q_ptr, dist_ptr, int(m), int(k), float(lo), float(hi),
+                                      float(h), ctypes.byref(c), int(device), stream))
+    return c.value
+
+
+def comm_unique_id() -> bytes:
+    buf = (ctypes.c_uint8 * COMM_ID_BYTES)()
+    _check(lib().nbkd_comm_unique_id(buf))
+    return bytes(buf)
+
+
+class Comm:
+    """RCCL communicator over librccl (dlopen'ed by libnbkd)."""
+
+    def __init__(self, uid: bytes, rank: int, world: int, device: int):
+        buf = (ctypes.c_uint8 * COMM_ID_BYTES).from_buffer_copy(uid)
+        h = _c_p()
+        _check(lib().nbkd_comm_init(buf, int(rank), int(world), int(device), ctypes.byref(h)))
+        self.h = h
+
+    def exchange(self, pairs, stream=None):
+        """pairs: list of (send_ptr, send_bytes, send_peer, recv_ptr, recv_bytes, recv_peer)."""
+        n = len(pairs)
+        sp = (_c_p * n)(*[p[0] for p in pairs])
+        sb = (_u64 * n)(*[int(p[1]) for p in pairs])
+        speer = (_i32 * n)(*[int(p[2]) for p in pairs])
+        rp = (_c_p * n)(*[p[3] for p in pairs])
+        rb = (_u64 * n)(*[int(p[4]) for p in pairs])
+        rpeer = (_i32 * n)(*[int(p[5]) for p in pairs])
+        _check(lib().nbkd_comm_exchange(self.h, n, sp, sb, speer, rp, rb, rpeer, stream))
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().nbkd_comm_free(self.h)
+            self.h = None
+
+    __del__ = close

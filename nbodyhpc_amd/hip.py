@@ -46,6 +46,17 @@ def _hip():
     return _LIB
 
 
+def preload():
+    """Load the ROCm 7.2 HIP runtime and libnbkd.so NOW.  Call before anything
+    imports torch: torch's bundled libamdhip64.so.7 / libhsa-runtime64.so.1
+    (ROCm 7.0) carry the same sonames, so whichever loads first serves the
+    process; loading ours second fails (missing ROCR_1 symbols)."""
+    _hip()
+    from . import capi
+
+    capi.lib()
+
+
 def _ok(rc, what):
     if rc != 0:
         raise RuntimeError(f"{what}: {_hip().hipGetErrorString(rc).decode()}")
@@ -105,6 +116,12 @@ class DeviceArray:
             self.ptr = None
 
     __del__ = free
+
+
+def memcpy(dst_ptr, src_ptr, nbytes, kind=D2D):
+    """Synchronous copy between raw pointers (kind: H2D / D2H / D2D)."""
+    if nbytes:
+        _ok(_hip().hipMemcpy(dst_ptr, src_ptr, int(nbytes), int(kind)), "hipMemcpy")
 
 
 class Stream:

@@ -1,0 +1,270 @@
+"""Slab decomposition of the periodic box across ranks.
+
+One process per GPU.  Rank r of W owns the particles with x in the slab
+[lo, hi) = [r L / W, (r+1) L / W).  Its kd-tree is built over its own particles
+plus two halo strips of width h received from its ring neighbours: the
+right neighbour's particles with x in [lo', lo' + h) and the left neighbour's
+with x in [hi' - h, hi').  Halo particles keep their periodic coordinates (the
+tree is periodic over the whole box, so min-image distances between local
+points are the true ones) and their global ids (`nbkd_set_ids`), so the local
+kNN of an own particle returns global ids.  A row is exact (equal to the
+single-tree result over all W slabs) iff its k-th distance stays strictly
+inside [lo - h, hi + h) along x (`nbkd_slab_violations`); `knn_setup` widens
+h and rebuilds until every row is exact.
+
+The bulk transfer is RCCL point-to-point over xGMI (`nbkd_comm_exchange`, one
+grouped send/recv set with each neighbour).  Strip sizes (8 bytes per
+neighbour) go over torch.distributed/gloo, which also carries the RCCL unique
+id.  `exchange_host` is the same protocol on host arrays over gloo: the path
+the world-size-2 CPU tests run and the fallback when RCCL cannot start.
+"""
+from __future__ import annotations
+
+import math
+import sys
+
+import numpy as np
+
+_TAG_RIGHTWARD, _TAG_LEFTWARD = 17, 18
+
+
+def slab_bounds(rank: int, world: int, box: float):
+    """[lo, hi) of `rank` as float32 values (the comparisons run in f32)."""
+    lo = np.float32(box * rank / world)
+    hi = np.float32(box) if rank == world - 1 else np.float32(box * (rank + 1) / world)
+    return float(lo), float(hi)
+
+
+def halo_width(n_total: int, k: int, box: float, factor: float = 2.5) -> float:
+    """factor x the mean k-th neighbour radius of a uniform density."""
+    rho = n_total / box ** 3
+    r_k = (k / (4.0 / 3.0 * math.pi * rho)) ** (1.0 / 3.0)
+    return float(factor * r_k)
+
+
+def gen_slab_points(n_per: int, seed: int, box: float, rank: int, world: int):
+    """Uniform particles of rank `rank`'s slab; the union over ranks is a
+    uniform sample of the box.  Global ids are rank * n_per + i."""
+    lo, hi = slab_bounds(rank, world, box)
+    lo32, hi32 = np.float32(lo), np.float32(hi)
+    top = np.nextafter(hi32, np.float32(-np.inf))
+    rng = np.random.Generator(np.random.PCG64([seed, rank]))
+    out = np.empty((n_per, 3), np.float32)
+    chunk = 1 << 24
+    for s in range(0, n_per, chunk):
+        e = min(n_per, s + chunk)
+        u = rng.uniform(0.0, 1.0, size=(e - s, 3))
+        out[s:e, 0] = np.clip((lo + (hi - lo) * u[:, 0]).astype(np.float32), lo32, top)
+        out[s:e, 1:] = (box * u[:, 1:]).astype(np.float32)
+    out[:, 1:] = np.minimum(out[:, 1:], np.nextafter(np.float32(box), np.float32(-np.inf)))
+    ids = (np.uint64(rank) * np.uint64(n_per) + np.arange(n_per, dtype=np.uint64))
+    if n_per and ids[-1] > np.uint64(0xFFFFFFFE):
+        raise ValueError("global ids exceed uint32")
+    return out, ids.astype(np.uint32)
+
+
+def neighbours(rank: int, world: int):
+    return (rank - 1) % world, (rank + 1) % world
+
+
+def _strip_counts(dist, rank, world, to_right: int, to_left: int):
+    """all-gather of (to_right, to_left); returns (from_left, from_right)."""
+    import torch
+
+    left, right = neighbours(rank, world)
+    mine = torch.tensor([to_right, to_left], dtype=torch.int64)
+    allc = [torch.zeros(2, dtype=torch.int64) for _ in range(world)]
+    dist.all_gather(allc, mine)
+    return int(allc[left][0]), int(allc[right][1])
+
+
+def _host_sendrecv(dist, rank, world, send_r, send_l, n_fl, n_fr, dtype, cols):
+    """gloo point-to-point: send_r -> right, send_l -> left; receive from left
+    (its rightward strip) and from right (its leftward strip)."""
+    import torch
+
+    left, right = neighbours(rank, world)
+    shape = (lambda n: (n, cols)) if cols > 1 else (lambda n: (n,))
+    rl = torch.empty(shape(n_fl), dtype=dtype)
+    rr = torch.empty(shape(n_fr), dtype=dtype)
+    reqs = []
+    if len(send_r):
+        reqs.append(dist.isend(torch.from_numpy(np.ascontiguousarray(send_r)), right,
+                               tag=_TAG_RIGHTWARD))
+    if len(send_l):
+        reqs.append(dist.isend(torch.from_numpy(np.ascontiguousarray(send_l)), left,
+                               tag=_TAG_LEFTWARD))
+    if n_fl:
+        reqs.append(dist.irecv(rl, left, tag=_TAG_RIGHTWARD))
+    if n_fr:
+        reqs.append(dist.irecv(rr, right, tag=_TAG_LEFTWARD))
+    for r in reqs:
+        r.wait()
+    return rl.numpy(), rr.numpy()
+
+
+def exchange_host(own_xyz, own_ids, rank, world, box, h, dist):
+    """Host-array halo exchange over gloo.  Returns (local_xyz, local_ids) with
+    the own particles first, then the strip from the left neighbour, then the
+    strip from the right neighbour."""
+    if world == 1:
+        return own_xyz, own_ids
+    lo, hi = slab_bounds(rank, world, box)
+    x = own_xyz[:, 0]
+    mr = x >= np.float32(hi - h)
+    ml = x < np.float32(lo + h)
+    n_fl, n_fr = _strip_counts(dist, rank, world, int(mr.sum()), int(ml.sum()))
+    import torch
+
+    fl_x, fr_x = _host_sendrecv(dist, rank, world, own_xyz[mr], own_xyz[ml], n_fl, n_fr,
+                                torch.float32, 3)
+    fl_i, fr_i = _host_sendrecv(dist, rank, world, own_ids[mr].astype(np.int32),
+                                own_ids[ml].astype(np.int32), n_fl, n_fr, torch.int32, 1)
+    xyz = np.concatenate([own_xyz, fl_x, fr_x])
+    ids = np.concatenate([own_ids, fl_i.astype(np.uint32), fr_i.astype(np.uint32)])
+    return xyz, ids
+
+
+def violations_host(q_xyz, kth_dist, rank, world, box, h):
+    """numpy statement of nbkd_slab_violations (slab.hip violations_kernel)."""
+    if world == 1:
+        return 0
+    lo, hi = slab_bounds(rank, world, box)
+    x = q_xyz[:, 0].astype(np.float32)
+    margin = np.minimum(x - np.float32(lo - h), np.float32(hi + h) - x)
+    ok = kth_dist.astype(np.float32) < margin * np.float32(1.0 - 4e-7)
+    return int((~ok).sum())
+
+
+# ------------------------------------------------------------------ device path
+class DeviceSlab:
+    """Own particles + halo on the GPU for one rank (device arrays via hip.py)."""
+
+    def __init__(self, own_xyz, own_ids, rank, world, box, device, dist=None, comm=None,
+                 log=None):
+        from . import hip
+
+        self.rank, self.world, self.box, self.device = rank, world, box, device
+        self.dist, self.comm = dist, comm
+        self.log = log or (lambda *a: None)
+        self.n_own = len(own_xyz)
+        self.lo, self.hi = slab_bounds(rank, world, box)
+        self.own_xyz = hip.DeviceArray.from_numpy(own_xyz)
+        self.own_ids = hip.DeviceArray.from_numpy(own_ids)
+        self.xyz = self.ids = None
+        self.n_local = self.n_own
+        self.h = 0.0
+        self.transport = "none"
+
+    def exchange(self, h, stream=None):
+        """(Re)build the local arrays with halo width h."""
+        from . import capi, hip
+
+        self.h = float(h)
+        if self.world == 1:
+            self.xyz, self.ids, self.n_local = self.own_xyz, self.own_ids, self.n_own
+            return
+        lo, hi = self.lo, self.hi
+        dev, s = self.device, stream
+        sel = {}
+        for name, (a, b) in (("r", (hi - h, hi)), ("l", (lo, lo + h))):
+            n = capi.slab_select(self.own_xyz.ptr, self.own_ids.ptr, self.n_own, a, b,
+                                 device=dev, stream=s)
+            bx = hip.DeviceArray((max(n, 1), 3), np.float32)
+            bi = hip.DeviceArray((max(n, 1),), np.uint32)
+            capi.slab_select(self.own_xyz.ptr, self.own_ids.ptr, self.n_own, a, b, bx.ptr, bi.ptr,
+                             n, device=dev, stream=s)
+            sel[name] = (n, bx, bi)
+        n_fl, n_fr = _strip_counts(self.dist, self.rank, self.world, sel["r"][0], sel["l"][0])
+        n_loc = self.n_own + n_fl + n_fr
+        xyz = hip.DeviceArray((n_loc, 3), np.float32)
+        ids = hip.DeviceArray((n_loc,), np.uint32)
+        hip.memcpy(xyz.ptr, self.own_xyz.ptr, self.n_own * 12)
+        hip.memcpy(ids.ptr, self.own_ids.ptr, self.n_own * 4)
+        o_fl, o_fr = self.n_own, self.n_own + n_fl
+        left, right = neighbours(self.rank, self.world)
+        done = False
+        if self.comm is not None:
+            nr, rx, ri = sel["r"]
+            nl, lx, li = sel["l"]
+            pairs = [
+                (rx.ptr, nr * 12, right, xyz.ptr + o_fl * 12, n_fl * 12, left),
+                (lx.ptr, nl * 12, left, xyz.ptr + o_fr * 12, n_fr * 12, right),
+                (ri.ptr, nr * 4, right, ids.ptr + o_fl * 4, n_fl * 4, left),
+                (li.ptr, nl * 4, left, ids.ptr + o_fr * 4, n_fr * 4, right),
+            ]
+            try:
+                self.comm.exchange(pairs, stream=s)
+                hip.synchronize()
+                done = True
+                self.transport = "rccl"
+            except Exception as e:  # reported; the host path below is exact too
+                self.log(f"rank {self.rank}: RCCL exchange failed ({e}); staging over gloo")
+        if not done:
+            sr = (sel["r"][1].numpy_head(sel["r"][0]), sel["r"][2].numpy_head(sel["r"][0]))
+            sl = (sel["l"][1].numpy_head(sel["l"][0]), sel["l"][2].numpy_head(sel["l"][0]))
+            import torch
+
+            fl_x, fr_x = _host_sendrecv(self.dist, self.rank, self.world, sr[0], sl[0], n_fl,
+                                        n_fr, torch.float32, 3)
+            fl_i, fr_i = _host_sendrecv(self.dist, self.rank, self.world,
+                                        sr[1].astype(np.int32), sl[1].astype(np.int32), n_fl,
+                                        n_fr, torch.int32, 1)
+            for arr, off, item in ((fl_x, o_fl, 12), (fr_x, o_fr, 12)):
+                a = np.ascontiguousarray(arr, np.float32)
+                hip.memcpy(xyz.ptr + off * item, a.ctypes.data, a.nbytes, hip.H2D)
+            for arr, off in ((fl_i, o_fl), (fr_i, o_fr)):
+                a = np.ascontiguousarray(arr).view(np.uint32)
+                hip.memcpy(ids.ptr + off * 4, a.ctypes.data, a.nbytes, hip.H2D)
+            self.transport = "gloo-staged"
+        for v in sel.values():
+            v[1].free()
+            v[2].free()
+        self.xyz, self.ids, self.n_local = xyz, ids, n_loc
+
+    def violations(self, dist_ptr, k, stream=None):
+        from . import capi
+
+        if self.world == 1:
+            return 0
+        return capi.slab_violations(self.xyz.ptr, dist_ptr, self.n_own, k, self.lo, self.hi,
+                                    self.h, device=self.device, stream=stream)
+
+
+def init_comm(dist, rank, world, device, log=None):
+    """RCCL communicator (unique id broadcast over gloo); None if it cannot start."""
+    from . import capi
+
+    log = log or (lambda *a: None)
+    if world == 1:
+        return None
+    import torch
+
+    buf = torch.zeros(capi.COMM_ID_BYTES, dtype=torch.uint8)
+    ok = torch.zeros(1, dtype=torch.int64)
+    if rank == 0:
+        try:
+            buf = torch.tensor(list(capi.comm_unique_id()), dtype=torch.uint8)
+            ok[0] = 1
+        except Exception as e:
+            log(f"RCCL unavailable: {e}")
+    dist.broadcast(ok, 0)
+    if not int(ok[0]):
+        return None
+    dist.broadcast(buf, 0)
+    try:
+        c = capi.Comm(bytes(buf.numpy().tobytes()), rank, world, device)
+    except Exception as e:
+        log(f"rank {rank}: ncclCommInitRank failed: {e}")
+        c = None
+    flag = torch.tensor([1 if c is not None else 0], dtype=torch.int64)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    if not int(flag[0]):
+        if c is not None:
+            c.close()
+        return None
+    return c
+
+
+def log_stderr(*a):
+    print("[slab]", *a, file=sys.stderr, flush=True)

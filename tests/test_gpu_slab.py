@@ -1,0 +1,143 @@
+"""Slab entry points of the C ABI on the GPU.
+
+Single-GPU checks of strip selection, id remapping, the exactness check and
+the RCCL exchange (a self-exchange on a world-size-1 communicator), plus a
+world-size-2 slab kNN with both ranks on the one GPU of the box (halo staged
+over gloo, since RCCL needs one GPU per rank) compared with the single-tree
+oracle result.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from nbodyhpc_amd import slab
+
+pytestmark = pytest.mark.gpu
+
+
+def test_slab_select_stable(gpu):
+    from nbodyhpc_amd import hip
+    rng = np.random.default_rng(5)
+    n = 50_001
+    xyz = rng.uniform(0, 1, (n, 3)).astype(np.float32)
+    ids = rng.permutation(n).astype(np.uint32)
+    dx, di = hip.DeviceArray.from_numpy(xyz), hip.DeviceArray.from_numpy(ids)
+    lo, hi = 0.25, 0.3125
+    c = gpu.slab_select(dx.ptr, di.ptr, n, lo, hi)
+    m = (xyz[:, 0] >= np.float32(lo)) & (xyz[:, 0] < np.float32(hi))
+    assert c == int(m.sum())
+    ox, oi = hip.DeviceArray((c, 3), np.float32), hip.DeviceArray((c,), np.uint32)
+    assert gpu.slab_select(dx.ptr, di.ptr, n, lo, hi, ox.ptr, oi.ptr, c) == c
+    assert np.array_equal(ox.numpy(), xyz[m])
+    assert np.array_equal(oi.numpy(), ids[m])
+    with pytest.raises(gpu.NbkdError):
+        gpu.slab_select(dx.ptr, di.ptr, n, lo, hi, ox.ptr, oi.ptr, c - 1)
+
+
+def test_set_ids_maps_query_results(gpu):
+    rng = np.random.default_rng(6)
+    pts = rng.uniform(0, 1, (30_000, 3)).astype(np.float32)
+    ids = (rng.permutation(30_000) + 1_000_000).astype(np.uint32)
+    t = gpu.Tree(pts, leafsize=32, boxsize=1.0)
+    d0, i0 = t.query(pts[:2000], 16)
+    t.set_ids(ids)
+    d1, i1 = t.query(pts[:2000], 16)
+    assert np.array_equal(d0, d1)
+    assert np.array_equal(i1, ids[i0])
+    t.close()
+
+
+def test_violations_kernel_matches_host(gpu):
+    from nbodyhpc_amd import hip
+    rng = np.random.default_rng(8)
+    world, rank, box, k = 4, 1, 1.0, 4
+    lo, hi = slab.slab_bounds(rank, world, box)
+    m = 20_000
+    q = rng.uniform(0, 1, (m, 3)).astype(np.float32)
+    q[:, 0] = rng.uniform(lo, hi, m).astype(np.float32)
+    dist = rng.uniform(0, 0.02, (m, k)).astype(np.float32)
+    h = 0.01
+    want = slab.violations_host(q, dist[:, -1], rank, world, box, h)
+    assert 0 < want < m
+    dq, dd = hip.DeviceArray.from_numpy(q), hip.DeviceArray.from_numpy(dist)
+    got = gpu.slab_violations(dq.ptr, dd.ptr, m, k, lo, hi, h)
+    assert got == want
+
+
+def test_rccl_self_exchange(gpu):
+    """dlopen of librccl, communicator init and a grouped send/recv (to self)."""
+    from nbodyhpc_amd import hip
+    uid = gpu.comm_unique_id()
+    assert len(uid) == gpu.COMM_ID_BYTES
+    comm = gpu.Comm(uid, 0, 1, 0)
+    a = hip.DeviceArray.from_numpy(np.arange(1000, dtype=np.uint32))
+    b = hip.DeviceArray((1000,), np.uint32)
+    s = hip.Stream()
+    comm.exchange([(a.ptr, 4000, 0, b.ptr, 4000, 0)], stream=s.handle)
+    s.synchronize()
+    assert np.array_equal(b.numpy(), np.arange(1000, dtype=np.uint32))
+    comm.close()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, n_per, k, outdir):
+    from nbodyhpc_amd import capi, hip
+
+    hip.preload()  # the ROCm 7.2 runtime must load before torch's bundled one
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        hip.set_device(0)
+        xyz, ids = slab.gen_slab_points(n_per, 21, 1.0, rank, world)
+        ds = slab.DeviceSlab(xyz, ids, rank, world, 1.0, 0, dist, comm=None)
+        h = slab.halo_width(n_per * world, k, 1.0)
+        ds.exchange(h)
+        t = capi.Tree(n=ds.n_local, dev_ptr=ds.xyz.ptr, leafsize=32, boxsize=1.0, device=0)
+        t.set_ids(dev_ptr=ds.ids.ptr)
+        od = hip.DeviceArray((n_per, k), np.float32)
+        oi = hip.DeviceArray((n_per, k), np.uint32)
+        t.query_device(ds.xyz.ptr, n_per, k, od.ptr, oi.ptr)
+        hip.synchronize()
+        v = ds.violations(od.ptr, k)
+        np.savez(os.path.join(outdir, f"r{rank}.npz"), d=od.numpy(), i=oi.numpy(), v=v,
+                 nloc=ds.n_local, transport=ds.transport)
+        t.close()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_slab_knn_on_one_gpu(gpu, oracle, tmp_path):
+    import multiprocessing as mp
+
+    from tests.parity import assert_knn_equal
+    world, n_per, k = 2, 60_000, 32
+    ctx = mp.get_context("spawn")  # plain multiprocessing: torch must not load first
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n_per, k, str(tmp_path)))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=300)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    parts = [slab.gen_slab_points(n_per, 21, 1.0, r, world)[0] for r in range(world)]
+    allp = np.concatenate(parts)
+    gd, gi = oracle.tree(allp, 32, 1.0).query(allp, k, workers=8)
+    for r in range(world):
+        res = np.load(os.path.join(tmp_path, f"r{r}.npz"))
+        assert int(res["v"]) == 0 and res["nloc"] > n_per
+        assert str(res["transport"]) == "gloo-staged"
+        sl = slice(r * n_per, (r + 1) * n_per)
+        assert_knn_equal(res["d"], res["i"], gd[sl], gi[sl], allp, parts[r], 1.0)
