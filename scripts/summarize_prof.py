@@ -1,0 +1,80 @@
+"""Turn one gpu_round.sh output directory into the committed profile summaries.
+
+    python scripts/summarize_prof.py gpurun_out/<tag> <round-tag>
+
+writes
+  profiles/<round>_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary (copied)
+  profiles/<round>_pmc_knn.json       HBM bytes per knn launch from the FETCH_SIZE and
+                                      WRITE_SIZE passes (separate runs), gfx950-corrected
+  profiles/<round>_bench.json         the bench line of the same call
+FETCH_SIZE / WRITE_SIZE are rocprofv3 derived counters in KiB; on gfx950 FETCH_SIZE
+reports half the bytes of wide coalesced reads (MI355X_MICROARCH.md, HBM section),
+so fetched bytes = 2 * 1024 * FETCH_SIZE.  WRITE_SIZE is taken as reported.
+"""
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+
+
+def find(d, pat):
+    hits = sorted(glob.glob(os.path.join(d, "**", pat), recursive=True))
+    return hits[-1] if hits else None
+
+
+def per_dispatch(path, regex):
+    vals = {}
+    with open(path) as f:
+        for row in csv.DictReader(f):
+            if regex not in row["Kernel_Name"]:
+                continue
+            key = row["Dispatch_Id"]
+            vals[key] = vals.get(key, 0.0) + float(row["Counter_Value"])
+    return list(vals.values())
+
+
+def main():
+    src, tag = sys.argv[1], sys.argv[2]
+    regex = sys.argv[3] if len(sys.argv) > 3 else "knn4"
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    prof = os.path.join(root, "profiles")
+    stats = find(os.path.join(src, "trace"), "*kernel_stats.csv")
+    if stats:
+        shutil.copy(stats, os.path.join(prof, f"{tag}_kernel_stats.csv"))
+    bench = os.path.join(src, "bench.json")
+    b = None
+    if os.path.exists(bench) and os.path.getsize(bench) > 0:
+        b = json.loads(open(bench).read().strip().splitlines()[-1])
+        json.dump(b, open(os.path.join(prof, f"{tag}_bench.json"), "w"), indent=1)
+    fetch = find(os.path.join(src, "fetch"), "*counter_collection.csv")
+    write = find(os.path.join(src, "write"), "*counter_collection.csv")
+    if fetch and write:
+        fv = per_dispatch(fetch, regex)
+        wv = per_dispatch(write, regex)
+        f_kib = sum(fv) / len(fv)
+        w_kib = sum(wv) / len(wv)
+        hbm = 2.0 * 1024.0 * f_kib + 1024.0 * w_kib
+        cfg = (b or {}).get("config", {})
+        out = {
+            "kernel": (b or {}).get("roofline", {}).get("kernel", regex),
+            "command": f"rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE --kernel-include-regex {regex} -- "
+                       "python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-parity",
+            "n_particles": cfg.get("n_particles_per_gpu", 100_000_000), "k": cfg.get("k", 32),
+            "dispatches": [len(fv), len(wv)],
+            "FETCH_SIZE_KiB_per_launch": f_kib, "WRITE_SIZE_KiB_per_launch": w_kib,
+            "fetch_bytes_per_launch_corrected": 2.0 * 1024.0 * f_kib,
+            "write_bytes_per_launch": 1024.0 * w_kib,
+            "hbm_bytes_per_launch": hbm,
+            "note": "FETCH_SIZE doubled (gfx950 wide-read correction); Infinity-Cache hits "
+                    "are counted by these counters, not excluded",
+        }
+        json.dump(out, open(os.path.join(prof, f"{tag}_pmc_knn.json"), "w"), indent=1)
+        print(json.dumps(out, indent=1))
+    if b:
+        print(json.dumps(b)[:2000])
+
+
+if __name__ == "__main__":
+    main()
