@@ -7,7 +7,7 @@
 
 One step = one pass of the hot path over one batch: every local particle
 queried for its k=32 nearest neighbours (query bucketing + radix sort + packet
-kNN kernel), inputs and outputs resident in HBM.  N > 1: the particles are
+collect / select kernels), inputs and outputs resident in HBM.  N > 1: the particles are
 sharded by x-slab, each rank holds its slab plus a periodic halo exchanged
 over RCCL at setup, and queries its own particles (weak scaling: 1e8 per GPU).
 
@@ -223,6 +223,9 @@ def main():
     sort_ms, _ = capi.timing_read("sort")
     key_ms, _ = capi.timing_read("leaf_key")
     oob_ms, _ = capi.timing_read("knn_outside_box")
+    fb_ms, _ = capi.timing_read("knn_fallback")
+    col_ms, col_launches = capi.timing_read("knn_collect")
+    sel_ms, _ = capi.timing_read("knn_select")
     capi.timing_enable(False)
     elapsed_max = allmax(elapsed)
 
@@ -246,8 +249,13 @@ def main():
     value = total_q / elapsed_max
     ms_per_step = elapsed_max / args.steps * 1e3
     bq = bytes_per_query(k)
-    knn_avg_ms = knn_ms / max(knn_launches, 1)
-    achieved = bq * own / (knn_avg_ms * 1e-3) / 1e9
+    # dominant kernel: knn_collect_kernel, launched once per query batch (the
+    # candidate-column budget); achieved = algorithmic bytes of the queries one
+    # launch processes / that launch's average duration (HIP events, launch stream)
+    col_launches = max(col_launches, 1)
+    col_avg_ms = col_ms / col_launches
+    q_per_launch = own * args.steps / col_launches
+    achieved = bq * q_per_launch / (col_avg_ms * 1e-3) / 1e9
     traffic = None
     # HBM bytes per knn launch from the newest committed rocprofv3 PMC summary
     # (profiles/rNN_pmc_knn.json: FETCH_SIZE x2 (gfx950) + WRITE_SIZE passes)
@@ -256,7 +264,9 @@ def main():
     if pmcs:
         try:
             pm = json.load(open(pmcs[-1]))
-            if pm.get("n_particles") == own and pm.get("k") == k:
+            if (pm.get("n_particles") == own and pm.get("k") == k
+                    and str(pm.get("kernel", "")).startswith("knn_collect")
+                    and pm.get("queries_per_launch") == q_per_launch):
                 traffic = pm.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
@@ -289,19 +299,24 @@ def main():
         "roofline": {
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-            "kernel": "knn4_kernel<32,periodic> (nbodyhpc_amd/csrc/knn_packet.hip)",
-            "kernel_ms_per_launch": knn_avg_ms,
+            "kernel": "knn_collect_kernel<periodic> (nbodyhpc_amd/csrc/knn_collect.hip)",
+            "kernel_ms_per_launch": col_avg_ms,
+            "launches_per_step": col_launches / args.steps,
+            "queries_per_launch": q_per_launch,
             "bytes_per_query": bq,
         },
         "breakdown_ms_per_step": {
             "leaf_key": key_ms / args.steps, "sort": sort_ms / args.steps,
-            "knn": knn_ms / args.steps, "outside_box_check": oob_ms / args.steps,
+            "knn": knn_ms / args.steps, "knn_collect": col_ms / args.steps,
+            "knn_select": sel_ms / args.steps, "outside_box_check": oob_ms / args.steps,
+            "fallback": fb_ms / args.steps,
         },
         "traversal_per_query": {"nodes_visited": nodes_vis / own,
                                 "distance_evals": pts_scanned / own},
         "traversal_per_packet": {kk: st[kk] / max(st["packets"], 1)
-                                 for kk in ("dense_rounds", "sparse_iters", "merges", "candidates",
-                                           "fill_merges")},
+                                 for kk in ("dense_steps", "sparse_iters", "points_staged",
+                                            "candidates", "leaves_scanned")},
+        "fallback_queries": st["fallback_queries"],
         "cpu_baseline": None if cpu is None else {kk: cpu[kk] for kk in
                                                   ("value", "unit", "cores", "kind", "sample")},
         "cpu_build_ms": None if cpu is None else cpu["build_s"] * 1e3,

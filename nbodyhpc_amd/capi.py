@@ -219,8 +219,12 @@ def stats_read():
     return a.value, b.value
 
 
-STATS_NAMES = ("node_lane_visits", "pair_evals", "dense_rounds", "sparse_iters", "merges",
-               "packets", "candidates", "fill_merges")
+# work counters of the last kNN call (collect kernel, knn_collect.hip): nodes
+# entered x packet lanes, (query, point) distance evaluations, dense point steps,
+# sparse (lane-compacted) iterations, leaf points staged, packets (waves),
+# candidates appended, leaves scanned, queries sent to the exact kernel
+STATS_NAMES = ("node_lane_visits", "pair_evals", "dense_steps", "sparse_iters", "points_staged",
+               "packets", "candidates", "leaves_scanned", "fallback_queries")
 
 
 def stats_read_all():

@@ -48,6 +48,8 @@ void free_tree(Tree &t) {
     if (t.splits) (void)hipFree(t.splits);
     if (t.shape_c) (void)hipFree(t.shape_c);
     if (t.shape_n) (void)hipFree(t.shape_n);
+    if (t.leafinfo) (void)hipFree(t.leafinfo);
+    t.leafinfo = nullptr;
     t.splits = nullptr;
     t.shape_c = t.shape_n = nullptr;
     t.x = t.y = t.z = nullptr;

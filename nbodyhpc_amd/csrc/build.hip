@@ -495,6 +495,36 @@ extract_splits_kernel(const nbkd_node *__restrict__ nodes, uint64_t nn, float *_
         splits[i] = nodes[i].split;
 }
 
+// Per-leaf record for the streaming kNN kernel (8 words per node id, leaves
+// only): the tight bounding box of the leaf's real points (padding rows,
+// idx >= n, excluded) and its point range.  A tight box is a valid (and
+// better) pruning bound than the split-plane box: every point of the leaf
+// lies inside it.
+__global__ void __launch_bounds__(TB)
+leafinfo_kernel(const nbkd_node *__restrict__ nodes, uint64_t nn, const float *__restrict__ x,
+                const float *__restrict__ y, const float *__restrict__ z,
+                const uint32_t *__restrict__ idx, uint64_t n, uint32_t *__restrict__ info) {
+    for (uint64_t i = blockIdx.x * (uint64_t)TB + threadIdx.x; i < nn; i += (uint64_t)gridDim.x * TB) {
+        const nbkd_node nd = nodes[i];
+        if (nd.dimension >= 0) continue;
+        float lo[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, hi[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+        for (uint32_t j = nd.left; j < nd.right; ++j) {
+            if (idx[j] >= n) continue;
+            const float p[3] = {x[j], y[j], z[j]};
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+                lo[a] = fminf(lo[a], p[a]);
+                hi[a] = fmaxf(hi[a], p[a]);
+            }
+        }
+        uint32_t *o = info + 8 * i;
+        const float4 w0 = make_float4(lo[0], lo[1], lo[2], hi[0]);
+        const float4 w1 = make_float4(hi[1], hi[2], __uint_as_float(nd.left), __uint_as_float(nd.right));
+        reinterpret_cast<float4 *>(o)[0] = w0;
+        reinterpret_cast<float4 *>(o)[1] = w1;
+    }
+}
+
 // ------------------------------------------------------------------ host side
 struct Skeleton {
     std::map<uint64_t, uint32_t> memo; // count -> subtree node count
@@ -715,6 +745,14 @@ nbkd_status build_tree(Tree &t, const float *xyz, uint64_t n, int32_t leaf_size,
         uint64_t blocks = std::min<uint64_t>((t.nnodes + TB - 1) / TB, 4096);
         extract_splits_kernel<<<(unsigned)std::max<uint64_t>(blocks, 1), TB, 0, s>>>(
             t.nodes, t.nnodes, t.splits);
+        NBKD_HIP(hipGetLastError());
+    }
+    {
+        TimedScope ts("build_leafinfo", s);
+        NBKD_HIP(hipMalloc(&t.leafinfo, std::max<uint64_t>(t.nnodes, 1) * 32));
+        uint64_t blocks = std::min<uint64_t>((t.nnodes + TB - 1) / TB, 16384);
+        leafinfo_kernel<<<(unsigned)std::max<uint64_t>(blocks, 1), TB, 0, s>>>(
+            t.nodes, t.nnodes, t.x, t.y, t.z, t.idx, t.n, t.leafinfo);
         NBKD_HIP(hipGetLastError());
     }
     NBKD_HIP(hipStreamSynchronize(s));

@@ -17,7 +17,8 @@ namespace nbkd {
 // Workspace::mu is held for the whole call).
 enum WsSlot {
     WS_Q = 0, WS_KEYS, WS_KEYS2, WS_ORDER, WS_TMP, WS_HIST, WS_SUMS, WS_OUTD, WS_OUTI,
-    WS_COUNT, WS_OFF, WS_IDX, WS_STATS, WS_LIST, WS_LT, WS_NSLOTS
+    WS_COUNT, WS_OFF, WS_IDX, WS_STATS, WS_LIST, WS_LT, WS_TG, WS_CAND, WS_CCOUNT,
+    WS_NSLOTS
 };
 struct Workspace {
     std::mutex mu;
@@ -48,6 +49,8 @@ struct Tree {
     float *splits = nullptr;
     uint32_t *shape_c = nullptr, *shape_n = nullptr;
     int shape_len = 0;
+    // per node id, leaves only: tight box lo.xyz, hi.xyz, left, right (8 words)
+    uint32_t *leafinfo = nullptr;
     mutable Workspace ws;
 };
 
@@ -87,7 +90,7 @@ struct TimedScope {
 };
 bool timing_enabled();
 bool stats_enabled();
-constexpr int NBKD_NSTATS = 8; // nodes*lanes, lane-point evals, dense rounds, sparse iters, merges, waves, candidates, fill merges
+constexpr int NBKD_NSTATS = 9; // see capi.STATS_NAMES (collect kernel) + fallback queries
 void stats_store(const uint64_t *v);
 
 // RAII device allocation (plain hipMalloc; freed after the stream drained).
@@ -117,8 +120,19 @@ nbkd_status build_tree(Tree &t, const float *xyz, uint64_t n, int32_t leaf_size,
                        hipStream_t s);
 
 // knn_packet.hip
+// tg: per-query seed bound on the k-th squared distance (nullptr: none); queries
+// that end with fewer than k points below it are appended to fail_list
 void launch_knn_packet(const Tree &t, const float *q, const uint32_t *order, uint32_t m, int k,
-                       float *od, uint32_t *oi, unsigned long long *stats, hipStream_t s);
+                       const float *tg, float *od, uint32_t *oi, uint32_t *fail_list,
+                       uint32_t *fail_count, unsigned long long *stats, hipStream_t s);
+
+// knn_collect.hip: candidate column capacity for k, and one collect + select
+// pass over m queries (order[0..m) = query ids, kd-ordered; tg = seed bounds)
+uint32_t collect_capacity(int k);
+nbkd_status launch_knn_collect(const Tree &t, const float *q, const uint32_t *order, uint32_t m,
+                               int k, const float *tg, uint2 *cand, uint32_t capg,
+                               uint32_t *ccount, float *od, uint32_t *oi, uint32_t *fail_list,
+                               uint32_t *fail_count, unsigned long long *stats, hipStream_t s);
 
 // query.hip
 nbkd_status query_knn(const Tree &t, const float *q, uint64_t m, int k, float *out_d,

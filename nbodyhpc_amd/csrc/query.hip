@@ -61,11 +61,29 @@ leaf_key_kernel(DevTree t, const float *__restrict__ q, uint32_t m, uint32_t *__
 // |subtree(m)|, m = (count/2)/8*8, axis = depth % 3 — so only the 4-B split
 // values are read (a 33 MB array at 1e8 points, Infinity-Cache resident).
 constexpr int SHAPE_MAX = 256;
+
+// Guessed squared search radius of a query from the point density of the
+// subtree it falls in (count points in the box lo..hi): the radius of a sphere
+// expected to hold `mu_c` * 4/3*pi points, mu = k + 4 sqrt(k) + 4 (Poisson
+// tail ~1e-4 below k).  Only a pruning seed: the kNN kernel starts with this
+// bound instead of +inf and sends every query that finds fewer than k points
+// inside it to the reference-exact kernel, so a bad guess costs time, never
+// correctness.
+__device__ __forceinline__ float guess_r2(uint32_t count, const float lo[3], const float hi[3],
+                                          float mu_c) {
+    const float v = (hi[0] - lo[0]) * (hi[1] - lo[1]) * (hi[2] - lo[2]);
+    if (!(v > 0.0f) || !(v < FLT_MAX) || count == 0) return FLT_MAX;
+    const float r3 = mu_c * v / (float)count;
+    const float r2 = cbrtf(r3 * r3);
+    return r2 < FLT_MAX ? r2 : FLT_MAX;
+}
+
 __global__ void __launch_bounds__(TB)
 leaf_key2_kernel(const float *__restrict__ splits, const uint32_t *__restrict__ shape_c,
                  const uint32_t *__restrict__ shape_n, int shape_len, uint32_t n8, uint32_t leaf,
                  const float *__restrict__ q, uint32_t m, uint32_t *__restrict__ keys,
-                 uint32_t *__restrict__ vals) {
+                 uint32_t *__restrict__ vals, float *__restrict__ tg, float mu_c, uint32_t anchor,
+                 float box_lo, float box_hi) {
     __shared__ uint32_t sc[SHAPE_MAX], sn[SHAPE_MAX];
     for (int i = threadIdx.x; i < shape_len; i += TB) {
         sc[i] = shape_c[i];
@@ -76,33 +94,44 @@ leaf_key2_kernel(const float *__restrict__ splits, const uint32_t *__restrict__ 
         const float p[3] = {q[3 * (size_t)i], q[3 * (size_t)i + 1], q[3 * (size_t)i + 2]};
         uint32_t node = 0, left = 0, count = n8;
         int dim = 0;
+        float lo[3] = {box_lo, box_lo, box_lo}, hi[3] = {box_hi, box_hi, box_hi};
+        float r2 = FLT_MAX;
+        bool have_r2 = tg == nullptr;
         while (count > leaf) {
+            if (!have_r2 && count <= anchor) {
+                r2 = guess_r2(count, lo, hi, mu_c);
+                have_r2 = true;
+            }
             const uint32_t mm = (count / 2) / 8 * 8;
             const float s = splits[node];
             if (p[dim] > s) { // near child, kdtree_impl.hpp:633
+                lo[dim] = s;
                 uint32_t sub = 1;
                 if (mm > leaf) {
-                    int lo = 0, hi = shape_len - 1;
-                    while (lo < hi) {
-                        const int mid = (lo + hi) >> 1;
+                    int bl = 0, bh = shape_len - 1;
+                    while (bl < bh) {
+                        const int mid = (bl + bh) >> 1;
                         if (sc[mid] < mm)
-                            lo = mid + 1;
+                            bl = mid + 1;
                         else
-                            hi = mid;
+                            bh = mid;
                     }
-                    sub = sn[lo];
+                    sub = sn[bl];
                 }
                 node += 1 + sub;
                 left += mm;
                 count -= mm;
             } else {
+                hi[dim] = s;
                 node += 1;
                 count = mm;
             }
             dim = dim == 2 ? 0 : dim + 1;
         }
+        if (!have_r2) r2 = guess_r2(count, lo, hi, mu_c);
         keys[i] = left >> 3;
         vals[i] = i;
+        if (tg) tg[i] = r2;
     }
 }
 
@@ -283,158 +312,6 @@ nbkd_status radix_sort(Workspace &ws, uint32_t *k0, uint32_t *v0, uint32_t *k1, 
         NBKD_HIP(hipGetLastError());
     }
     return NBKD_OK;
-}
-
-template <int KC, bool PER>
-__global__ void __launch_bounds__(TB)
-knn_kernel(DevTree t, const float *__restrict__ q, const uint32_t *__restrict__ order, uint32_t m,
-           int k, float *__restrict__ out_d, uint32_t *__restrict__ out_i,
-           unsigned long long *__restrict__ stats) {
-    constexpr int CAP = KC < 16 ? KC : 16;
-    __shared__ float s_bd[WPB][CAP][64];
-    __shared__ uint32_t s_bi[WPB][CAP][64];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint32_t gq = (blockIdx.x * WPB + wave) * 64u + lane;
-    const bool valid = gq < m;
-    const uint32_t qo = valid ? order[gq] : 0u;
-    const float qx = valid ? q[3 * (size_t)qo] : 0.0f;
-    const float qy = valid ? q[3 * (size_t)qo + 1] : 0.0f;
-    const float qz = valid ? q[3 * (size_t)qo + 2] : 0.0f;
-    const float L = t.box;
-    const uint32_t nvalid = (uint32_t)__popcll(__ballot(valid));
-
-    float td[KC];
-    uint32_t ti[KC];
-#pragma unroll
-    for (int j = 0; j < KC; ++j) {
-        td[j] = (j < KC - k) ? -INFINITY : FLT_MAX;
-        ti[j] = 0xFFFFFFFFu;
-    }
-    float kth = valid ? FLT_MAX : -INFINITY;
-    uint32_t cnt = 0;
-    float *bd_col = &s_bd[wave][0][lane];
-    uint32_t *bi_col = &s_bi[wave][0][lane];
-
-    auto merge = [&]() {
-        float bd[CAP];
-        uint32_t bi[CAP];
-#pragma unroll
-        for (int s = 0; s < CAP; ++s) {
-            float dv = bd_col[s * 64];
-            uint32_t iv = bi_col[s * 64];
-            bool have = (uint32_t)s < cnt;
-            bd[s] = have ? dv : INFINITY;
-            bi[s] = have ? iv : 0xFFFFFFFFu;
-        }
-        bitonic_sort<CAP>(bd, bi);
-#pragma unroll
-        for (int s = 0; s < CAP; ++s) {
-            const int pos = KC - CAP + s, o = CAP - 1 - s;
-            bool take = bd[o] < td[pos];
-            td[pos] = take ? bd[o] : td[pos];
-            ti[pos] = take ? bi[o] : ti[pos];
-        }
-        bitonic_merge<KC>(td, ti);
-        if (valid) kth = td[KC - 1];
-        cnt = 0;
-    };
-
-    uint64_t n_nodes = 0, n_pts = 0;
-    WaveStack stk;
-    stk.node = 0;
-    stk.b0 = stk.b1 = stk.b2 = stk.b3 = stk.b4 = stk.b5 = 0.0f;
-    int sp = 0;
-    {
-        float box[6];
-#pragma unroll
-        for (int a = 0; a < 3; ++a) {
-            box[2 * a] = PER ? 0.0f : -FLT_MAX;
-            box[2 * a + 1] = PER ? L : FLT_MAX;
-        }
-        NBKD_PUSH(sp, 0u, box);
-    }
-    while (sp > 0) {
-        --sp;
-        const uint32_t node = __builtin_amdgcn_readlane(stk.node, sp);
-        float box[6] = {rdlane(stk.b0, sp), rdlane(stk.b1, sp), rdlane(stk.b2, sp),
-                        rdlane(stk.b3, sp), rdlane(stk.b4, sp), rdlane(stk.b5, sp)};
-        const float bdist = box_d2<PER>(qx, qy, qz, box, L);
-        if (!__any(bdist <= kth)) continue;
-        ++n_nodes;
-        const nbkd_node nd = t.nodes[node];
-        const int dim = (int)uni((uint32_t)nd.dimension);
-        if (dim < 0) {
-            const uint32_t b = uni(nd.left), e = uni(nd.right);
-            n_pts += e - b;
-            for (uint32_t j = b; j < e; j += 8) {
-                float px[8], py[8], pz[8];
-#pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    px[u] = t.x[j + u];
-                    py[u] = t.y[j + u];
-                    pz[u] = t.z[j + u];
-                }
-#pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    const float d = point_d2<PER>(qx, qy, qz, px[u], py[u], pz[u], L);
-                    if (d < kth) {
-                        bd_col[cnt * 64] = d;
-                        bi_col[cnt * 64] = j + u;
-                        ++cnt;
-                    }
-                    if (__any(cnt == CAP)) merge();
-                }
-            }
-            continue;
-        }
-        const float split = unif(nd.split);
-        const uint32_t lchild = uni(nd.left), rchild = uni(nd.right);
-        const float qd = dim == 0 ? qx : (dim == 1 ? qy : qz);
-        const uint32_t right_votes = (uint32_t)__popcll(__ballot(valid && qd > split));
-        const bool right_first = 2 * right_votes > nvalid;
-        float lbox[6], rbox[6];
-#pragma unroll
-        for (int a = 0; a < 6; ++a) {
-            lbox[a] = box[a];
-            rbox[a] = box[a];
-        }
-        // left child: hi[dim] = split; right child: lo[dim] = split
-        if (dim == 0) {
-            lbox[1] = split;
-            rbox[0] = split;
-        } else if (dim == 1) {
-            lbox[3] = split;
-            rbox[2] = split;
-        } else {
-            lbox[5] = split;
-            rbox[4] = split;
-        }
-        if (right_first) {
-            NBKD_PUSH(sp, lchild, lbox);
-            NBKD_PUSH(sp, rchild, rbox);
-        } else {
-            NBKD_PUSH(sp, rchild, rbox);
-            NBKD_PUSH(sp, lchild, lbox);
-        }
-    }
-    if (__any(cnt > 0)) merge();
-
-    if (valid) {
-        const int skip = KC - k;
-        const size_t row = (size_t)qo * (size_t)k;
-#pragma unroll
-        for (int j = 0; j < KC; ++j) {
-            if (j >= skip) {
-                out_d[row + (j - skip)] = sqrtf(td[j]);
-                const uint32_t p = ti[j];
-                out_i[row + (j - skip)] = p == 0xFFFFFFFFu ? p : t.idx[p];
-            }
-        }
-    }
-    if (stats && lane == 0) {
-        atomicAdd(&stats[0], (unsigned long long)n_nodes * nvalid);
-        atomicAdd(&stats[1], (unsigned long long)n_pts * nvalid);
-    }
 }
 
 // radius count: same packet traversal, fixed threshold r2
@@ -679,16 +556,6 @@ outside_box_kernel(const float *__restrict__ q, uint32_t m, float L, uint32_t *_
     if (!inside) list[atomicAdd(count, 1u)] = i;
 }
 
-template <int KC>
-void launch_knn(const Tree &t, const float *q, const uint32_t *order, uint32_t m, int k,
-                float *od, uint32_t *oi, unsigned long long *stats, hipStream_t s) {
-    const unsigned blocks = (m + TB - 1) / TB;
-    if (t.periodic)
-        knn_kernel<KC, true><<<blocks, TB, 0, s>>>(view(t), q, order, m, k, od, oi, stats);
-    else
-        knn_kernel<KC, false><<<blocks, TB, 0, s>>>(view(t), q, order, m, k, od, oi, stats);
-}
-
 int key_bits(const Tree &t) {
     uint64_t maxkey = t.n8 >> 3;
     int b = 1;
@@ -698,8 +565,27 @@ int key_bits(const Tree &t) {
 
 // bucket + sort queries by leaf: order[] = query ids in kd order
 // order[] (workspace slot WS_ORDER) = query ids sorted by leaf
+// Seed radius (guess_r2) parameters: mu = k + a sqrt(k) + b expected points in
+// the seed sphere, density from the first subtree of <= anchor points on the
+// query's descent.  NBKD_KNN_SEED=0 disables the seed (every bound starts +inf).
+struct SeedParams {
+    bool on;
+    float mu_c;
+    uint32_t anchor;
+};
+SeedParams seed_params(const Tree &t, int k) {
+    const char *e = getenv("NBKD_KNN_SEED");
+    const float a = e ? (float)atof(e) : 4.0f;
+    SeedParams p;
+    p.on = a > 0.0f;
+    const float mu = (float)k + a * sqrtf((float)k) + a;
+    p.mu_c = mu / (4.0f / 3.0f * 3.14159265f);
+    p.anchor = (uint32_t)t.leaf * 4u;
+    return p;
+}
+
 nbkd_status sort_queries(const Tree &t, const float *dq, uint32_t m, uint32_t *&order,
-                         hipStream_t s) {
+                         hipStream_t s, float *tg = nullptr, const SeedParams *sp = nullptr) {
     Workspace &ws = t.ws;
     order = (uint32_t *)ws.get(WS_ORDER, (size_t)m * 4, s);
     uint32_t *tmp = (uint32_t *)ws.get(WS_TMP, (size_t)m * 4, s);
@@ -710,10 +596,12 @@ nbkd_status sort_queries(const Tree &t, const float *dq, uint32_t m, uint32_t *&
         TimedScope ts("leaf_key", s);
         if (t.shape_len <= SHAPE_MAX) {
             const unsigned blocks = (unsigned)std::min<uint64_t>((m + TB - 1) / TB, 8192);
-            leaf_key2_kernel<<<blocks, TB, 0, s>>>(t.splits, t.shape_c, t.shape_n, t.shape_len,
-                                                   (uint32_t)t.n8, (uint32_t)t.leaf, dq, m, keys,
-                                                   order);
+            const float lo = t.periodic ? 0.0f : -FLT_MAX, hi = t.periodic ? t.box : FLT_MAX;
+            leaf_key2_kernel<<<blocks, TB, 0, s>>>(
+                t.splits, t.shape_c, t.shape_n, t.shape_len, (uint32_t)t.n8, (uint32_t)t.leaf, dq,
+                m, keys, order, tg, sp ? sp->mu_c : 0.0f, sp ? sp->anchor : 0u, lo, hi);
         } else {
+            if (tg) NBKD_HIP(hipMemsetD32Async((hipDeviceptr_t)tg, 0x7F7FFFFF, m, s)); // FLT_MAX: no seed
             leaf_key_kernel<<<(m + TB - 1) / TB, TB, 0, s>>>(view(t), dq, m, keys, order);
         }
         NBKD_HIP(hipGetLastError());
@@ -754,8 +642,15 @@ nbkd_status query_knn(const Tree &t, const float *q, uint64_t m, int k, float *o
     const float *dq = nullptr;
     nbkd_status rc = stage_queries(t, q, m, flags, dq, s);
     if (rc) return rc;
+    const bool packet = k <= 64;
+    const SeedParams sp = seed_params(t, k);
+    float *tg = nullptr;
+    if (packet && sp.on) {
+        tg = (float *)t.ws.get(WS_TG, (size_t)mm * 4, s);
+        if (!tg) return NBKD_ENOMEM;
+    }
     uint32_t *ord = nullptr;
-    rc = sort_queries(t, dq, mm, ord, s);
+    rc = sort_queries(t, dq, mm, ord, s, tg, &sp);
     if (rc) return rc;
     float *dd = out_d;
     uint32_t *di = out_i;
@@ -770,7 +665,22 @@ nbkd_status query_knn(const Tree &t, const float *q, uint64_t m, int k, float *o
         if (!stats) return NBKD_ENOMEM;
         NBKD_HIP(hipMemsetAsync(stats, 0, NBKD_NSTATS * 8, s));
     }
-    if (k > 64) { // all queries through the reference-exact lane-per-query kernel
+    // queries the packet kernel cannot answer exactly go through the
+    // reference-exact lane-per-query kernel: periodic queries outside [0, L]^3
+    // and queries whose seed radius held fewer than k points
+    uint32_t *list = nullptr, *count = nullptr;
+    if (packet && (t.periodic || tg)) {
+        list = (uint32_t *)t.ws.get(WS_LIST, (size_t)mm * 4 + 16, s);
+        if (!list) return NBKD_ENOMEM;
+        count = list + mm;
+        NBKD_HIP(hipMemsetAsync(count, 0, 4, s));
+        if (t.periodic) {
+            TimedScope ts("knn_outside_box", s);
+            outside_box_kernel<<<(mm + TB - 1) / TB, TB, 0, s>>>(dq, mm, t.box, list, count);
+            NBKD_HIP(hipGetLastError());
+        }
+    }
+    if (!packet) { // all queries through the reference-exact lane-per-query kernel
         TimedScope ts("knn_exact", s);
         uint32_t threads = (uint32_t)std::min<uint64_t>(
             std::max<uint64_t>((512ull << 20) / (32ull * (uint64_t)k), TB), 65536ull);
@@ -786,33 +696,47 @@ nbkd_status query_knn(const Tree &t, const float *q, uint64_t m, int k, float *o
                                                                  lt, dd, di);
         NBKD_HIP(hipGetLastError());
     } else {
-        TimedScope ts("knn", s);
-        static const bool v1 = getenv("NBKD_KNN_V1") != nullptr;
-        if (!v1)
-            launch_knn_packet(t, dq, ord, mm, k, dd, di, stats, s);
-        else if (k <= 8)
-            launch_knn<8>(t, dq, ord, mm, k, dd, di, stats, s);
-        else if (k <= 16)
-            launch_knn<16>(t, dq, ord, mm, k, dd, di, stats, s);
-        else if (k <= 32)
-            launch_knn<32>(t, dq, ord, mm, k, dd, di, stats, s);
-        else
-            launch_knn<64>(t, dq, ord, mm, k, dd, di, stats, s);
-        NBKD_HIP(hipGetLastError());
-    }
-    if (k <= 64 && t.periodic) {
-        // queries outside the periodic box: replay the reference traversal exactly
-        TimedScope ts("knn_outside_box", s);
-        uint32_t *list = (uint32_t *)t.ws.get(WS_LIST, (size_t)mm * 4 + 16, s);
-        const uint32_t threads = 16384;
-        LtEntry *lt = (LtEntry *)t.ws.get(WS_LT, (size_t)threads * 2 * k * sizeof(LtEntry), s);
-        if (!list || !lt) return NBKD_ENOMEM;
-        uint32_t *count = list + mm;
-        NBKD_HIP(hipMemsetAsync(count, 0, 4, s));
-        outside_box_kernel<<<(mm + TB - 1) / TB, TB, 0, s>>>(dq, mm, t.box, list, count);
-        knn_exact_kernel<true><<<threads / TB, TB, 0, s>>>(view(t), dq, list, count, mm, k, lt,
-                                                           dd, di);
-        NBKD_HIP(hipGetLastError());
+        static const bool collect_off = [] {
+            const char *e = getenv("NBKD_KNN_COLLECT");
+            return e && atoi(e) == 0;
+        }();
+        if (tg && !collect_off) {
+            // collect + select in batches sized to the candidate-column budget
+            const uint32_t capg = collect_capacity(k);
+            const char *eb = getenv("NBKD_CAND_BYTES");
+            const uint64_t budget = eb ? strtoull(eb, nullptr, 10) : (8ull << 30);
+            uint64_t batch = budget / ((uint64_t)capg * 8u) / 64u * 64u;
+            batch = std::max<uint64_t>(batch, 64);
+            batch = std::min<uint64_t>(batch, ((uint64_t)mm + 63) / 64 * 64);
+            uint2 *cand = (uint2 *)t.ws.get(WS_CAND, batch * capg * 8u, s);
+            uint32_t *ccount = (uint32_t *)t.ws.get(WS_CCOUNT, batch * 4u, s);
+            if (!cand || !ccount) return NBKD_ENOMEM;
+            TimedScope ts("knn", s);
+            for (uint64_t b0 = 0; b0 < mm; b0 += batch) {
+                const uint32_t nb = (uint32_t)std::min<uint64_t>(batch, mm - b0);
+                rc = launch_knn_collect(t, dq, ord + b0, nb, k, tg, cand, capg, ccount, dd, di,
+                                        list, count, stats, s);
+                if (rc) return rc;
+            }
+        } else {
+            TimedScope ts("knn", s);
+            launch_knn_packet(t, dq, ord, mm, k, tg, dd, di, list, count, stats, s);
+            NBKD_HIP(hipGetLastError());
+        }
+        if (list) {
+            TimedScope ts("knn_fallback", s);
+            const uint32_t threads = 16384;
+            LtEntry *lt = (LtEntry *)t.ws.get(WS_LT, (size_t)threads * 2 * k * sizeof(LtEntry), s);
+            if (!lt) return NBKD_ENOMEM;
+            if (t.periodic)
+                knn_exact_kernel<true><<<threads / TB, TB, 0, s>>>(view(t), dq, list, count, mm, k,
+                                                                   lt, dd, di);
+            else
+                knn_exact_kernel<false><<<threads / TB, TB, 0, s>>>(view(t), dq, list, count, mm,
+                                                                    k, lt, dd, di);
+            NBKD_HIP(hipGetLastError());
+            if (stats) NBKD_HIP(hipMemcpyAsync(stats + 8, count, 4, hipMemcpyDeviceToDevice, s));
+        }
     }
     if (stats) {
         uint64_t h[NBKD_NSTATS];

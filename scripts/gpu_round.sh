@@ -13,8 +13,8 @@ timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout
  && echo "[round] smoke" && timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 \
  && echo "[round] bench" && timeout -k 10 600 python3 bench.py > $O/bench.json 2> $O/bench.err \
  && echo "[round] trace" && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/trace -o run --output-format csv -- $B > $O/trace.log 2>&1 \
- && echo "[round] fetch" && timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex knn4 -d $O/fetch -o run --output-format csv -- $B > $O/fetch.log 2>&1 \
- && echo "[round] write" && timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex knn4 -d $O/write -o run --output-format csv -- $B > $O/write.log 2>&1
+ && echo "[round] fetch" && timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex knn_collect -d $O/fetch -o run --output-format csv -- $B > $O/fetch.log 2>&1 \
+ && echo "[round] write" && timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex knn_collect -d $O/write -o run --output-format csv -- $B > $O/write.log 2>&1
 rc=$?
 date
 tail -5 $O/tests.log

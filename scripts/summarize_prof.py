@@ -37,7 +37,7 @@ def per_dispatch(path, regex):
 
 def main():
     src, tag = sys.argv[1], sys.argv[2]
-    regex = sys.argv[3] if len(sys.argv) > 3 else "knn4"
+    regex = sys.argv[3] if len(sys.argv) > 3 else "knn_collect"
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     prof = os.path.join(root, "profiles")
     stats = find(os.path.join(src, "trace"), "*kernel_stats.csv")
@@ -62,6 +62,7 @@ def main():
             "command": f"rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE --kernel-include-regex {regex} -- "
                        "python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-parity",
             "n_particles": cfg.get("n_particles_per_gpu", 100_000_000), "k": cfg.get("k", 32),
+            "queries_per_launch": (b or {}).get("roofline", {}).get("queries_per_launch"),
             "dispatches": [len(fv), len(wv)],
             "FETCH_SIZE_KiB_per_launch": f_kib, "WRITE_SIZE_KiB_per_launch": w_kib,
             "fetch_bytes_per_launch_corrected": 2.0 * 1024.0 * f_kib,

@@ -24,8 +24,18 @@ od = hip.DeviceArray((n, k), np.float32)
 oi = hip.DeviceArray((n, k), np.uint32)
 ref = None
 res = {}
-for v in a.variants.split(","):
+for spec in a.variants.split(","):
+    # "V" or "V/S": kernel variant V, seed parameter S (NBKD_KNN_SEED; 0 = off)
+    # "V[/S[/C[/D]]]": kernel variant V, seed parameter S (NBKD_KNN_SEED; 0 = off),
+    # collect path C (NBKD_KNN_COLLECT; 0 = off), dense threshold D (NBKD_DENSE_MIN)
+    parts = spec.split("/")
+    v = parts[0]
     os.environ["NBKD_KNN_VARIANT"] = v
+    for i, var in ((1, "NBKD_KNN_SEED"), (2, "NBKD_KNN_COLLECT"), (3, "NBKD_DENSE_MIN")):
+        if len(parts) > i and parts[i] != "":
+            os.environ[var] = parts[i]
+        else:
+            os.environ.pop(var, None)
     tree.query_device(dp.ptr, n, k, od.ptr, oi.ptr, s.handle)
     s.synchronize()
     capi.timing_enable(True); capi.timing_reset()
@@ -33,8 +43,14 @@ for v in a.variants.split(","):
         tree.query_device(dp.ptr, n, k, od.ptr, oi.ptr, s.handle)
     s.synchronize()
     ms, cnt = capi.timing_read("knn")
+    fb_ms, _ = capi.timing_read("knn_fallback")
+    col_ms, _ = capi.timing_read("knn_collect")
+    sel_ms, _ = capi.timing_read("knn_select")
+    lk_ms, _ = capi.timing_read("leaf_key")
     capi.timing_enable(False)
-    r = {"knn_ms": ms / cnt, "qps_kernel": n / (ms / cnt * 1e-3)}
+    r = {"knn_ms": ms / cnt, "collect_ms": col_ms / cnt, "select_ms": sel_ms / cnt,
+         "fallback_ms": fb_ms / cnt, "leaf_key_ms": lk_ms / cnt,
+         "qps_kernel": n / (ms / cnt * 1e-3)}
     head = od.numpy_head(200000)
     if ref is None:
         ref = head
@@ -46,8 +62,8 @@ for v in a.variants.split(","):
         st = capi.stats_read_all()
         capi.stats_enable(False)
         p = max(st["packets"], 1)
-        r.update({kk: round(st[kk] / p, 2) for kk in ("dense_rounds", "sparse_iters", "merges",
-                                                       "candidates", "fill_merges")})
-    res[v] = r
+        r.update({kk: round(st[kk] / p, 2) for kk in capi.STATS_NAMES if kk not in ("packets", "fallback_queries")})
+        r["fallback_queries"] = st["fallback_queries"]
+    res[spec] = r
     print(v, json.dumps(r), flush=True)
 json.dump(res, open(os.path.join(ROOT, "gpurun_out", "variants.json"), "w"), indent=1)
