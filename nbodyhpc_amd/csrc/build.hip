@@ -503,7 +503,8 @@ extract_splits_kernel(const nbkd_node *__restrict__ nodes, uint64_t nn, float *_
 __global__ void __launch_bounds__(TB)
 leafinfo_kernel(const nbkd_node *__restrict__ nodes, uint64_t nn, const float *__restrict__ x,
                 const float *__restrict__ y, const float *__restrict__ z,
-                const uint32_t *__restrict__ idx, uint64_t n, uint32_t *__restrict__ info) {
+                const uint32_t *__restrict__ idx, uint64_t n, uint32_t *__restrict__ info,
+                uint32_t *__restrict__ bbox) {
     for (uint64_t i = blockIdx.x * (uint64_t)TB + threadIdx.x; i < nn; i += (uint64_t)gridDim.x * TB) {
         const nbkd_node nd = nodes[i];
         if (nd.dimension >= 0) continue;
@@ -515,6 +516,17 @@ leafinfo_kernel(const nbkd_node *__restrict__ nodes, uint64_t nn, const float *_
             for (int a = 0; a < 3; ++a) {
                 lo[a] = fminf(lo[a], p[a]);
                 hi[a] = fmaxf(hi[a], p[a]);
+            }
+        }
+        // data bounding box (order-preserving keys; the seed radius of
+        // non-periodic queries needs finite subtree volumes)
+        if (bbox) {
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+                if (lo[a] <= hi[a]) {
+                    atomicMin(&bbox[a], fkey(lo[a]));
+                    atomicMax(&bbox[3 + a], fkey(hi[a]));
+                }
             }
         }
         uint32_t *o = info + 8 * i;
@@ -751,9 +763,20 @@ nbkd_status build_tree(Tree &t, const float *xyz, uint64_t n, int32_t leaf_size,
         TimedScope ts("build_leafinfo", s);
         NBKD_HIP(hipMalloc(&t.leafinfo, std::max<uint64_t>(t.nnodes, 1) * 32));
         uint64_t blocks = std::min<uint64_t>((t.nnodes + TB - 1) / TB, 16384);
+        DevBuf d_bbox;
+        NBKD_HIP(d_bbox.alloc(6 * 4, s));
+        const uint32_t init[6] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u, 0u};
+        NBKD_HIP(hipMemcpyAsync(d_bbox.p, init, sizeof(init), hipMemcpyHostToDevice, s));
         leafinfo_kernel<<<(unsigned)std::max<uint64_t>(blocks, 1), TB, 0, s>>>(
-            t.nodes, t.nnodes, t.x, t.y, t.z, t.idx, t.n, t.leafinfo);
+            t.nodes, t.nnodes, t.x, t.y, t.z, t.idx, t.n, t.leafinfo, d_bbox.as<uint32_t>());
         NBKD_HIP(hipGetLastError());
+        uint32_t hb[6];
+        NBKD_HIP(hipMemcpyAsync(hb, d_bbox.p, sizeof(hb), hipMemcpyDeviceToHost, s));
+        NBKD_HIP(hipStreamSynchronize(s));
+        for (int a = 0; a < 3; ++a) {
+            t.bbox_lo[a] = hb[a] == 0xFFFFFFFFu ? 0.0f : fkey_inv(hb[a]);
+            t.bbox_hi[a] = hb[3 + a] == 0u ? 0.0f : fkey_inv(hb[3 + a]);
+        }
     }
     NBKD_HIP(hipStreamSynchronize(s));
     return NBKD_OK;

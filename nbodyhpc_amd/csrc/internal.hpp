@@ -51,6 +51,7 @@ struct Tree {
     int shape_len = 0;
     // per node id, leaves only: tight box lo.xyz, hi.xyz, left, right (8 words)
     uint32_t *leafinfo = nullptr;
+    float bbox_lo[3] = {0.0f, 0.0f, 0.0f}, bbox_hi[3] = {0.0f, 0.0f, 0.0f}; // of the real points
     mutable Workspace ws;
 };
 

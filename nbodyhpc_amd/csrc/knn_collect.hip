@@ -38,21 +38,37 @@ constexpr int TB = 256;
 constexpr int WPB = TB / 64;
 constexpr int CHUNK = 32; // leaf points staged per step (leaves hold <= 32 at leafsize 32)
 
+constexpr int NB = 16; // distance buckets of the bound histogram
+
 struct CollectLds {
-    float4 qt[64]; // query xyz + seed bound
+    float4 qt[64]; // query xyz + current bound
     uint32_t cnt[64];
+    uint32_t hist[NB / 4][64]; // per lane: NB 8-bit counts of candidates by d2 bucket
+    float2 sc[64];             // per lane: (S/NB, NB/S) bucket scale
     uint8_t owners[64];
     float pb[3][CHUNK];
 };
 
+// Bound tightening without a top-k: the seed ball [0, S) is cut into NB
+// buckets of width S/NB in d2; a candidate is counted in bucket j only if
+// d2 < (j+1)*S/NB as computed here in f32.  Once the buckets 0..j hold >= k
+// candidates, k points lie strictly inside (j+1)*S/NB, so the k-th distance
+// does too and it becomes the lane's new bound (candidates already appended
+// beyond it are harmless: select keeps the k smallest).
+__device__ __forceinline__ uint32_t d2_bucket(float d, float nb_over_s, float s_over_nb) {
+    uint32_t j = min((uint32_t)(d * nb_over_s), (uint32_t)(NB - 1));
+    if (!(d < (float)(j + 1) * s_over_nb) && j < (uint32_t)(NB - 1)) ++j;
+    return j;
+}
+
 // Candidate columns are slot-major per packet: entry (slot s, lane l) of packet
 // pk at cand[(pk * capg + s) * 64 + l] = {d2 bits, tree position}.
-template <bool PER, int DENSE_MIN, bool STATS>
-__global__ void __launch_bounds__(TB, 8)
+template <bool PER, int DENSE_MIN, int OCC, int G, bool STATS>
+__global__ void __launch_bounds__(TB, OCC)
 knn_collect_kernel(DevTree t, const uint32_t *__restrict__ linfo, const float *__restrict__ q,
-                   const uint32_t *__restrict__ order, uint32_t m, const float *__restrict__ tg,
-                   uint2 *__restrict__ cand, uint32_t capg, uint32_t *__restrict__ ccount,
-                   unsigned long long *__restrict__ stats) {
+                   const uint32_t *__restrict__ order, uint32_t m, int kq,
+                   const float *__restrict__ tg, uint2 *__restrict__ cand, uint32_t capg,
+                   uint32_t *__restrict__ ccount, unsigned long long *__restrict__ stats) {
     __shared__ CollectLds Wl[WPB];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     CollectLds &W = Wl[wave];
@@ -64,21 +80,41 @@ knn_collect_kernel(DevTree t, const uint32_t *__restrict__ linfo, const float *_
     const float qy = valid ? q[3 * (size_t)qo + 1] : 0.0f;
     const float qz = valid ? q[3 * (size_t)qo + 2] : 0.0f;
     const float L = t.box;
-    const float kth = valid ? tg[qo] : -INFINITY;
+    const float seed = valid ? tg[qo] : -INFINITY;
+    float kth = seed;
+    // bucket scale of the bound histogram (0 when the seed is not finite: no
+    // tightening, everything lands in the last bucket)
+    const bool fin = seed < FLT_MAX;
+    const float s_over_nb = fin ? seed * (1.0f / NB) : 0.0f;
+    const float nb_over_s = (fin && seed > 0.0f) ? (float)NB / seed : 0.0f;
     W.qt[lane] = make_float4(qx, qy, qz, kth);
+    W.sc[lane] = make_float2(s_over_nb, nb_over_s);
+#pragma unroll
+    for (int w = 0; w < NB / 4; ++w) W.hist[w][lane] = 0u;
     uint2 *const col = cand + (size_t)pk * capg * 64u;
     uint32_t cnt = 0;
 
     uint64_t n_nodes = 0, n_leaves = 0, n_scanned = 0, n_dense = 0, n_sparse = 0, n_evals = 0;
-    WaveStack stk;
-    stk.node = 0;
-    stk.b0 = stk.b1 = stk.b2 = stk.b3 = stk.b4 = stk.b5 = 0.0f;
+    // Stack: entry i in lane i of these VGPRs (node id + its box).  The
+    // current node's box stays wave-uniform (SGPRs); each lane keeps its three
+    // per-axis lower-bound terms of that box (tm), so a child's test only
+    // recomputes the split axis.  Children are tested when their parent is
+    // expanded: a far child no lane wants is never pushed (bounds only shrink).
+    uint32_t sk_node = 0;
+    float sk_b[6] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
     int sp = 0;
     const cnode_ptr cnodes = (cnode_ptr)t.nodes;
     uint32_t node = 0;
-    float b0 = PER ? 0.0f : -FLT_MAX, b1 = PER ? L : FLT_MAX;
-    float b2 = b0, b3 = b1, b4 = b0, b5 = b1;
-    bool have = true;
+    float bx[6];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        bx[2 * a] = PER ? 0.0f : -FLT_MAX;
+        bx[2 * a + 1] = PER ? L : FLT_MAX;
+    }
+    float tm[3] = {box_lb_axis<PER>(qx, bx[0], bx[1], L), box_lb_axis<PER>(qy, bx[2], bx[3], L),
+                   box_lb_axis<PER>(qz, bx[4], bx[5], L)};
+    uint64_t wm = __ballot((tm[0] + tm[1]) + tm[2] <= kth);
+    bool have = wm != 0;
 
     for (;;) {
         // ---------------------------------------------------- next wanted leaf
@@ -88,20 +124,17 @@ knn_collect_kernel(DevTree t, const uint32_t *__restrict__ linfo, const float *_
             if (!have) {
                 if (sp == 0) break;
                 --sp;
-                node = __builtin_amdgcn_readlane(stk.node, sp);
-                b0 = rdlane(stk.b0, sp);
-                b1 = rdlane(stk.b1, sp);
-                b2 = rdlane(stk.b2, sp);
-                b3 = rdlane(stk.b3, sp);
-                b4 = rdlane(stk.b4, sp);
-                b5 = rdlane(stk.b5, sp);
+                node = __builtin_amdgcn_readlane(sk_node, sp);
+#pragma unroll
+                for (int a = 0; a < 6; ++a) bx[a] = rdlane(sk_b[a], sp);
+                tm[0] = box_lb_axis<PER>(qx, bx[0], bx[1], L);
+                tm[1] = box_lb_axis<PER>(qy, bx[2], bx[3], L);
+                tm[2] = box_lb_axis<PER>(qz, bx[4], bx[5], L);
+                wm = __ballot((tm[0] + tm[1]) + tm[2] <= kth);
+                if (wm == 0) continue;
             }
             have = false;
             const nbkd_node nd = cnodes[node];
-            const float box[6] = {b0, b1, b2, b3, b4, b5};
-            const bool want = box_d2<PER>(qx, qy, qz, box, L) <= kth;
-            const uint64_t wm = __ballot(want);
-            if (wm == 0) continue;
             if constexpr (STATS) ++n_nodes;
             const int dim = nd.dimension;
             if (dim < 0) {
@@ -112,23 +145,46 @@ knn_collect_kernel(DevTree t, const uint32_t *__restrict__ linfo, const float *_
             }
             const float split = nd.split;
             const float qd = dim == 0 ? qx : (dim == 1 ? qy : qz);
-            const uint32_t right_votes = (uint32_t)__popcll(__ballot(want && qd > split));
+            const float lo = dim == 0 ? bx[0] : (dim == 1 ? bx[2] : bx[4]);
+            const float hi = dim == 0 ? bx[1] : (dim == 1 ? bx[3] : bx[5]);
+            // children's split-axis terms and totals, summed in the fixed axis order
+            const float tl = box_lb_axis<PER>(qd, lo, split, L); // left: hi = split
+            const float tr = box_lb_axis<PER>(qd, split, hi, L); // right: lo = split
+            const float dl = ((dim == 0 ? tl : tm[0]) + (dim == 1 ? tl : tm[1])) + (dim == 2 ? tl : tm[2]);
+            const float dr = ((dim == 0 ? tr : tm[0]) + (dim == 1 ? tr : tm[1])) + (dim == 2 ? tr : tm[2]);
+            const uint64_t wl = __ballot(dl <= kth), wr = __ballot(dr <= kth);
+            const uint32_t right_votes = (uint32_t)__popcll(wm & __ballot(qd > split));
             const bool right_first = 2 * right_votes > (uint32_t)__popcll(wm);
-            // left child: hi[dim] = split; right child: lo[dim] = split
-            const int far_slot = right_first ? 2 * dim + 1 : 2 * dim;
+            const uint64_t wn = right_first ? wr : wl, wf = right_first ? wl : wr;
+            // left child: hi[dim] = split (slot 2*dim+1); right child: lo[dim] = split (slot 2*dim)
             const int near_slot = right_first ? 2 * dim : 2 * dim + 1;
-            float fb[6] = {b0, b1, b2, b3, b4, b5};
+            const int far_slot = right_first ? 2 * dim + 1 : 2 * dim;
+            const uint32_t sb = __float_as_uint(split);
+            if (wn != 0 && wf != 0) { // push the far child
+                const uint32_t far_node = right_first ? nd.left : nd.right;
+                const bool me = lane == sp;
+                sk_node = me ? far_node : sk_node;
 #pragma unroll
-            for (int a = 0; a < 6; ++a) fb[a] = a == far_slot ? split : fb[a];
-            const uint32_t far_node = right_first ? nd.left : nd.right;
-            NBKD_PUSH(sp, far_node, fb);
-            node = right_first ? nd.right : nd.left;
-            b0 = near_slot == 0 ? split : b0;
-            b1 = near_slot == 1 ? split : b1;
-            b2 = near_slot == 2 ? split : b2;
-            b3 = near_slot == 3 ? split : b3;
-            b4 = near_slot == 4 ? split : b4;
-            b5 = near_slot == 5 ? split : b5;
+                for (int a = 0; a < 6; ++a) {
+                    const uint32_t fv =
+                        __builtin_amdgcn_readfirstlane(a == far_slot ? sb : __float_as_uint(bx[a]));
+                    sk_b[a] = me ? __uint_as_float(fv) : sk_b[a];
+                }
+                ++sp;
+            }
+            if (wn == 0 && wf == 0) continue; // neither child: pop
+            // descend into the near child, or straight into the far one
+            const bool go_near = wn != 0;
+            const int slot = go_near ? near_slot : far_slot;
+            const bool go_right = go_near == right_first;
+            node = go_right ? nd.right : nd.left;
+            const float tnew = go_right ? tr : tl;
+#pragma unroll
+            for (int a = 0; a < 3; ++a) tm[a] = dim == a ? tnew : tm[a];
+#pragma unroll
+            for (int a = 0; a < 6; ++a)
+                bx[a] = __uint_as_float(__builtin_amdgcn_readfirstlane(a == slot ? sb : __float_as_uint(bx[a])));
+            wm = go_near ? wn : wf;
             have = true;
         }
         if (!found) break;
@@ -145,7 +201,7 @@ knn_collect_kernel(DevTree t, const uint32_t *__restrict__ linfo, const float *_
         const float tb[6] = {rdlane(__uint_as_float(iw), 0), rdlane(__uint_as_float(iw), 3),
                              rdlane(__uint_as_float(iw), 1), rdlane(__uint_as_float(iw), 4),
                              rdlane(__uint_as_float(iw), 2), rdlane(__uint_as_float(iw), 5)};
-        const uint64_t need = __ballot(box_d2<PER>(qx, qy, qz, tb, L) <= kth);
+        const uint64_t need = __ballot(box_lb2<PER>(qx, qy, qz, tb, L) <= kth);
         if (need == 0) continue;
         const uint32_t nneed = (uint32_t)__popcll(need);
         if constexpr (STATS) ++n_leaves;
@@ -157,21 +213,32 @@ knn_collect_kernel(DevTree t, const uint32_t *__restrict__ linfo, const float *_
                     n_dense += cn;
                     n_evals += (uint64_t)cn * 64;
                 }
-                for (uint32_t u0 = 0; u0 < cn; u0 += 8) {
-                    float px[8], py[8], pz[8];
+                for (uint32_t u0 = 0; u0 < cn; u0 += G) {
+                    // d2 of G points for every lane, then the hits compacted:
+                    // the append runs max-hits-per-lane times, not once per point
+                    float dg[G];
 #pragma unroll
-                    for (int u = 0; u < 8; u += 4) {
+                    for (int u = 0; u < G; u += 4) {
                         const float4 xv = *reinterpret_cast<const float4 *>(&W.pb[0][u0 + u]);
                         const float4 yv = *reinterpret_cast<const float4 *>(&W.pb[1][u0 + u]);
                         const float4 zv = *reinterpret_cast<const float4 *>(&W.pb[2][u0 + u]);
-                        px[u] = xv.x; px[u + 1] = xv.y; px[u + 2] = xv.z; px[u + 3] = xv.w;
-                        py[u] = yv.x; py[u + 1] = yv.y; py[u + 2] = yv.z; py[u + 3] = yv.w;
-                        pz[u] = zv.x; pz[u + 1] = zv.y; pz[u + 2] = zv.z; pz[u + 3] = zv.w;
+                        dg[u] = point_d2_fast<PER>(qx, qy, qz, xv.x, yv.x, zv.x, L);
+                        dg[u + 1] = point_d2_fast<PER>(qx, qy, qz, xv.y, yv.y, zv.y, L);
+                        dg[u + 2] = point_d2_fast<PER>(qx, qy, qz, xv.z, yv.z, zv.z, L);
+                        dg[u + 3] = point_d2_fast<PER>(qx, qy, qz, xv.w, yv.w, zv.w, L);
                     }
+                    uint32_t hm = 0;
 #pragma unroll
-                    for (int u = 0; u < 8; ++u) {
-                        const float d = point_d2<PER>(qx, qy, qz, px[u], py[u], pz[u], L);
-                        if (d < kth) {
+                    for (int u = 0; u < G; ++u) hm |= (dg[u] < kth ? 1u : 0u) << u;
+                    while (__any(hm != 0)) {
+                        if (hm != 0) {
+                            const uint32_t u = (uint32_t)__builtin_ctz(hm);
+                            hm &= hm - 1u;
+                            float d = dg[0];
+#pragma unroll
+                            for (int v = 1; v < G; ++v) d = u == (uint32_t)v ? dg[v] : d;
+                            const uint32_t j = d2_bucket(d, nb_over_s, s_over_nb);
+                            atomicAdd(&W.hist[j >> 2][lane], 1u << (8 * (j & 3)));
                             if (cnt < capg)
                                 col[(size_t)cnt * 64 + lane] = make_uint2(__float_as_uint(d), c0 + u0 + u);
                             ++cnt;
@@ -196,9 +263,12 @@ knn_collect_kernel(DevTree t, const uint32_t *__restrict__ linfo, const float *_
                     if (slot < nneed && pi < pairs) {
                         const uint32_t owner = W.owners[slot];
                         const float4 qq = W.qt[owner];
-                        const float d = point_d2<PER>(qq.x, qq.y, qq.z, W.pb[0][pr], W.pb[1][pr],
-                                                      W.pb[2][pr], L);
+                        const float d = point_d2_fast<PER>(qq.x, qq.y, qq.z, W.pb[0][pr],
+                                                           W.pb[1][pr], W.pb[2][pr], L);
                         if (d < qq.w) {
+                            const float2 sc = W.sc[owner];
+                            const uint32_t j = d2_bucket(d, sc.y, sc.x);
+                            atomicAdd(&W.hist[j >> 2][owner], 1u << (8 * (j & 3)));
                             const uint32_t sl = atomicAdd(&W.cnt[owner], 1u);
                             if (sl < capg)
                                 col[(size_t)sl * 64 + owner] = make_uint2(__float_as_uint(d), c0 + pr);
@@ -209,7 +279,29 @@ knn_collect_kernel(DevTree t, const uint32_t *__restrict__ linfo, const float *_
                 cnt = W.cnt[lane];
             }
             c0 += cn;
-            if (c0 >= lend) break;
+            if (c0 >= lend) {
+                // tighten: smallest bucket edge with >= k candidates below it
+                // (the last bucket's edge is the seed itself: nothing to gain)
+                wave_sync();
+                uint32_t acc = 0, jstar = NB;
+#pragma unroll
+                for (int w = 0; w < NB / 4; ++w) {
+                    const uint32_t h = W.hist[w][lane];
+#pragma unroll
+                    for (int b = 0; b < 4; ++b) {
+                        acc += (h >> (8 * b)) & 0xFFu;
+                        jstar = (jstar == NB && acc >= (uint32_t)kq) ? (uint32_t)(4 * w + b) : jstar;
+                    }
+                }
+                if (jstar < (uint32_t)(NB - 1)) {
+                    const float nb = (float)(jstar + 1) * s_over_nb;
+                    if (nb < kth) {
+                        kth = nb;
+                        W.qt[lane].w = kth;
+                    }
+                }
+                break;
+            }
             cn = min((uint32_t)CHUNK, lend - c0);
             wave_sync();
             glds_f32(t.x + c0, W.pb[0], lane, cn);
@@ -319,28 +411,39 @@ knn_select_kernel(DevTree t, const float *__restrict__ q, const uint32_t *__rest
 
 int dense_min() {
     const char *e = getenv("NBKD_DENSE_MIN"); // tuning experiments only
-    return e ? atoi(e) : 17;
+    return e ? atoi(e) : 33;
 }
 
 template <bool PER>
-void launch_collect(const Tree &t, const float *q, const uint32_t *order, uint32_t m,
+void launch_collect(const Tree &t, const float *q, const uint32_t *order, uint32_t m, int k,
                     const float *tg, uint2 *cand, uint32_t capg, uint32_t *ccount,
                     unsigned long long *stats, hipStream_t s) {
     const unsigned blocks = (m + TB - 1) / TB;
     const int dm = dense_min();
-#define NBKD_COLLECT(DM)                                                                           \
+    const char *eo = getenv("NBKD_COLLECT_OCC"); // tuning experiments only
+    const int occ = eo ? atoi(eo) : 8;
+#define NBKD_COLLECT(DM, OC, G)                                                                    \
     do {                                                                                           \
         if (stats)                                                                                 \
-            knn_collect_kernel<PER, DM, true><<<blocks, TB, 0, s>>>(                               \
-                view(t), t.leafinfo, q, order, m, tg, cand, capg, ccount, stats);                  \
+            knn_collect_kernel<PER, DM, OC, G, true><<<blocks, TB, 0, s>>>(                        \
+                view(t), t.leafinfo, q, order, m, k, tg, cand, capg, ccount, stats);               \
         else                                                                                       \
-            knn_collect_kernel<PER, DM, false><<<blocks, TB, 0, s>>>(                              \
-                view(t), t.leafinfo, q, order, m, tg, cand, capg, ccount, nullptr);                \
+            knn_collect_kernel<PER, DM, OC, G, false><<<blocks, TB, 0, s>>>(                       \
+                view(t), t.leafinfo, q, order, m, k, tg, cand, capg, ccount, nullptr);             \
     } while (0)
-    if (dm <= 9) NBKD_COLLECT(9);
-    else if (dm <= 17) NBKD_COLLECT(17);
-    else if (dm <= 25) NBKD_COLLECT(25);
-    else NBKD_COLLECT(33);
+    if (occ <= 6) {
+        NBKD_COLLECT(17, 6, 8);
+    } else if (occ == 7) {
+        NBKD_COLLECT(17, 7, 4);
+    } else if (dm <= 17) {
+        NBKD_COLLECT(17, 8, 4);
+    } else if (dm <= 33) {
+        NBKD_COLLECT(33, 8, 4);
+    } else if (dm <= 49) {
+        NBKD_COLLECT(49, 8, 4);
+    } else {
+        NBKD_COLLECT(65, 8, 4);
+    }
 #undef NBKD_COLLECT
 }
 
@@ -375,9 +478,9 @@ nbkd_status launch_knn_collect(const Tree &t, const float *q, const uint32_t *or
     {
         TimedScope ts("knn_collect", s);
         if (t.periodic)
-            launch_collect<true>(t, q, order, m, tg, cand, capg, ccount, stats, s);
+            launch_collect<true>(t, q, order, m, k, tg, cand, capg, ccount, stats, s);
         else
-            launch_collect<false>(t, q, order, m, tg, cand, capg, ccount, stats, s);
+            launch_collect<false>(t, q, order, m, k, tg, cand, capg, ccount, stats, s);
         NBKD_HIP(hipGetLastError());
     }
     {

@@ -57,6 +57,52 @@ __device__ __forceinline__ float box_d2(float qx, float qy, float qz, const floa
     return r;
 }
 
+// Same d2 bits as point_d2 with fewer instructions, for |x - q| <= L per axis
+// (both points in [0, L]): fl(d - L) = -fl(L - d) exactly, and of the three
+// images only |d| and L - |d| can be the smallest, so min(|d|, L - |d|) is the
+// reference's per-axis minimum before squaring (and min commutes with the
+// monotone square).  Callers use it only for queries inside the periodic box;
+// queries outside it are answered by the reference-exact kernel.
+template <bool PER>
+__device__ __forceinline__ float point_d2_fast(float qx, float qy, float qz, float px, float py,
+                                               float pz, float L) {
+    float dx = px - qx, dy = py - qy, dz = pz - qz;
+    if constexpr (PER) {
+        dx = fminf(fabsf(dx), L - fabsf(dx));
+        dy = fminf(fabsf(dy), L - fabsf(dy));
+        dz = fminf(fabsf(dz), L - fabsf(dz));
+    }
+    float a = dx * dx, b = dy * dy, c = dz * dz;
+    return (a + b) + c;
+}
+
+// Lower bound of the squared distance from q to any point of the box, for the
+// packet kernels' pruning (not the reference's box_distance, whose exact bits
+// only the reference-exact kernel needs).  Per axis, a = lo - q, b = q - hi:
+// non-periodic max(a, b, 0); periodic the shorter way round,
+// med3(max(a, b), L + min(a, b), 0) (L + min(a, b) >= 0 for q, lo, hi in
+// [0, L]).  Each term is monotone in the same roundings point_d2_fast uses
+// (fl(L + (q - hi)) = fl(L - (hi - q))), so it never exceeds the d2 of a point
+// inside the box.
+template <bool PER>
+__device__ __forceinline__ float box_lb_axis(float p, float lo, float hi, float L) {
+    const float a = lo - p, b = p - hi;
+    float m;
+    if constexpr (PER)
+        m = __builtin_amdgcn_fmed3f(fmaxf(a, b), L + fminf(a, b), 0.0f);
+    else
+        m = fmaxf(fmaxf(a, b), 0.0f);
+    return m * m;
+}
+
+template <bool PER>
+__device__ __forceinline__ float box_lb2(float qx, float qy, float qz, const float b[6], float L) {
+    float r = box_lb_axis<PER>(qx, b[0], b[1], L);
+    r += box_lb_axis<PER>(qy, b[2], b[3], L);
+    r += box_lb_axis<PER>(qz, b[4], b[5], L);
+    return r;
+}
+
 // ------------------------------------------------------------------ register sorting networks
 template <int N, bool IDX = true>
 __device__ __forceinline__ void ce(float (&d)[N], uint32_t (&i)[N], int a, int b) {

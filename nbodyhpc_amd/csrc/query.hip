@@ -83,7 +83,7 @@ leaf_key2_kernel(const float *__restrict__ splits, const uint32_t *__restrict__ 
                  const uint32_t *__restrict__ shape_n, int shape_len, uint32_t n8, uint32_t leaf,
                  const float *__restrict__ q, uint32_t m, uint32_t *__restrict__ keys,
                  uint32_t *__restrict__ vals, float *__restrict__ tg, float mu_c, uint32_t anchor,
-                 float box_lo, float box_hi) {
+                 float3 box_lo, float3 box_hi) {
     __shared__ uint32_t sc[SHAPE_MAX], sn[SHAPE_MAX];
     for (int i = threadIdx.x; i < shape_len; i += TB) {
         sc[i] = shape_c[i];
@@ -94,7 +94,7 @@ leaf_key2_kernel(const float *__restrict__ splits, const uint32_t *__restrict__ 
         const float p[3] = {q[3 * (size_t)i], q[3 * (size_t)i + 1], q[3 * (size_t)i + 2]};
         uint32_t node = 0, left = 0, count = n8;
         int dim = 0;
-        float lo[3] = {box_lo, box_lo, box_lo}, hi[3] = {box_hi, box_hi, box_hi};
+        float lo[3] = {box_lo.x, box_lo.y, box_lo.z}, hi[3] = {box_hi.x, box_hi.y, box_hi.z};
         float r2 = FLT_MAX;
         bool have_r2 = tg == nullptr;
         while (count > leaf) {
@@ -596,7 +596,12 @@ nbkd_status sort_queries(const Tree &t, const float *dq, uint32_t m, uint32_t *&
         TimedScope ts("leaf_key", s);
         if (t.shape_len <= SHAPE_MAX) {
             const unsigned blocks = (unsigned)std::min<uint64_t>((m + TB - 1) / TB, 8192);
-            const float lo = t.periodic ? 0.0f : -FLT_MAX, hi = t.periodic ? t.box : FLT_MAX;
+            // periodic: the box; otherwise the real points' bounding box (the
+            // density estimate only; the traversal itself starts unbounded)
+            const float3 lo = t.periodic ? make_float3(0.0f, 0.0f, 0.0f)
+                                         : make_float3(t.bbox_lo[0], t.bbox_lo[1], t.bbox_lo[2]);
+            const float3 hi = t.periodic ? make_float3(t.box, t.box, t.box)
+                                         : make_float3(t.bbox_hi[0], t.bbox_hi[1], t.bbox_hi[2]);
             leaf_key2_kernel<<<blocks, TB, 0, s>>>(
                 t.splits, t.shape_c, t.shape_n, t.shape_len, (uint32_t)t.n8, (uint32_t)t.leaf, dq,
                 m, keys, order, tg, sp ? sp->mu_c : 0.0f, sp ? sp->anchor : 0u, lo, hi);

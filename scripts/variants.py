@@ -31,7 +31,8 @@ for spec in a.variants.split(","):
     parts = spec.split("/")
     v = parts[0]
     os.environ["NBKD_KNN_VARIANT"] = v
-    for i, var in ((1, "NBKD_KNN_SEED"), (2, "NBKD_KNN_COLLECT"), (3, "NBKD_DENSE_MIN")):
+    for i, var in ((1, "NBKD_KNN_SEED"), (2, "NBKD_KNN_COLLECT"), (3, "NBKD_DENSE_MIN"),
+                   (4, "NBKD_COLLECT_OCC")):
         if len(parts) > i and parts[i] != "":
             os.environ[var] = parts[i]
         else:
