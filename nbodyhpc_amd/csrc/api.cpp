@@ -49,7 +49,9 @@ void free_tree(Tree &t) {
     if (t.shape_c) (void)hipFree(t.shape_c);
     if (t.shape_n) (void)hipFree(t.shape_n);
     if (t.leafinfo) (void)hipFree(t.leafinfo);
+    if (t.hsplit) (void)hipFree(t.hsplit);
     t.leafinfo = nullptr;
+    t.hsplit = nullptr;
     t.splits = nullptr;
     t.shape_c = t.shape_n = nullptr;
     t.x = t.y = t.z = nullptr;

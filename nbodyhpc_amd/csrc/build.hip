@@ -537,6 +537,52 @@ leafinfo_kernel(const nbkd_node *__restrict__ nodes, uint64_t nn, const float *_
     }
 }
 
+// Split values in heap (BFS) order for the query bucketing descent: the node
+// reached by turns t_1..t_d (0 left, 1 right) has heap index h, children 2h+1 /
+// 2h+2, so the descent needs neither child ids nor the shape table, and the top
+// levels sit together in a few KB (cache resident).  One thread per leaf walks
+// from the root and writes every ancestor whose first point is the leaf's first
+// point (each internal node exactly once); preorder ids come from the shape
+// table as in leaf_key2_kernel.
+__global__ void __launch_bounds__(TB)
+heap_splits_kernel(const nbkd_node *__restrict__ nodes, uint64_t nn, const float *__restrict__ splits,
+                   const uint32_t *__restrict__ shape_c, const uint32_t *__restrict__ shape_n,
+                   int shape_len, uint32_t n8, uint32_t leaf, float *__restrict__ heap) {
+    for (uint64_t i = blockIdx.x * (uint64_t)TB + threadIdx.x; i < nn; i += (uint64_t)gridDim.x * TB) {
+        const nbkd_node nd = nodes[i];
+        if (nd.dimension >= 0) continue;
+        const uint32_t target = nd.left;
+        uint32_t node = 0, left = 0, count = n8;
+        uint64_t h = 0;
+        while (count > leaf) {
+            if (left == target) heap[h] = splits[node];
+            const uint32_t mm = (count / 2) / 8 * 8;
+            if (target >= left + mm) {
+                uint32_t sub = 1;
+                if (mm > leaf) {
+                    int bl = 0, bh = shape_len - 1;
+                    while (bl < bh) {
+                        const int mid = (bl + bh) >> 1;
+                        if (shape_c[mid] < mm)
+                            bl = mid + 1;
+                        else
+                            bh = mid;
+                    }
+                    sub = shape_n[bl];
+                }
+                node += 1 + sub;
+                left += mm;
+                count -= mm;
+                h = 2 * h + 2;
+            } else {
+                node += 1;
+                count = mm;
+                h = 2 * h + 1;
+            }
+        }
+    }
+}
+
 // ------------------------------------------------------------------ host side
 struct Skeleton {
     std::map<uint64_t, uint32_t> memo; // count -> subtree node count
@@ -757,6 +803,14 @@ nbkd_status build_tree(Tree &t, const float *xyz, uint64_t n, int32_t leaf_size,
         uint64_t blocks = std::min<uint64_t>((t.nnodes + TB - 1) / TB, 4096);
         extract_splits_kernel<<<(unsigned)std::max<uint64_t>(blocks, 1), TB, 0, s>>>(
             t.nodes, t.nnodes, t.splits);
+        NBKD_HIP(hipGetLastError());
+    }
+    if (t.depth <= 30) {
+        NBKD_HIP(hipMalloc(&t.hsplit, ((size_t)1 << t.depth) * 4));
+        uint64_t blocks = std::min<uint64_t>((t.nnodes + TB - 1) / TB, 16384);
+        heap_splits_kernel<<<(unsigned)std::max<uint64_t>(blocks, 1), TB, 0, s>>>(
+            t.nodes, t.nnodes, t.splits, t.shape_c, t.shape_n, t.shape_len, (uint32_t)t.n8,
+            (uint32_t)t.leaf, t.hsplit);
         NBKD_HIP(hipGetLastError());
     }
     {

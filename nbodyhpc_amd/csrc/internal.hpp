@@ -51,6 +51,8 @@ struct Tree {
     int shape_len = 0;
     // per node id, leaves only: tight box lo.xyz, hi.xyz, left, right (8 words)
     uint32_t *leafinfo = nullptr;
+    // internal nodes' split values in heap order (2^depth entries), or nullptr
+    float *hsplit = nullptr;
     float bbox_lo[3] = {0.0f, 0.0f, 0.0f}, bbox_hi[3] = {0.0f, 0.0f, 0.0f}; // of the real points
     mutable Workspace ws;
 };

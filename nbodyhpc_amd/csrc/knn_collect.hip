@@ -61,8 +61,12 @@ __device__ __forceinline__ uint32_t d2_bucket(float d, float nb_over_s, float s_
     return j;
 }
 
-// Candidate columns are slot-major per packet: entry (slot s, lane l) of packet
-// pk at cand[(pk * capg + s) * 64 + l] = {d2 bits, tree position}.
+// Candidate columns, entries {d2 bits, tree position}: packet pk owns
+// cand[pk * 64 * capg ...) as capg/16 blocks of 64 lanes x 16 slots; slot s of
+// lane l sits at block s/16, row l, column s%16.  A lane appends in order, so
+// it fills whole 128-B lines (a slot-major layout left lines partly written and
+// tripled the HBM write traffic), and select reads each block as one contiguous
+// 8-KB run, transposed through LDS.
 template <bool PER, int DENSE_MIN, int OCC, int G, bool STATS>
 __global__ void __launch_bounds__(TB, OCC)
 knn_collect_kernel(DevTree t, const uint32_t *__restrict__ linfo, const float *__restrict__ q,
@@ -91,7 +95,7 @@ knn_collect_kernel(DevTree t, const uint32_t *__restrict__ linfo, const float *_
     W.sc[lane] = make_float2(s_over_nb, nb_over_s);
 #pragma unroll
     for (int w = 0; w < NB / 4; ++w) W.hist[w][lane] = 0u;
-    uint2 *const col = cand + (size_t)pk * capg * 64u;
+    uint2 *const col = cand + (size_t)pk * 64u * capg;
     uint32_t cnt = 0;
 
     uint64_t n_nodes = 0, n_leaves = 0, n_scanned = 0, n_dense = 0, n_sparse = 0, n_evals = 0;
@@ -240,7 +244,8 @@ knn_collect_kernel(DevTree t, const uint32_t *__restrict__ linfo, const float *_
                             const uint32_t j = d2_bucket(d, nb_over_s, s_over_nb);
                             atomicAdd(&W.hist[j >> 2][lane], 1u << (8 * (j & 3)));
                             if (cnt < capg)
-                                col[(size_t)cnt * 64 + lane] = make_uint2(__float_as_uint(d), c0 + u0 + u);
+                                col[((cnt >> 4) * 64u + lane) * 16u + (cnt & 15u)] =
+                                    make_uint2(__float_as_uint(d), c0 + u0 + u);
                             ++cnt;
                         }
                     }
@@ -271,7 +276,8 @@ knn_collect_kernel(DevTree t, const uint32_t *__restrict__ linfo, const float *_
                             atomicAdd(&W.hist[j >> 2][owner], 1u << (8 * (j & 3)));
                             const uint32_t sl = atomicAdd(&W.cnt[owner], 1u);
                             if (sl < capg)
-                                col[(size_t)sl * 64 + owner] = make_uint2(__float_as_uint(d), c0 + pr);
+                                col[((sl >> 4) * 64u + owner) * 16u + (sl & 15u)] =
+                                    make_uint2(__float_as_uint(d), c0 + pr);
                         }
                     }
                 }
@@ -340,7 +346,8 @@ knn_select_kernel(DevTree t, const float *__restrict__ q, const uint32_t *__rest
                   uint32_t *__restrict__ fail_count) {
     constexpr int NS = 16;                  // candidates merged per pass
     constexpr int CC = KC < 32 ? KC : 32;   // top-k registers staged per output pass
-    __shared__ uint32_t stage_all[WPB][CC * 64];
+    constexpr int SW = CC < 32 ? 32 * 64 : CC * 64; // >= 8 KB: one candidate block
+    __shared__ uint32_t stage_all[WPB][SW];
     __shared__ uint32_t rowq_all[WPB][64];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     uint32_t *stage = stage_all[wave], *rowq = rowq_all[wave];
@@ -367,17 +374,38 @@ knn_select_kernel(DevTree t, const float *__restrict__ q, const uint32_t *__rest
         td[j] = (j < KC - k) ? -INFINITY : FLT_MAX;
         ti[j] = 0xFFFFFFFFu;
     }
-    const uint2 *colp = cand + (size_t)pk * capg * 64u + lane;
+    const uint4 *blk = reinterpret_cast<const uint4 *>(cand + (size_t)pk * 64u * capg);
+    uint4 *const lds4 = reinterpret_cast<uint4 *>(stage);
     for (uint32_t s0 = 0; s0 < maxn; s0 += NS) {
         float bd[NS];
         uint32_t bi[NS];
+        // block s0/16: 8 KB contiguous -> LDS (row r, 16-B piece j at r*8 + (j ^ (r&7)))
+        const uint4 *b4 = blk + (size_t)(s0 >> 4) * 512u;
+        // piece g = i*64 + lane: row r = g/8 = 8i + lane/8, column j = lane%8
+        const uint32_t r0 = (uint32_t)lane >> 3, jj = (uint32_t)lane & 7u;
+        const uint4 v0 = b4[lane], v1 = b4[64 + lane], v2 = b4[128 + lane], v3 = b4[192 + lane];
+        const uint4 v4 = b4[256 + lane], v5 = b4[320 + lane], v6 = b4[384 + lane], v7 = b4[448 + lane];
+        wave_sync();
+        // (8i + r0) & 7 == r0: the swizzle column is the same for every i
+        uint4 *const w4 = lds4 + r0 * 8 + (jj ^ r0);
+        w4[0] = v0;
+        w4[64] = v1;
+        w4[128] = v2;
+        w4[192] = v3;
+        w4[256] = v4;
+        w4[320] = v5;
+        w4[384] = v6;
+        w4[448] = v7;
+        wave_sync();
 #pragma unroll
-        for (int j = 0; j < NS; ++j) {
+        for (int j = 0; j < NS; j += 2) {
+            const uint4 e = lds4[lane * 8 + ((uint32_t)(j >> 1) ^ ((uint32_t)lane & 7u))];
             const uint32_t s = s0 + j;
-            uint2 e = make_uint2(0x7F800000u, 0xFFFFFFFFu); // (+inf, none)
-            if (s < nn) e = colp[(size_t)s * 64];
-            bd[j] = __uint_as_float(e.x);
-            bi[j] = e.y;
+            const bool h0 = s < nn, h1 = s + 1 < nn;
+            bd[j] = h0 ? __uint_as_float(e.x) : INFINITY;
+            bi[j] = h0 ? e.y : 0xFFFFFFFFu;
+            bd[j + 1] = h1 ? __uint_as_float(e.z) : INFINITY;
+            bi[j + 1] = h1 ? e.w : 0xFFFFFFFFu;
         }
         bitonic_sort<NS>(bd, bi);
 #pragma unroll

@@ -78,6 +78,47 @@ __device__ __forceinline__ float guess_r2(uint32_t count, const float lo[3], con
     return r2 < FLT_MAX ? r2 : FLT_MAX;
 }
 
+// Bucketing descent over the heap-ordered splits (build.hip heap_splits_kernel):
+// same turns, same leaf key and seed as leaf_key2_kernel, no shape table.
+__global__ void __launch_bounds__(TB)
+leaf_key3_kernel(const float *__restrict__ hsplit, uint32_t n8, uint32_t leaf,
+                 const float *__restrict__ q, uint32_t m, uint32_t *__restrict__ keys,
+                 uint32_t *__restrict__ vals, float *__restrict__ tg, float mu_c, uint32_t anchor,
+                 float3 box_lo, float3 box_hi) {
+    for (uint32_t i = blockIdx.x * TB + threadIdx.x; i < m; i += gridDim.x * TB) {
+        const float p[3] = {q[3 * (size_t)i], q[3 * (size_t)i + 1], q[3 * (size_t)i + 2]};
+        uint32_t left = 0, count = n8;
+        uint64_t h = 0;
+        int dim = 0;
+        float lo[3] = {box_lo.x, box_lo.y, box_lo.z}, hi[3] = {box_hi.x, box_hi.y, box_hi.z};
+        float r2 = FLT_MAX;
+        bool have_r2 = tg == nullptr;
+        while (count > leaf) {
+            if (!have_r2 && count <= anchor) {
+                r2 = guess_r2(count, lo, hi, mu_c);
+                have_r2 = true;
+            }
+            const uint32_t mm = (count / 2) / 8 * 8;
+            const float s = hsplit[h];
+            if (p[dim] > s) { // near child, kdtree_impl.hpp:633
+                lo[dim] = s;
+                left += mm;
+                count -= mm;
+                h = 2 * h + 2;
+            } else {
+                hi[dim] = s;
+                count = mm;
+                h = 2 * h + 1;
+            }
+            dim = dim == 2 ? 0 : dim + 1;
+        }
+        if (!have_r2) r2 = guess_r2(count, lo, hi, mu_c);
+        keys[i] = left >> 3;
+        vals[i] = i;
+        if (tg) tg[i] = r2;
+    }
+}
+
 __global__ void __launch_bounds__(TB)
 leaf_key2_kernel(const float *__restrict__ splits, const uint32_t *__restrict__ shape_c,
                  const uint32_t *__restrict__ shape_n, int shape_len, uint32_t n8, uint32_t leaf,
@@ -292,15 +333,17 @@ nbkd_status device_excl_scan(Workspace &ws, uint32_t *a, uint64_t n, hipStream_t
     return NBKD_OK;
 }
 
-// sorts (keys, vals) by the low `nbits` of keys; result in (k0, v0)
+// sorts (keys, vals) by the low `nbits` of keys, ceil(nbits/8) LSD passes
+// ping-ponging between (k0, v0) and (k1, v1); *vout = the sorted values
 nbkd_status radix_sort(Workspace &ws, uint32_t *k0, uint32_t *v0, uint32_t *k1, uint32_t *v1,
-                       uint32_t n, int nbits, hipStream_t s) {
+                       uint32_t n, int nbits, hipStream_t s, uint32_t **vout) {
+    *vout = v0;
     if (n <= 1) return NBKD_OK;
     const uint32_t ntiles = (n + RS_TILE - 1) / RS_TILE;
     uint32_t *hist = (uint32_t *)ws.get(WS_HIST, (size_t)256 * ntiles * 4, s);
     if (!hist) return NBKD_ENOMEM;
-    int passes = (nbits + 7) / 8;
-    if (passes & 1) ++passes; // even number of passes: the result lands back in (k0, v0)
+    const int passes = (nbits + 7) / 8;
+    *vout = (passes & 1) ? v1 : v0;
     for (int p = 0; p < passes; ++p) {
         const int shift = 8 * p;
         uint32_t *ki = (p & 1) ? k1 : k0, *vi = (p & 1) ? v1 : v0;
@@ -594,7 +637,17 @@ nbkd_status sort_queries(const Tree &t, const float *dq, uint32_t m, uint32_t *&
     if (!order || !tmp || !keys || !keys2) return NBKD_ENOMEM;
     {
         TimedScope ts("leaf_key", s);
-        if (t.shape_len <= SHAPE_MAX) {
+        static const bool no_heap = getenv("NBKD_NO_HEAP_SPLITS") != nullptr; // A/B only
+        if (t.hsplit && !no_heap) {
+            const unsigned blocks = (unsigned)std::min<uint64_t>((m + TB - 1) / TB, 8192);
+            const float3 lo = t.periodic ? make_float3(0.0f, 0.0f, 0.0f)
+                                         : make_float3(t.bbox_lo[0], t.bbox_lo[1], t.bbox_lo[2]);
+            const float3 hi = t.periodic ? make_float3(t.box, t.box, t.box)
+                                         : make_float3(t.bbox_hi[0], t.bbox_hi[1], t.bbox_hi[2]);
+            leaf_key3_kernel<<<blocks, TB, 0, s>>>(t.hsplit, (uint32_t)t.n8, (uint32_t)t.leaf, dq, m,
+                                                   keys, order, tg, sp ? sp->mu_c : 0.0f,
+                                                   sp ? sp->anchor : 0u, lo, hi);
+        } else if (t.shape_len <= SHAPE_MAX) {
             const unsigned blocks = (unsigned)std::min<uint64_t>((m + TB - 1) / TB, 8192);
             // periodic: the box; otherwise the real points' bounding box (the
             // density estimate only; the traversal itself starts unbounded)
@@ -612,7 +665,7 @@ nbkd_status sort_queries(const Tree &t, const float *dq, uint32_t m, uint32_t *&
         NBKD_HIP(hipGetLastError());
     }
     TimedScope ts("sort", s);
-    return radix_sort(ws, keys, order, keys2, tmp, m, key_bits(t), s);
+    return radix_sort(ws, keys, order, keys2, tmp, m, key_bits(t), s, &order);
 }
 
 nbkd_status stage_queries(const Tree &t, const float *q, uint64_t m, uint32_t flags,

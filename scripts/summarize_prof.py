@@ -30,6 +30,8 @@ def per_dispatch(path, regex):
         for row in csv.DictReader(f):
             if regex not in row["Kernel_Name"]:
                 continue
+            if ", true>(" in row["Kernel_Name"]:  # the work-counter (STATS) instance
+                continue
             key = row["Dispatch_Id"]
             vals[key] = vals.get(key, 0.0) + float(row["Counter_Value"])
     return list(vals.values())
