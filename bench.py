@@ -224,6 +224,7 @@ def main():
     key_ms, _ = capi.timing_read("leaf_key")
     oob_ms, _ = capi.timing_read("knn_outside_box")
     fb_ms, _ = capi.timing_read("knn_fallback")
+    rt_ms, _ = capi.timing_read("knn_retry")
     col_ms, col_launches = capi.timing_read("knn_collect")
     sel_ms, _ = capi.timing_read("knn_select")
     capi.timing_enable(False)
@@ -309,14 +310,14 @@ def main():
             "leaf_key": key_ms / args.steps, "sort": sort_ms / args.steps,
             "knn": knn_ms / args.steps, "knn_collect": col_ms / args.steps,
             "knn_select": sel_ms / args.steps, "outside_box_check": oob_ms / args.steps,
-            "fallback": fb_ms / args.steps,
+            "retry": rt_ms / args.steps, "fallback": fb_ms / args.steps,
         },
         "traversal_per_query": {"nodes_visited": nodes_vis / own,
                                 "distance_evals": pts_scanned / own},
         "traversal_per_packet": {kk: st[kk] / max(st["packets"], 1)
                                  for kk in ("dense_steps", "sparse_iters", "points_staged",
                                             "candidates", "leaves_scanned")},
-        "fallback_queries": st["fallback_queries"],
+        "fallback_queries": st["fallback_queries"], "retry_queries": st["retry_queries"],
         "cpu_baseline": None if cpu is None else {kk: cpu[kk] for kk in
                                                   ("value", "unit", "cores", "kind", "sample")},
         "cpu_build_ms": None if cpu is None else cpu["build_s"] * 1e3,

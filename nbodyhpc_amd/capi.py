@@ -222,9 +222,10 @@ def stats_read():
 # work counters of the last kNN call (collect kernel, knn_collect.hip): nodes
 # entered x packet lanes, (query, point) distance evaluations, dense point steps,
 # sparse (lane-compacted) iterations, leaf points staged, packets (waves),
-# candidates appended, leaves scanned, queries sent to the exact kernel
+# candidates appended, leaves scanned, queries sent to the exact kernel,
+# queries retried with a larger seed ball
 STATS_NAMES = ("node_lane_visits", "pair_evals", "dense_steps", "sparse_iters", "points_staged",
-               "packets", "candidates", "leaves_scanned", "fallback_queries")
+               "packets", "candidates", "leaves_scanned", "fallback_queries", "retry_queries")
 
 
 def stats_read_all():

@@ -18,7 +18,7 @@ namespace nbkd {
 enum WsSlot {
     WS_Q = 0, WS_KEYS, WS_KEYS2, WS_ORDER, WS_TMP, WS_HIST, WS_SUMS, WS_OUTD, WS_OUTI,
     WS_COUNT, WS_OFF, WS_IDX, WS_STATS, WS_LIST, WS_LT, WS_TG, WS_CAND, WS_CCOUNT,
-    WS_NSLOTS
+    WS_LIST2, WS_NSLOTS
 };
 struct Workspace {
     std::mutex mu;
@@ -93,7 +93,7 @@ struct TimedScope {
 };
 bool timing_enabled();
 bool stats_enabled();
-constexpr int NBKD_NSTATS = 9; // see capi.STATS_NAMES (collect kernel) + fallback queries
+constexpr int NBKD_NSTATS = 10; // see capi.STATS_NAMES (collect kernel) + exact-kernel and retried queries
 void stats_store(const uint64_t *v);
 
 // RAII device allocation (plain hipMalloc; freed after the stream drained).
@@ -130,12 +130,15 @@ void launch_knn_packet(const Tree &t, const float *q, const uint32_t *order, uin
                        uint32_t *fail_count, unsigned long long *stats, hipStream_t s);
 
 // knn_collect.hip: candidate column capacity for k, and one collect + select
-// pass over m queries (order[0..m) = query ids, kd-ordered; tg = seed bounds)
+// pass over m queries (order[0..m) = query ids; tg = seed bounds, scaled by
+// seed_mul; qpp = queries per packet: 64 for kd-ordered batches, 1 for the
+// retry of scattered seed failures)
 uint32_t collect_capacity(int k);
 nbkd_status launch_knn_collect(const Tree &t, const float *q, const uint32_t *order, uint32_t m,
-                               int k, const float *tg, uint2 *cand, uint32_t capg,
-                               uint32_t *ccount, float *od, uint32_t *oi, uint32_t *fail_list,
-                               uint32_t *fail_count, unsigned long long *stats, hipStream_t s);
+                               int k, const float *tg, float seed_mul, uint32_t qpp, uint2 *cand,
+                               uint32_t capg, uint32_t *ccount, float *od, uint32_t *oi,
+                               uint32_t *fail_list, uint32_t *fail_count,
+                               unsigned long long *stats, hipStream_t s);
 
 // query.hip
 nbkd_status query_knn(const Tree &t, const float *q, uint64_t m, int k, float *out_d,

@@ -71,20 +71,23 @@ template <bool PER, int DENSE_MIN, int OCC, int G, bool STATS>
 __global__ void __launch_bounds__(TB, OCC)
 knn_collect_kernel(DevTree t, const uint32_t *__restrict__ linfo, const float *__restrict__ q,
                    const uint32_t *__restrict__ order, uint32_t m, int kq,
-                   const float *__restrict__ tg, uint2 *__restrict__ cand, uint32_t capg,
-                   uint32_t *__restrict__ ccount, unsigned long long *__restrict__ stats) {
+                   const float *__restrict__ tg, float seed_mul, uint32_t qpp,
+                   uint2 *__restrict__ cand, uint32_t capg, uint32_t *__restrict__ ccount,
+                   unsigned long long *__restrict__ stats) {
     __shared__ CollectLds Wl[WPB];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     CollectLds &W = Wl[wave];
+    // packet pk holds queries pk*qpp .. pk*qpp + qpp-1 (lanes < qpp): qpp = 64
+    // for kd-ordered batches, 1 for the retry of scattered seed failures
     const uint32_t pk = blockIdx.x * WPB + wave;
-    const uint32_t gq = pk * 64u + lane;
-    const bool valid = gq < m;
+    const uint32_t gq = pk * qpp + lane;
+    const bool valid = (uint32_t)lane < qpp && gq < m;
     const uint32_t qo = valid ? order[gq] : 0u;
     const float qx = valid ? q[3 * (size_t)qo] : 0.0f;
     const float qy = valid ? q[3 * (size_t)qo + 1] : 0.0f;
     const float qz = valid ? q[3 * (size_t)qo + 2] : 0.0f;
     const float L = t.box;
-    const float seed = valid ? tg[qo] : -INFINITY;
+    const float seed = valid ? fminf(tg[qo] * seed_mul, FLT_MAX) : -INFINITY;
     float kth = seed;
     // bucket scale of the bound histogram (0 when the seed is not finite: no
     // tightening, everything lands in the last bucket)
@@ -95,7 +98,7 @@ knn_collect_kernel(DevTree t, const uint32_t *__restrict__ linfo, const float *_
     W.sc[lane] = make_float2(s_over_nb, nb_over_s);
 #pragma unroll
     for (int w = 0; w < NB / 4; ++w) W.hist[w][lane] = 0u;
-    uint2 *const col = cand + (size_t)pk * 64u * capg;
+    uint2 *const col = cand + (size_t)pk * qpp * capg; // qpp rows x capg slots, blocked by 16
     uint32_t cnt = 0;
 
     uint64_t n_nodes = 0, n_leaves = 0, n_scanned = 0, n_dense = 0, n_sparse = 0, n_evals = 0;
@@ -244,7 +247,7 @@ knn_collect_kernel(DevTree t, const uint32_t *__restrict__ linfo, const float *_
                             const uint32_t j = d2_bucket(d, nb_over_s, s_over_nb);
                             atomicAdd(&W.hist[j >> 2][lane], 1u << (8 * (j & 3)));
                             if (cnt < capg)
-                                col[((cnt >> 4) * 64u + lane) * 16u + (cnt & 15u)] =
+                                col[((cnt >> 4) * qpp + lane) * 16u + (cnt & 15u)] =
                                     make_uint2(__float_as_uint(d), c0 + u0 + u);
                             ++cnt;
                         }
@@ -276,7 +279,7 @@ knn_collect_kernel(DevTree t, const uint32_t *__restrict__ linfo, const float *_
                             atomicAdd(&W.hist[j >> 2][owner], 1u << (8 * (j & 3)));
                             const uint32_t sl = atomicAdd(&W.cnt[owner], 1u);
                             if (sl < capg)
-                                col[((sl >> 4) * 64u + owner) * 16u + (sl & 15u)] =
+                                col[((sl >> 4) * qpp + owner) * 16u + (sl & 15u)] =
                                     make_uint2(__float_as_uint(d), c0 + pr);
                         }
                     }
@@ -340,7 +343,7 @@ knn_collect_kernel(DevTree t, const uint32_t *__restrict__ linfo, const float *_
 template <int KC, bool PER>
 __global__ void __launch_bounds__(TB)
 knn_select_kernel(DevTree t, const float *__restrict__ q, const uint32_t *__restrict__ order,
-                  uint32_t m, int k, const uint2 *__restrict__ cand, uint32_t capg,
+                  uint32_t m, int k, uint32_t qpp, const uint2 *__restrict__ cand, uint32_t capg,
                   const uint32_t *__restrict__ ccount, float *__restrict__ out_d,
                   uint32_t *__restrict__ out_i, uint32_t *__restrict__ fail_list,
                   uint32_t *__restrict__ fail_count) {
@@ -351,8 +354,8 @@ knn_select_kernel(DevTree t, const float *__restrict__ q, const uint32_t *__rest
     __shared__ uint32_t rowq_all[WPB][64];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     uint32_t *stage = stage_all[wave], *rowq = rowq_all[wave];
-    const uint32_t pk = blockIdx.x * WPB + wave;
-    const uint32_t gq = pk * 64u + lane;
+    // lane = one query gq; its candidates: packet gq / qpp, row gq % qpp
+    const uint32_t gq = (blockIdx.x * WPB + wave) * 64u + lane;
     const bool valid = gq < m;
     const uint32_t qo = valid ? order[gq] : 0u;
     const uint32_t n = valid ? ccount[gq] : 0u;
@@ -374,12 +377,28 @@ knn_select_kernel(DevTree t, const float *__restrict__ q, const uint32_t *__rest
         td[j] = (j < KC - k) ? -INFINITY : FLT_MAX;
         ti[j] = 0xFFFFFFFFu;
     }
-    const uint4 *blk = reinterpret_cast<const uint4 *>(cand + (size_t)pk * 64u * capg);
+    // qpp == 64: the wave's 64 lanes are one packet's 64 rows (blocked, read
+    // through LDS); qpp == 1: each lane's row is contiguous at gq * capg
+    const bool whole = qpp == 64u;
+    const uint4 *blk = reinterpret_cast<const uint4 *>(
+        cand + (whole ? (size_t)(gq >> 6) * 64u * capg : (size_t)gq * capg));
     uint4 *const lds4 = reinterpret_cast<uint4 *>(stage);
     for (uint32_t s0 = 0; s0 < maxn; s0 += NS) {
         float bd[NS];
         uint32_t bi[NS];
         // block s0/16: 8 KB contiguous -> LDS (row r, 16-B piece j at r*8 + (j ^ (r&7)))
+        if (!whole) { // scattered packets: each lane reads its own row directly
+#pragma unroll
+            for (int j = 0; j < NS; j += 2) {
+                const uint32_t s = s0 + j;
+                const bool h0 = s < nn, h1 = s + 1 < nn;
+                const uint4 e = h0 ? blk[s >> 1] : make_uint4(0u, 0u, 0u, 0u);
+                bd[j] = h0 ? __uint_as_float(e.x) : INFINITY;
+                bi[j] = h0 ? e.y : 0xFFFFFFFFu;
+                bd[j + 1] = h1 ? __uint_as_float(e.z) : INFINITY;
+                bi[j + 1] = h1 ? e.w : 0xFFFFFFFFu;
+            }
+        } else {
         const uint4 *b4 = blk + (size_t)(s0 >> 4) * 512u;
         // piece g = i*64 + lane: row r = g/8 = 8i + lane/8, column j = lane%8
         const uint32_t r0 = (uint32_t)lane >> 3, jj = (uint32_t)lane & 7u;
@@ -406,6 +425,7 @@ knn_select_kernel(DevTree t, const float *__restrict__ q, const uint32_t *__rest
             bi[j] = h0 ? e.y : 0xFFFFFFFFu;
             bd[j + 1] = h1 ? __uint_as_float(e.z) : INFINITY;
             bi[j + 1] = h1 ? e.w : 0xFFFFFFFFu;
+        }
         }
         bitonic_sort<NS>(bd, bi);
 #pragma unroll
@@ -444,9 +464,9 @@ int dense_min() {
 
 template <bool PER>
 void launch_collect(const Tree &t, const float *q, const uint32_t *order, uint32_t m, int k,
-                    const float *tg, uint2 *cand, uint32_t capg, uint32_t *ccount,
-                    unsigned long long *stats, hipStream_t s) {
-    const unsigned blocks = (m + TB - 1) / TB;
+                    const float *tg, float seed_mul, uint32_t qpp, uint2 *cand, uint32_t capg,
+                    uint32_t *ccount, unsigned long long *stats, hipStream_t s) {
+    const unsigned blocks = (unsigned)(((uint64_t)m + qpp - 1) / qpp + WPB - 1) / WPB;
     const int dm = dense_min();
     const char *eo = getenv("NBKD_COLLECT_OCC"); // tuning experiments only
     const int occ = eo ? atoi(eo) : 8;
@@ -454,10 +474,11 @@ void launch_collect(const Tree &t, const float *q, const uint32_t *order, uint32
     do {                                                                                           \
         if (stats)                                                                                 \
             knn_collect_kernel<PER, DM, OC, G, true><<<blocks, TB, 0, s>>>(                        \
-                view(t), t.leafinfo, q, order, m, k, tg, cand, capg, ccount, stats);               \
+                view(t), t.leafinfo, q, order, m, k, tg, seed_mul, qpp, cand, capg, ccount, stats); \
         else                                                                                       \
             knn_collect_kernel<PER, DM, OC, G, false><<<blocks, TB, 0, s>>>(                       \
-                view(t), t.leafinfo, q, order, m, k, tg, cand, capg, ccount, nullptr);             \
+                view(t), t.leafinfo, q, order, m, k, tg, seed_mul, qpp, cand, capg, ccount,        \
+                nullptr);                                                                          \
     } while (0)
     if (occ <= 6) {
         NBKD_COLLECT(17, 6, 8);
@@ -477,15 +498,17 @@ void launch_collect(const Tree &t, const float *q, const uint32_t *order, uint32
 
 template <int KC>
 void launch_select(const Tree &t, const float *q, const uint32_t *order, uint32_t m, int k,
-                   const uint2 *cand, uint32_t capg, const uint32_t *ccount, float *od,
-                   uint32_t *oi, uint32_t *fail_list, uint32_t *fail_count, hipStream_t s) {
+                   uint32_t qpp, const uint2 *cand, uint32_t capg, const uint32_t *ccount,
+                   float *od, uint32_t *oi, uint32_t *fail_list, uint32_t *fail_count,
+                   hipStream_t s) {
     const unsigned blocks = (m + TB - 1) / TB;
     if (t.periodic)
-        knn_select_kernel<KC, true><<<blocks, TB, 0, s>>>(view(t), q, order, m, k, cand, capg,
+        knn_select_kernel<KC, true><<<blocks, TB, 0, s>>>(view(t), q, order, m, k, qpp, cand, capg,
                                                           ccount, od, oi, fail_list, fail_count);
     else
-        knn_select_kernel<KC, false><<<blocks, TB, 0, s>>>(view(t), q, order, m, k, cand, capg,
-                                                           ccount, od, oi, fail_list, fail_count);
+        knn_select_kernel<KC, false><<<blocks, TB, 0, s>>>(view(t), q, order, m, k, qpp, cand,
+                                                           capg, ccount, od, oi, fail_list,
+                                                           fail_count);
 }
 
 } // namespace
@@ -499,26 +522,30 @@ uint32_t collect_capacity(int k) {
 }
 
 nbkd_status launch_knn_collect(const Tree &t, const float *q, const uint32_t *order, uint32_t m,
-                               int k, const float *tg, uint2 *cand, uint32_t capg,
-                               uint32_t *ccount, float *od, uint32_t *oi, uint32_t *fail_list,
-                               uint32_t *fail_count, unsigned long long *stats, hipStream_t s) {
+                               int k, const float *tg, float seed_mul, uint32_t qpp, uint2 *cand,
+                               uint32_t capg, uint32_t *ccount, float *od, uint32_t *oi,
+                               uint32_t *fail_list, uint32_t *fail_count,
+                               unsigned long long *stats, hipStream_t s) {
     if (m == 0) return NBKD_OK;
     {
-        TimedScope ts("knn_collect", s);
+        TimedScope ts(qpp == 64 ? "knn_collect" : "knn_retry", s);
         if (t.periodic)
-            launch_collect<true>(t, q, order, m, k, tg, cand, capg, ccount, stats, s);
+            launch_collect<true>(t, q, order, m, k, tg, seed_mul, qpp, cand, capg, ccount, stats, s);
         else
-            launch_collect<false>(t, q, order, m, k, tg, cand, capg, ccount, stats, s);
+            launch_collect<false>(t, q, order, m, k, tg, seed_mul, qpp, cand, capg, ccount, stats, s);
         NBKD_HIP(hipGetLastError());
     }
     {
-        TimedScope ts("knn_select", s);
+        TimedScope ts(qpp == 64 ? "knn_select" : "knn_retry", s);
         if (k <= 16)
-            launch_select<16>(t, q, order, m, k, cand, capg, ccount, od, oi, fail_list, fail_count, s);
+            launch_select<16>(t, q, order, m, k, qpp, cand, capg, ccount, od, oi, fail_list,
+                              fail_count, s);
         else if (k <= 32)
-            launch_select<32>(t, q, order, m, k, cand, capg, ccount, od, oi, fail_list, fail_count, s);
+            launch_select<32>(t, q, order, m, k, qpp, cand, capg, ccount, od, oi, fail_list,
+                              fail_count, s);
         else
-            launch_select<64>(t, q, order, m, k, cand, capg, ccount, od, oi, fail_list, fail_count, s);
+            launch_select<64>(t, q, order, m, k, qpp, cand, capg, ccount, od, oi, fail_list,
+                              fail_count, s);
         NBKD_HIP(hipGetLastError());
     }
     return NBKD_OK;

@@ -768,13 +768,39 @@ nbkd_status query_knn(const Tree &t, const float *q, uint64_t m, int k, float *o
             batch = std::min<uint64_t>(batch, ((uint64_t)mm + 63) / 64 * 64);
             uint2 *cand = (uint2 *)t.ws.get(WS_CAND, batch * capg * 8u, s);
             uint32_t *ccount = (uint32_t *)t.ws.get(WS_CCOUNT, batch * 4u, s);
-            if (!cand || !ccount) return NBKD_ENOMEM;
-            TimedScope ts("knn", s);
-            for (uint64_t b0 = 0; b0 < mm; b0 += batch) {
-                const uint32_t nb = (uint32_t)std::min<uint64_t>(batch, mm - b0);
-                rc = launch_knn_collect(t, dq, ord + b0, nb, k, tg, cand, capg, ccount, dd, di,
-                                        list, count, stats, s);
-                if (rc) return rc;
+            // seed failures (fewer than k points in the seed ball, or more than
+            // the column holds) are retried with a 4x seed (2x radius), one
+            // query per wave; what still fails joins the exact kernel's list
+            uint32_t *rlist = (uint32_t *)t.ws.get(WS_LIST2, (size_t)mm * 4 + 16, s);
+            if (!cand || !ccount || !rlist) return NBKD_ENOMEM;
+            uint32_t *rcount = rlist + mm;
+            NBKD_HIP(hipMemsetAsync(rcount, 0, 4, s));
+            {
+                TimedScope ts("knn", s);
+                for (uint64_t b0 = 0; b0 < mm; b0 += batch) {
+                    const uint32_t nb = (uint32_t)std::min<uint64_t>(batch, mm - b0);
+                    rc = launch_knn_collect(t, dq, ord + b0, nb, k, tg, 1.0f, 64u, cand, capg,
+                                            ccount, dd, di, rlist, rcount, stats, s);
+                    if (rc) return rc;
+                }
+            }
+            uint32_t nr = 0;
+            NBKD_HIP(hipMemcpyAsync(&nr, rcount, 4, hipMemcpyDeviceToHost, s));
+            NBKD_HIP(hipStreamSynchronize(s));
+            if (stats) NBKD_HIP(hipMemcpyAsync(stats + 9, rcount, 4, hipMemcpyDeviceToDevice, s));
+            if (nr > 0) {
+                const uint32_t capr = collect_capacity(k) * 8u;
+                const uint64_t rb = std::max<uint64_t>(
+                    1, std::min<uint64_t>(nr, budget / ((uint64_t)capr * 8u)));
+                uint2 *rcand = (uint2 *)t.ws.get(WS_CAND, rb * capr * 8u, s);
+                uint32_t *rcc = (uint32_t *)t.ws.get(WS_CCOUNT, rb * 4u, s);
+                if (!rcand || !rcc) return NBKD_ENOMEM;
+                for (uint64_t b0 = 0; b0 < nr; b0 += rb) {
+                    const uint32_t nb = (uint32_t)std::min<uint64_t>(rb, nr - b0);
+                    rc = launch_knn_collect(t, dq, rlist + b0, nb, k, tg, 4.0f, 1u, rcand, capr,
+                                            rcc, dd, di, list, count, nullptr, s);
+                    if (rc) return rc;
+                }
             }
         } else {
             TimedScope ts("knn", s);

@@ -48,9 +48,12 @@ for spec in a.variants.split(","):
     col_ms, _ = capi.timing_read("knn_collect")
     sel_ms, _ = capi.timing_read("knn_select")
     lk_ms, _ = capi.timing_read("leaf_key")
+    rt_ms, _ = capi.timing_read("knn_retry")
+    so_ms, _ = capi.timing_read("sort")
     capi.timing_enable(False)
     r = {"knn_ms": ms / cnt, "collect_ms": col_ms / cnt, "select_ms": sel_ms / cnt,
-         "fallback_ms": fb_ms / cnt, "leaf_key_ms": lk_ms / cnt,
+         "fallback_ms": fb_ms / cnt, "retry_ms": rt_ms / cnt, "leaf_key_ms": lk_ms / cnt,
+         "sort_ms": so_ms / cnt,
          "qps_kernel": n / (ms / cnt * 1e-3)}
     head = od.numpy_head(200000)
     if ref is None:
@@ -63,8 +66,9 @@ for spec in a.variants.split(","):
         st = capi.stats_read_all()
         capi.stats_enable(False)
         p = max(st["packets"], 1)
-        r.update({kk: round(st[kk] / p, 2) for kk in capi.STATS_NAMES if kk not in ("packets", "fallback_queries")})
+        r.update({kk: round(st[kk] / p, 2) for kk in capi.STATS_NAMES if kk not in ("packets", "fallback_queries", "retry_queries")})
         r["fallback_queries"] = st["fallback_queries"]
+        r["retry_queries"] = st["retry_queries"]
     res[spec] = r
     print(v, json.dumps(r), flush=True)
 json.dump(res, open(os.path.join(ROOT, "gpurun_out", "variants.json"), "w"), indent=1)

@@ -222,3 +222,22 @@ def test_device_pointer_path(gpu):
     t.ball_count_device(dev.ptr, pts.shape[0], 0.02, cnt.ptr, stream.handle)
     stream.synchronize()
     assert np.array_equal(cnt.numpy(), t.ball_count(pts, 0.02))
+
+
+# ---------------------------------------------------------------- seed ball retries
+@pytest.mark.parametrize("seed_param", ["0.05", "0"])
+@pytest.mark.parametrize("box", [None, 1.0])
+def test_knn_seed_retry_and_no_seed(gpu, oracle, monkeypatch, seed_param, box):
+    """A tiny seed ball (NBKD_KNN_SEED=0.05) makes most queries fail the collect
+    pass: they go through the 4x-seed retry and, failing that, the exact kernel.
+    NBKD_KNN_SEED=0 switches the seed off (register top-k packet kernel)."""
+    monkeypatch.setenv("NBKD_KNN_SEED", seed_param)
+    pts = uniform(60_000, 31, L=box or 1.0)
+    rng = np.random.Generator(np.random.PCG64(32))
+    q = np.concatenate([pts[:3000], rng.uniform(0, box or 1.0, (2000, 3)).astype(np.float32)])
+    t = gpu.Tree(pts, leafsize=32, boxsize=box)
+    o = oracle.tree(pts, 32, box)
+    for k in (1, 16, 32, 50):
+        d, i = t.query(q, k)
+        dr, ir = o.query(q, k)
+        assert_knn_equal(d, i, dr, ir, pts, q, box)
