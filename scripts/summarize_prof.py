@@ -25,7 +25,9 @@ def find(d, pat):
 
 
 def per_dispatch(path, regex):
-    vals = {}
+    """Counter sum per dispatch of the full-size launches of the kernel (the
+    work-counter instance and the small retry launches are left out)."""
+    vals, grid = {}, {}
     with open(path) as f:
         for row in csv.DictReader(f):
             if regex not in row["Kernel_Name"]:
@@ -34,7 +36,9 @@ def per_dispatch(path, regex):
                 continue
             key = row["Dispatch_Id"]
             vals[key] = vals.get(key, 0.0) + float(row["Counter_Value"])
-    return list(vals.values())
+            grid[key] = int(row["Grid_Size"])
+    gmax = max(grid.values())
+    return [v for kk, v in vals.items() if grid[kk] == gmax]
 
 
 def main():
