@@ -505,6 +505,7 @@ leafinfo_kernel(const nbkd_node *__restrict__ nodes, uint64_t nn, const float *_
                 const float *__restrict__ y, const float *__restrict__ z,
                 const uint32_t *__restrict__ idx, uint64_t n, uint32_t *__restrict__ info,
                 uint32_t *__restrict__ bbox) {
+    float blo[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, bhi[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
     for (uint64_t i = blockIdx.x * (uint64_t)TB + threadIdx.x; i < nn; i += (uint64_t)gridDim.x * TB) {
         const nbkd_node nd = nodes[i];
         if (nd.dimension >= 0) continue;
@@ -518,22 +519,36 @@ leafinfo_kernel(const nbkd_node *__restrict__ nodes, uint64_t nn, const float *_
                 hi[a] = fmaxf(hi[a], p[a]);
             }
         }
-        // data bounding box (order-preserving keys; the seed radius of
-        // non-periodic queries needs finite subtree volumes)
-        if (bbox) {
 #pragma unroll
-            for (int a = 0; a < 3; ++a) {
-                if (lo[a] <= hi[a]) {
-                    atomicMin(&bbox[a], fkey(lo[a]));
-                    atomicMax(&bbox[3 + a], fkey(hi[a]));
-                }
-            }
+        for (int a = 0; a < 3; ++a) {
+            blo[a] = fminf(blo[a], lo[a]);
+            bhi[a] = fmaxf(bhi[a], hi[a]);
         }
         uint32_t *o = info + 8 * i;
         const float4 w0 = make_float4(lo[0], lo[1], lo[2], hi[0]);
         const float4 w1 = make_float4(hi[1], hi[2], __uint_as_float(nd.left), __uint_as_float(nd.right));
         reinterpret_cast<float4 *>(o)[0] = w0;
         reinterpret_cast<float4 *>(o)[1] = w1;
+    }
+    // data bounding box (order-preserving keys; the seed radius of non-periodic
+    // queries needs finite subtree volumes): reduced over the wave first, so one
+    // lane per wave issues the atomics
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            blo[a] = fminf(blo[a], __shfl_xor(blo[a], o, 64));
+            bhi[a] = fmaxf(bhi[a], __shfl_xor(bhi[a], o, 64));
+        }
+    }
+    if (bbox && (threadIdx.x & 63) == 0) {
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            if (blo[a] <= bhi[a]) {
+                atomicMin(&bbox[a], fkey(blo[a]));
+                atomicMax(&bbox[3 + a], fkey(bhi[a]));
+            }
+        }
     }
 }
 

@@ -41,11 +41,13 @@ constexpr int CHUNK = 32; // leaf points staged per step (leaves hold <= 32 at l
 constexpr int NB = 16; // distance buckets of the bound histogram
 
 struct CollectLds {
-    float4 qt[64]; // query xyz + current bound
-    uint32_t cnt[64];
-    uint32_t hist[NB / 4][64]; // per lane: NB 8-bit counts of candidates by d2 bucket
-    float2 sc[64];             // per lane: (S/NB, NB/S) bucket scale
+    // sparse mode, indexed by slot (the rank of a needing lane): its query xyz +
+    // bound, its bucket scale (S/NB, NB/S) and its lane
+    float4 sq[64];
+    float2 ssc[64];
     uint8_t owners[64];
+    uint32_t cnt[64];          // per lane: candidates appended
+    uint32_t hist[NB / 4][64]; // per lane: NB 8-bit counts of candidates by d2 bucket
     float pb[3][CHUNK];
 };
 
@@ -94,8 +96,6 @@ knn_collect_kernel(DevTree t, const uint32_t *__restrict__ linfo, const float *_
     const bool fin = seed < FLT_MAX;
     const float s_over_nb = fin ? seed * (1.0f / NB) : 0.0f;
     const float nb_over_s = (fin && seed > 0.0f) ? (float)NB / seed : 0.0f;
-    W.qt[lane] = make_float4(qx, qy, qz, kth);
-    W.sc[lane] = make_float2(s_over_nb, nb_over_s);
 #pragma unroll
     for (int w = 0; w < NB / 4; ++w) W.hist[w][lane] = 0u;
     uint2 *const col = cand + (size_t)pk * qpp * capg; // qpp rows x capg slots, blocked by 16
@@ -257,7 +257,12 @@ knn_collect_kernel(DevTree t, const uint32_t *__restrict__ linfo, const float *_
                 // (needing query, point) pairs compacted onto the 64 lanes:
                 // slot = pair & (c2-1), point = pair >> log2(c2), c2 = pow2 >= nneed
                 W.cnt[lane] = cnt;
-                if ((need >> lane) & 1ull) W.owners[mbcnt64(need)] = (uint8_t)lane;
+                if ((need >> lane) & 1ull) {
+                    const uint32_t r = mbcnt64(need);
+                    W.owners[r] = (uint8_t)lane;
+                    W.sq[r] = make_float4(qx, qy, qz, kth);
+                    W.ssc[r] = make_float2(s_over_nb, nb_over_s);
+                }
                 wave_sync();
                 uint32_t c2 = 1;
                 while (c2 < nneed) c2 <<= 1;
@@ -269,12 +274,12 @@ knn_collect_kernel(DevTree t, const uint32_t *__restrict__ linfo, const float *_
                     const uint32_t pi = p0 + lane;
                     const uint32_t slot = pi & (c2 - 1u), pr = pi >> lgc;
                     if (slot < nneed && pi < pairs) {
-                        const uint32_t owner = W.owners[slot];
-                        const float4 qq = W.qt[owner];
+                        const float4 qq = W.sq[slot];
                         const float d = point_d2_fast<PER>(qq.x, qq.y, qq.z, W.pb[0][pr],
                                                            W.pb[1][pr], W.pb[2][pr], L);
                         if (d < qq.w) {
-                            const float2 sc = W.sc[owner];
+                            const uint32_t owner = W.owners[slot];
+                            const float2 sc = W.ssc[slot];
                             const uint32_t j = d2_bucket(d, sc.y, sc.x);
                             atomicAdd(&W.hist[j >> 2][owner], 1u << (8 * (j & 3)));
                             const uint32_t sl = atomicAdd(&W.cnt[owner], 1u);
@@ -304,10 +309,7 @@ knn_collect_kernel(DevTree t, const uint32_t *__restrict__ linfo, const float *_
                 }
                 if (jstar < (uint32_t)(NB - 1)) {
                     const float nb = (float)(jstar + 1) * s_over_nb;
-                    if (nb < kth) {
-                        kth = nb;
-                        W.qt[lane].w = kth;
-                    }
+                    kth = fminf(kth, nb);
                 }
                 break;
             }
@@ -339,9 +341,21 @@ knn_collect_kernel(DevTree t, const uint32_t *__restrict__ linfo, const float *_
     }
 }
 
+// One 8-KB candidate block (64 rows x 8 pieces of 16 B, row-contiguous) into
+// LDS by direct loads, no VGPR staging: LDS piece x = i*64 + lane takes the
+// block's row r = x/8, piece (x%8) ^ (r%8), so row r's piece j sits at
+// r*8 + (j ^ (r & 7)) and the per-row reads are bank-conflict free.
+__device__ __forceinline__ void issue_block(const uint4 *b4, uint4 *lds4, int lane) {
+    const uint32_t r0 = (uint32_t)lane >> 3, jj = (uint32_t)lane & 7u;
+    const uint4 *src = b4 + r0 * 8 + (jj ^ r0);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+        __builtin_amdgcn_global_load_lds((gas_ptr)(src + 64 * i), (las_ptr)(lds4 + 64 * i), 16, 0, 0);
+}
+
 // One lane per query: the k smallest of its candidate column, sorted, as rows.
-template <int KC, bool PER>
-__global__ void __launch_bounds__(TB)
+template <int KC, bool PER, bool WHOLE>
+__global__ void __launch_bounds__(TB, KC <= 32 ? 4 : 2)
 knn_select_kernel(DevTree t, const float *__restrict__ q, const uint32_t *__restrict__ order,
                   uint32_t m, int k, uint32_t qpp, const uint2 *__restrict__ cand, uint32_t capg,
                   const uint32_t *__restrict__ ccount, float *__restrict__ out_d,
@@ -379,15 +393,16 @@ knn_select_kernel(DevTree t, const float *__restrict__ q, const uint32_t *__rest
     }
     // qpp == 64: the wave's 64 lanes are one packet's 64 rows (blocked, read
     // through LDS); qpp == 1: each lane's row is contiguous at gq * capg
-    const bool whole = qpp == 64u;
+    constexpr bool whole = WHOLE; // == (qpp == 64)
     const uint4 *blk = reinterpret_cast<const uint4 *>(
         cand + (whole ? (size_t)(gq >> 6) * 64u * capg : (size_t)gq * capg));
     uint4 *const lds4 = reinterpret_cast<uint4 *>(stage);
+    if (whole && maxn > 0) issue_block(blk, lds4, lane);
     for (uint32_t s0 = 0; s0 < maxn; s0 += NS) {
         float bd[NS];
         uint32_t bi[NS];
         // block s0/16: 8 KB contiguous -> LDS (row r, 16-B piece j at r*8 + (j ^ (r&7)))
-        if (!whole) { // scattered packets: each lane reads its own row directly
+        if constexpr (!whole) { // scattered packets: each lane reads its own row directly
 #pragma unroll
             for (int j = 0; j < NS; j += 2) {
                 const uint32_t s = s0 + j;
@@ -399,34 +414,29 @@ knn_select_kernel(DevTree t, const float *__restrict__ q, const uint32_t *__rest
                 bi[j + 1] = h1 ? e.w : 0xFFFFFFFFu;
             }
         } else {
-        const uint4 *b4 = blk + (size_t)(s0 >> 4) * 512u;
-        // piece g = i*64 + lane: row r = g/8 = 8i + lane/8, column j = lane%8
-        const uint32_t r0 = (uint32_t)lane >> 3, jj = (uint32_t)lane & 7u;
-        const uint4 v0 = b4[lane], v1 = b4[64 + lane], v2 = b4[128 + lane], v3 = b4[192 + lane];
-        const uint4 v4 = b4[256 + lane], v5 = b4[320 + lane], v6 = b4[384 + lane], v7 = b4[448 + lane];
-        wave_sync();
-        // (8i + r0) & 7 == r0: the swizzle column is the same for every i
-        uint4 *const w4 = lds4 + r0 * 8 + (jj ^ r0);
-        w4[0] = v0;
-        w4[64] = v1;
-        w4[128] = v2;
-        w4[192] = v3;
-        w4[256] = v4;
-        w4[320] = v5;
-        w4[384] = v6;
-        w4[448] = v7;
-        wave_sync();
+            // block s0/16, loaded into LDS one pass ahead (issue_block)
+            wait_vm0();
+            wave_sync();
 #pragma unroll
-        for (int j = 0; j < NS; j += 2) {
-            const uint4 e = lds4[lane * 8 + ((uint32_t)(j >> 1) ^ ((uint32_t)lane & 7u))];
-            const uint32_t s = s0 + j;
-            const bool h0 = s < nn, h1 = s + 1 < nn;
-            bd[j] = h0 ? __uint_as_float(e.x) : INFINITY;
-            bi[j] = h0 ? e.y : 0xFFFFFFFFu;
-            bd[j + 1] = h1 ? __uint_as_float(e.z) : INFINITY;
-            bi[j + 1] = h1 ? e.w : 0xFFFFFFFFu;
+            for (int j = 0; j < NS; j += 2) {
+                const uint4 e = lds4[lane * 8 + ((uint32_t)(j >> 1) ^ ((uint32_t)lane & 7u))];
+                const uint32_t s = s0 + j;
+                const bool h0 = s < nn, h1 = s + 1 < nn;
+                bd[j] = h0 ? __uint_as_float(e.x) : INFINITY;
+                bi[j] = h0 ? e.y : 0xFFFFFFFFu;
+                bd[j + 1] = h1 ? __uint_as_float(e.z) : INFINITY;
+                bi[j + 1] = h1 ? e.w : 0xFFFFFFFFu;
+            }
+            // the reads have retired before the next block's DMA overwrites the buffer
+            __builtin_amdgcn_s_waitcnt(0xC07F); // lgkmcnt(0)
+            wave_sync();
+            if (s0 + NS < maxn) issue_block(blk + (size_t)((s0 + NS) >> 4) * 512u, lds4, lane);
         }
-        }
+        // a block with nothing below any lane's current k-th changes nothing
+        bool useful = false;
+#pragma unroll
+        for (int j = 0; j < NS; ++j) useful |= bd[j] < td[KC - 1];
+        if (!__any(useful)) continue;
         bitonic_sort<NS>(bd, bi);
 #pragma unroll
         for (int s = 0; s < NS; ++s) {
@@ -447,13 +457,17 @@ knn_select_kernel(DevTree t, const float *__restrict__ q, const uint32_t *__rest
         wave_sync();
         store_rows<CC>(stage, rowq, reinterpret_cast<uint32_t *>(out_d), k, j0 - (KC - k), lane);
     }
+    // tree positions -> original ids: KC independent gathers in flight per lane
+    // (inside store_rows' loop they would be issued one after another)
+#pragma unroll
+    for (int j = 0; j < KC; ++j) ti[j] = ti[j] == 0xFFFFFFFFu ? ti[j] : t.idx[ti[j]];
 #pragma unroll
     for (int j0 = 0; j0 < KC; j0 += CC) {
         wave_sync();
 #pragma unroll
         for (int j = 0; j < CC; ++j) stage[j * 64 + (lane ^ j)] = ti[j0 + j];
         wave_sync();
-        store_rows<CC>(stage, rowq, out_i, k, j0 - (KC - k), lane, t.idx);
+        store_rows<CC>(stage, rowq, out_i, k, j0 - (KC - k), lane);
     }
 }
 
@@ -502,13 +516,15 @@ void launch_select(const Tree &t, const float *q, const uint32_t *order, uint32_
                    float *od, uint32_t *oi, uint32_t *fail_list, uint32_t *fail_count,
                    hipStream_t s) {
     const unsigned blocks = (m + TB - 1) / TB;
-    if (t.periodic)
-        knn_select_kernel<KC, true><<<blocks, TB, 0, s>>>(view(t), q, order, m, k, qpp, cand, capg,
-                                                          ccount, od, oi, fail_list, fail_count);
-    else
-        knn_select_kernel<KC, false><<<blocks, TB, 0, s>>>(view(t), q, order, m, k, qpp, cand,
-                                                           capg, ccount, od, oi, fail_list,
-                                                           fail_count);
+#define NBKD_SELECT(PER, WH)                                                                       \
+    knn_select_kernel<KC, PER, WH><<<blocks, TB, 0, s>>>(view(t), q, order, m, k, qpp, cand, capg, \
+                                                        ccount, od, oi, fail_list, fail_count)
+    if (t.periodic) {
+        if (qpp == 64) NBKD_SELECT(true, true); else NBKD_SELECT(true, false);
+    } else {
+        if (qpp == 64) NBKD_SELECT(false, true); else NBKD_SELECT(false, false);
+    }
+#undef NBKD_SELECT
 }
 
 } // namespace
