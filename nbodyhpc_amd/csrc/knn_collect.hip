@@ -99,7 +99,7 @@ knn_collect_kernel(DevTree t, const uint32_t *__restrict__ linfo, const float *_
 #pragma unroll
     for (int w = 0; w < NB / 4; ++w) W.hist[w][lane] = 0u;
     uint2 *const col = cand + (size_t)pk * qpp * capg; // qpp rows x capg slots, blocked by 16
-    uint32_t cnt = 0;
+    uint32_t cnt = 0, last_cnt = 0;
 
     uint64_t n_nodes = 0, n_leaves = 0, n_scanned = 0, n_dense = 0, n_sparse = 0, n_evals = 0;
     // Stack: entry i in lane i of these VGPRs (node id + its box).  The
@@ -295,21 +295,34 @@ knn_collect_kernel(DevTree t, const uint32_t *__restrict__ linfo, const float *_
             c0 += cn;
             if (c0 >= lend) {
                 // tighten: smallest bucket edge with >= k candidates below it
-                // (the last bucket's edge is the seed itself: nothing to gain)
-                wave_sync();
-                uint32_t acc = 0, jstar = NB;
-#pragma unroll
-                for (int w = 0; w < NB / 4; ++w) {
-                    const uint32_t h = W.hist[w][lane];
-#pragma unroll
-                    for (int b = 0; b < 4; ++b) {
-                        acc += (h >> (8 * b)) & 0xFFu;
-                        jstar = (jstar == NB && acc >= (uint32_t)kq) ? (uint32_t)(4 * w + b) : jstar;
+                // (the last bucket's edge is the seed itself: nothing to gain).
+                // Only lanes holding >= k candidates, some of them new, can move.
+                const bool upd = cnt >= (uint32_t)kq && cnt != last_cnt;
+                if (__any(upd)) {
+                    wave_sync();
+                    if (upd) {
+                        last_cnt = cnt;
+                        // per word, h * 0x01010101 holds the prefix sums of its 4
+                        // byte counts (each < 256 while cnt <= capg; a lane past
+                        // capg is re-run anyway)
+                        const uint32_t p0 = W.hist[0][lane] * 0x01010101u;
+                        const uint32_t p1 = W.hist[1][lane] * 0x01010101u;
+                        const uint32_t p2 = W.hist[2][lane] * 0x01010101u;
+                        const uint32_t p3 = W.hist[3][lane] * 0x01010101u;
+                        const uint32_t c0w = p0 >> 24, c1w = c0w + (p1 >> 24), c2w = c1w + (p2 >> 24);
+                        const uint32_t kk = (uint32_t)kq;
+                        const uint32_t w = c0w >= kk ? 0u : c1w >= kk ? 1u : c2w >= kk ? 2u : 3u;
+                        const uint32_t base = w == 0 ? 0u : w == 1 ? c0w : w == 2 ? c1w : c2w;
+                        const uint32_t pw = w == 0 ? p0 : w == 1 ? p1 : w == 2 ? p2 : p3;
+                        const uint32_t need_k = kk - base; // first byte b with prefix >= need_k
+                        const uint32_t b = (((pw & 0xFFu) < need_k) ? 1u : 0u) +
+                                           ((((pw >> 8) & 0xFFu) < need_k) ? 1u : 0u) +
+                                           ((((pw >> 16) & 0xFFu) < need_k) ? 1u : 0u) +
+                                           (((pw >> 24) < need_k) ? 1u : 0u);
+                        const uint32_t jstar = 4 * w + b; // NB when fewer than k are counted
+                        if (jstar < (uint32_t)(NB - 1))
+                            kth = fminf(kth, (float)(jstar + 1) * s_over_nb);
                     }
-                }
-                if (jstar < (uint32_t)(NB - 1)) {
-                    const float nb = (float)(jstar + 1) * s_over_nb;
-                    kth = fminf(kth, nb);
                 }
                 break;
             }
