@@ -562,7 +562,7 @@ leafinfo_kernel(const nbkd_node *__restrict__ nodes, uint64_t nn, const float *_
 __global__ void __launch_bounds__(TB)
 heap_splits_kernel(const nbkd_node *__restrict__ nodes, uint64_t nn, const float *__restrict__ splits,
                    const uint32_t *__restrict__ shape_c, const uint32_t *__restrict__ shape_n,
-                   int shape_len, uint32_t n8, uint32_t leaf, float *__restrict__ heap) {
+                   int shape_len, uint32_t n8, uint32_t leaf, int o, float *__restrict__ heap) {
     for (uint64_t i = blockIdx.x * (uint64_t)TB + threadIdx.x; i < nn; i += (uint64_t)gridDim.x * TB) {
         const nbkd_node nd = nodes[i];
         if (nd.dimension >= 0) continue;
@@ -570,7 +570,7 @@ heap_splits_kernel(const nbkd_node *__restrict__ nodes, uint64_t nn, const float
         uint32_t node = 0, left = 0, count = n8;
         uint64_t h = 0;
         while (count > leaf) {
-            if (left == target) heap[h] = splits[node];
+            if (left == target) heap[hblk_slot(h, o)] = splits[node];
             const uint32_t mm = (count / 2) / 8 * 8;
             if (target >= left + mm) {
                 uint32_t sub = 1;
@@ -821,11 +821,11 @@ nbkd_status build_tree(Tree &t, const float *xyz, uint64_t n, int32_t leaf_size,
         NBKD_HIP(hipGetLastError());
     }
     if (t.depth <= 30) {
-        NBKD_HIP(hipMalloc(&t.hsplit, ((size_t)1 << t.depth) * 4));
+        NBKD_HIP(hipMalloc(&t.hsplit, std::max<uint64_t>(hblk_blocks(t.depth), 1) * 64));
         uint64_t blocks = std::min<uint64_t>((t.nnodes + TB - 1) / TB, 16384);
         heap_splits_kernel<<<(unsigned)std::max<uint64_t>(blocks, 1), TB, 0, s>>>(
             t.nodes, t.nnodes, t.splits, t.shape_c, t.shape_n, t.shape_len, (uint32_t)t.n8,
-            (uint32_t)t.leaf, t.hsplit);
+            (uint32_t)t.leaf, hblk_offset(t.depth), t.hsplit);
         NBKD_HIP(hipGetLastError());
     }
     {

@@ -51,7 +51,8 @@ struct Tree {
     int shape_len = 0;
     // per node id, leaves only: tight box lo.xyz, hi.xyz, left, right (8 words)
     uint32_t *leafinfo = nullptr;
-    // internal nodes' split values in heap order (2^depth entries), or nullptr
+    // internal nodes' split values in the 4-level blocked heap order below
+    // (hblk_blocks(depth) lines of 16 floats), or nullptr
     float *hsplit = nullptr;
     float bbox_lo[3] = {0.0f, 0.0f, 0.0f}, bbox_hi[3] = {0.0f, 0.0f, 0.0f}; // of the real points
     mutable Workspace ws;
@@ -156,6 +157,33 @@ __host__ __device__ inline uint32_t fkey(float f) {
 __host__ __device__ inline float fkey_inv(uint32_t k) {
     uint32_t u = (k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k;
     return __builtin_bit_cast(float, u);
+}
+
+// 4-level blocked heap: the splits of a heap of `depth` levels, cut into
+// 15-split subtrees of 4 levels, one 64-B line each (slot 15 unused), so the
+// bucketing descent reads one line per 4 levels.  The real root sits at level
+// o = hblk_offset(depth) of the first line, so the last level of splits ends a
+// line.  Lines are stored level by level: one at block level 0, 16 >> o at
+// level 1, then x16 per level; a line's 16 children are consecutive.
+__host__ __device__ inline int hblk_offset(int depth) { return (4 - depth % 4) % 4; }
+__host__ __device__ inline uint64_t hblk_level_lines(int j, int o) {
+    return j == 0 ? 1ull : (1ull << (4 * j - o));
+}
+__host__ __device__ inline uint64_t hblk_blocks(int depth) {
+    const int o = hblk_offset(depth);
+    uint64_t b = 0;
+    for (int j = 0; 4 * j < depth + o; ++j) b += hblk_level_lines(j, o);
+    return b;
+}
+// float slot of heap index h (level l, position p within its level)
+__host__ __device__ inline uint64_t hblk_slot(uint64_t h, int o) {
+    const int l = 63 - __builtin_clzll(h + 1);
+    const uint64_t p = h + 1 - (1ull << l);
+    const int v = l + o, j = v >> 2, ll = v & 3;
+    uint64_t base = 0;
+    for (int jj = 0; jj < j; ++jj) base += hblk_level_lines(jj, o);
+    const uint64_t loc = (1ull << ll) - 1 + (p & ((1ull << ll) - 1));
+    return (base + (p >> ll)) * 16 + loc;
 }
 
 } // namespace nbkd

@@ -78,39 +78,69 @@ __device__ __forceinline__ float guess_r2(uint32_t count, const float lo[3], con
     return r2 < FLT_MAX ? r2 : FLT_MAX;
 }
 
-// Bucketing descent over the heap-ordered splits (build.hip heap_splits_kernel):
-// same turns, same leaf key and seed as leaf_key2_kernel, no shape table.
+// Bucketing descent over the blocked heap of splits (internal.hpp hblk_*,
+// build.hip heap_splits_kernel): same turns, same leaf key and seed as
+// leaf_key2_kernel, one 64-B line (4 levels) per load instead of one dependent
+// load per level.
 __global__ void __launch_bounds__(TB)
-leaf_key3_kernel(const float *__restrict__ hsplit, uint32_t n8, uint32_t leaf,
+leaf_key3_kernel(const float4 *__restrict__ hb, int o, uint32_t n8, uint32_t leaf,
                  const float *__restrict__ q, uint32_t m, uint32_t *__restrict__ keys,
                  uint32_t *__restrict__ vals, float *__restrict__ tg, float mu_c, uint32_t anchor,
                  float3 box_lo, float3 box_hi) {
     for (uint32_t i = blockIdx.x * TB + threadIdx.x; i < m; i += gridDim.x * TB) {
         const float p[3] = {q[3 * (size_t)i], q[3 * (size_t)i + 1], q[3 * (size_t)i + 2]};
         uint32_t left = 0, count = n8;
-        uint64_t h = 0;
         int dim = 0;
         float lo[3] = {box_lo.x, box_lo.y, box_lo.z}, hi[3] = {box_hi.x, box_hi.y, box_hi.z};
         float r2 = FLT_MAX;
         bool have_r2 = tg == nullptr;
+        // line b of block level j (level start `base`, `nb` lines); first level l0
+        uint32_t b = 0, base = 0, nb = 1;
+        int l0 = o;
         while (count > leaf) {
-            if (!have_r2 && count <= anchor) {
-                r2 = guess_r2(count, lo, hi, mu_c);
-                have_r2 = true;
+            const float4 a0 = hb[4 * (size_t)b], a1 = hb[4 * (size_t)b + 1];
+            const float4 a2 = hb[4 * (size_t)b + 2], a3 = hb[4 * (size_t)b + 3];
+            uint32_t pos = 0; // position within the line's current level
+#pragma unroll
+            for (int l = 0; l < 4; ++l) {
+                if (l < l0) continue;
+                if (count <= leaf) break;
+                if (!have_r2 && count <= anchor) {
+                    r2 = guess_r2(count, lo, hi, mu_c);
+                    have_r2 = true;
+                }
+                float s;
+                if (l == 0)
+                    s = a0.x;
+                else if (l == 1)
+                    s = pos ? a0.z : a0.y;
+                else if (l == 2)
+                    s = (pos & 2) ? ((pos & 1) ? a1.z : a1.y) : ((pos & 1) ? a1.x : a0.w);
+                else
+                    s = (pos & 4) ? ((pos & 2) ? ((pos & 1) ? a3.z : a3.y)
+                                               : ((pos & 1) ? a3.x : a2.w))
+                                  : ((pos & 2) ? ((pos & 1) ? a2.z : a2.y)
+                                               : ((pos & 1) ? a2.x : a1.w));
+                const uint32_t mm = (count / 2) / 8 * 8;
+                const bool right = p[dim] > s; // near child, kdtree_impl.hpp:633
+                if (right) {
+                    lo[dim] = s;
+                    left += mm;
+                    count -= mm;
+                } else {
+                    hi[dim] = s;
+                    count = mm;
+                }
+                pos = 2 * pos + (right ? 1u : 0u);
+                dim = dim == 2 ? 0 : dim + 1;
             }
-            const uint32_t mm = (count / 2) / 8 * 8;
-            const float s = hsplit[h];
-            if (p[dim] > s) { // near child, kdtree_impl.hpp:633
-                lo[dim] = s;
-                left += mm;
-                count -= mm;
-                h = 2 * h + 2;
-            } else {
-                hi[dim] = s;
-                count = mm;
-                h = 2 * h + 1;
-            }
-            dim = dim == 2 ? 0 : dim + 1;
+            if (count <= leaf) break;
+            // pos = child index 0..15 of the next line
+            const uint32_t nbase = base + nb;
+            b = nbase + (b - base) * 16u + pos;
+            nb = base == 0 ? (16u >> o) : nb * 16u;
+            base = nbase;
+            l0 = 0;
         }
         if (!have_r2) r2 = guess_r2(count, lo, hi, mu_c);
         keys[i] = left >> 3;
@@ -333,12 +363,179 @@ nbkd_status device_excl_scan(Workspace &ws, uint32_t *a, uint64_t n, hipStream_t
     return NBKD_OK;
 }
 
+// ------------------------------------------------------------------ one-sweep LSD radix sort
+// One histogram read of the keys for all passes, then per 8-bit pass ONE kernel:
+// each 4096-item tile ranks its items (stable), publishes its digit counts,
+// finds its global digit offsets by decoupled look-back over the tiles before
+// it (tiles are numbered in start order by an atomic ticket, so every tile it
+// waits on is running), stages the tile digit-sorted in LDS and writes it out
+// in digit runs.  Per pass: 8 B read + 8 B written per item.
+constexpr int OS_ITEMS = 16;
+constexpr int OS_TILE = TB * OS_ITEMS; // 4096
+constexpr uint32_t OS_AGG = 1u << 30, OS_PRE = 2u << 30, OS_VAL = OS_AGG - 1;
+constexpr int OS_MAXP = 4;
+
+__global__ void __launch_bounds__(TB)
+os_hist_kernel(const uint32_t *__restrict__ keys, uint32_t n, int passes,
+               uint32_t *__restrict__ ghist) {
+    __shared__ uint32_t h[OS_MAXP][256];
+    for (int j = threadIdx.x; j < OS_MAXP * 256; j += TB) (&h[0][0])[j] = 0;
+    __syncthreads();
+    for (uint32_t i = blockIdx.x * TB + threadIdx.x; i < n; i += gridDim.x * TB) {
+        const uint32_t k = keys[i];
+        for (int p = 0; p < passes; ++p) atomicAdd(&h[p][(k >> (8 * p)) & 255u], 1u);
+    }
+    __syncthreads();
+    for (int p = 0; p < passes; ++p) {
+        const uint32_t v = h[p][threadIdx.x];
+        if (v) atomicAdd(&ghist[p * 256 + threadIdx.x], v);
+    }
+}
+
+// exclusive scan of each pass's 256 counts, in place (one block)
+__global__ void __launch_bounds__(TB) os_scan_kernel(uint32_t *__restrict__ ghist, int passes) {
+    __shared__ uint32_t sh[WPB];
+    for (int p = 0; p < passes; ++p) {
+        const uint32_t v = ghist[p * 256 + threadIdx.x];
+        ghist[p * 256 + threadIdx.x] = block_scan_excl(v, sh, nullptr);
+    }
+}
+
+__global__ void __launch_bounds__(TB)
+os_pass_kernel(const uint32_t *__restrict__ kin, const uint32_t *__restrict__ vin, uint32_t n,
+               int shift, const uint32_t *__restrict__ gexcl, uint32_t *__restrict__ status,
+               uint32_t *__restrict__ ticket, uint32_t *__restrict__ kout,
+               uint32_t *__restrict__ vout) {
+    __shared__ uint32_t wh[WPB][256]; // per wave digit counts, then wave-exclusive offsets
+    __shared__ uint32_t ls[256];      // tile-local digit start
+    __shared__ uint32_t gofs[256];    // global position of local index 0 of digit d
+    __shared__ uint32_t sk[OS_TILE], sv[OS_TILE];
+    __shared__ uint32_t sh[WPB];
+    __shared__ uint32_t tile_sh;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (tid == 0) tile_sh = atomicAdd(ticket, 1u);
+    for (int j = tid; j < WPB * 256; j += TB) (&wh[0][0])[j] = 0;
+    __syncthreads();
+    const uint32_t tile = tile_sh;
+    const uint32_t t0 = tile * (uint32_t)OS_TILE;
+    const uint32_t base = t0 + (uint32_t)wave * (OS_ITEMS * 64);
+    uint32_t kk[OS_ITEMS], vv[OS_ITEMS], rk[OS_ITEMS];
+#pragma unroll
+    for (int r = 0; r < OS_ITEMS; ++r) {
+        const uint32_t e = base + r * 64 + lane;
+        kk[r] = e < n ? kin[e] : 0xFFFFFFFFu;
+        vv[r] = e < n ? vin[e] : 0u;
+    }
+    // stable rank: items of wave w in element order, round by round
+#pragma unroll
+    for (int r = 0; r < OS_ITEMS; ++r) {
+        const uint32_t e = base + r * 64 + lane;
+        const uint32_t d = (kk[r] >> shift) & 255u;
+        uint64_t same = __ballot(e < n);
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+            const uint64_t bb = __ballot((d >> b) & 1u);
+            same &= ((d >> b) & 1u) ? bb : ~bb;
+        }
+        const uint32_t below = mbcnt64(same);
+        const uint32_t old = wh[wave][d];
+        rk[r] = old + below;
+        if (e < n && below == 0) wh[wave][d] = old + (uint32_t)__popcll(same);
+    }
+    __syncthreads();
+    {
+        const int d = tid;
+        uint32_t c = 0;
+#pragma unroll
+        for (int w = 0; w < WPB; ++w) {
+            const uint32_t x = wh[w][d];
+            wh[w][d] = c;
+            c += x;
+        }
+        uint32_t *st = status + (size_t)tile * 256 + d;
+        __hip_atomic_store(st, (tile == 0 ? OS_PRE : OS_AGG) | c, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t lsd = block_scan_excl(c, sh, nullptr);
+        ls[d] = lsd;
+        uint32_t acc = 0;
+        if (tile > 0) {
+            uint32_t tt = tile - 1;
+            for (;;) {
+                const uint32_t v = __hip_atomic_load(status + (size_t)tt * 256 + d, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT);
+                if ((v >> 30) == 0) {
+                    __builtin_amdgcn_s_sleep(1);
+                    continue;
+                }
+                acc += v & OS_VAL;
+                if (v & OS_PRE) break;
+                --tt;
+            }
+            __hip_atomic_store(st, OS_PRE | (acc + c), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        gofs[d] = gexcl[d] + acc - lsd;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < OS_ITEMS; ++r) {
+        const uint32_t e = base + r * 64 + lane;
+        if (e < n) {
+            const uint32_t d = (kk[r] >> shift) & 255u;
+            const uint32_t pos = ls[d] + wh[wave][d] + rk[r];
+            sk[pos] = kk[r];
+            sv[pos] = vv[r];
+        }
+    }
+    __syncthreads();
+    const uint32_t cnt = min((uint32_t)OS_TILE, n - t0);
+#pragma unroll
+    for (int r = 0; r < OS_ITEMS; ++r) {
+        const uint32_t i = r * TB + tid;
+        if (i < cnt) {
+            const uint32_t k = sk[i];
+            const uint32_t dst = gofs[(k >> shift) & 255u] + i;
+            kout[dst] = k;
+            vout[dst] = sv[i];
+        }
+    }
+}
+
+nbkd_status onesweep_sort(Workspace &ws, uint32_t *k0, uint32_t *v0, uint32_t *k1, uint32_t *v1,
+                          uint32_t n, int passes, hipStream_t s) {
+    const uint32_t ntiles = (n + OS_TILE - 1) / OS_TILE;
+    // [passes][256] histogram | [passes] tickets (padded to 64 words) | [passes][ntiles][256] status
+    const size_t words = (size_t)passes * 256 + 64 + (size_t)passes * ntiles * 256;
+    uint32_t *w = (uint32_t *)ws.get(WS_HIST, words * 4, s);
+    if (!w) return NBKD_ENOMEM;
+    NBKD_HIP(hipMemsetAsync(w, 0, words * 4, s));
+    uint32_t *ghist = w, *tickets = w + passes * 256, *status = tickets + 64;
+    const unsigned hb = (unsigned)std::min<uint32_t>((n + TB - 1) / TB, 2048);
+    os_hist_kernel<<<hb, TB, 0, s>>>(k0, n, passes, ghist);
+    os_scan_kernel<<<1, TB, 0, s>>>(ghist, passes);
+    for (int p = 0; p < passes; ++p) {
+        uint32_t *ki = (p & 1) ? k1 : k0, *vi = (p & 1) ? v1 : v0;
+        uint32_t *ko = (p & 1) ? k0 : k1, *vo = (p & 1) ? v0 : v1;
+        os_pass_kernel<<<ntiles, TB, 0, s>>>(ki, vi, n, 8 * p, ghist + p * 256, status +
+                                             (size_t)p * ntiles * 256, tickets + p, ko, vo);
+    }
+    NBKD_HIP(hipGetLastError());
+    return NBKD_OK;
+}
+
 // sorts (keys, vals) by the low `nbits` of keys, ceil(nbits/8) LSD passes
 // ping-ponging between (k0, v0) and (k1, v1); *vout = the sorted values
 nbkd_status radix_sort(Workspace &ws, uint32_t *k0, uint32_t *v0, uint32_t *k1, uint32_t *v1,
                        uint32_t n, int nbits, hipStream_t s, uint32_t **vout) {
     *vout = v0;
     if (n <= 1) return NBKD_OK;
+    {
+        static const bool old_sort = getenv("NBKD_OLD_SORT") != nullptr; // A/B only
+        const int passes = (nbits + 7) / 8;
+        if (!old_sort && n < OS_VAL && passes <= OS_MAXP) {
+            *vout = (passes & 1) ? v1 : v0;
+            return onesweep_sort(ws, k0, v0, k1, v1, n, passes, s);
+        }
+    }
     const uint32_t ntiles = (n + RS_TILE - 1) / RS_TILE;
     uint32_t *hist = (uint32_t *)ws.get(WS_HIST, (size_t)256 * ntiles * 4, s);
     if (!hist) return NBKD_ENOMEM;
@@ -644,7 +841,8 @@ nbkd_status sort_queries(const Tree &t, const float *dq, uint32_t m, uint32_t *&
                                          : make_float3(t.bbox_lo[0], t.bbox_lo[1], t.bbox_lo[2]);
             const float3 hi = t.periodic ? make_float3(t.box, t.box, t.box)
                                          : make_float3(t.bbox_hi[0], t.bbox_hi[1], t.bbox_hi[2]);
-            leaf_key3_kernel<<<blocks, TB, 0, s>>>(t.hsplit, (uint32_t)t.n8, (uint32_t)t.leaf, dq, m,
+            leaf_key3_kernel<<<blocks, TB, 0, s>>>((const float4 *)t.hsplit, hblk_offset(t.depth),
+                                                   (uint32_t)t.n8, (uint32_t)t.leaf, dq, m,
                                                    keys, order, tg, sp ? sp->mu_c : 0.0f,
                                                    sp ? sp->anchor : 0u, lo, hi);
         } else if (t.shape_len <= SHAPE_MAX) {
