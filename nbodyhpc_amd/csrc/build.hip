@@ -558,7 +558,8 @@ leafinfo_kernel(const nbkd_node *__restrict__ nodes, uint64_t nn, const float *_
 // levels sit together in a few KB (cache resident).  One thread per leaf walks
 // from the root and writes every ancestor whose first point is the leaf's first
 // point (each internal node exactly once); preorder ids come from the shape
-// table as in leaf_key2_kernel.
+// table as in leaf_key2_kernel.  Stored in the 4-level blocked layout
+// (internal.hpp hblk_slot): one 64-B line per 4-level subtree.
 __global__ void __launch_bounds__(TB)
 heap_splits_kernel(const nbkd_node *__restrict__ nodes, uint64_t nn, const float *__restrict__ splits,
                    const uint32_t *__restrict__ shape_c, const uint32_t *__restrict__ shape_n,

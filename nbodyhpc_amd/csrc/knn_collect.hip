@@ -15,10 +15,10 @@
 //            majority vote of the lanes that want the node; a leaf is scanned
 //            only by the lanes whose query ball reaches its TIGHT bounding box
 //            (leafinfo), its points staged in LDS by direct global->LDS loads.
-//            Each query's ball is its seed radius (leaf_key2_kernel), which is
+//            Each query's ball is its seed radius (leaf_key3_kernel), which is
 //            expected to hold k + 4 sqrt(k) + 4 points; every point inside it
 //            is appended to the query's candidate column in HBM.  No top-k is
-//            kept, so the kernel needs few VGPRs and ~2 KB of LDS per wave and
+//            kept, so the kernel needs few VGPRs and ~3 KB of LDS per wave and
 //            runs 8 waves per SIMD.
 //   select   one lane per query merges its column 16 candidates at a time into
 //            a sorted register top-k (bitonic networks) and writes the rows
