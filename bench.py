@@ -55,6 +55,12 @@ def parse():
                    help="queries timed on the CPU baseline (rank 0, N=1)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-parity", action="store_true")
+    p.add_argument("--suite", action="store_true",
+                   help="also measure SURVEY §8(d)'s secondary runs (independent uniform "
+                        "queries, C3 radius count + CSR batch, log-normal kNN) into 'suite'")
+    p.add_argument("--radius", type=float, default=0.01, help="C3 radius, units of L")
+    p.add_argument("--csr-batch", type=int, default=1_000_000)
+    p.add_argument("--lognormal-grid", type=int, default=512)
     return p.parse_args()
 
 
@@ -101,6 +107,98 @@ def cpu_baseline(points, k, leafsize, box, sample, gpu_d, gpu_i):
                       f"{len(points):.0e}-point periodic tree, k={k}, leafsize={leafsize}, "
                       f"{cores} threads; single-threaded CPU build {build_s:.2f} s",
             "build_s": build_s}, parity
+
+
+def timed(fn, steps, hip):
+    """fn() `steps` times between device synchronisations; seconds per call."""
+    hip.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    hip.synchronize()
+    return (time.perf_counter() - t0) / steps
+
+
+def suite(args, capi, hip, tree, dev_pts, n, k, L, stream, od, oi):
+    """SURVEY.md §8(d) secondary runs on one GPU (not the headline `value`)."""
+    from nbodyhpc_amd import synth
+    out = {}
+    steps = max(1, min(args.steps, 3))
+    # (ii) independent uniform query set of the same size, same tree
+    qh = synth.uniform(n, synth.SEED_QUERIES, L)
+    dq = hip.DeviceArray.from_numpy(qh)
+    del qh
+    tree.query_device(dq.ptr, n, k, od.ptr, oi.ptr, stream.handle)
+    sec = timed(lambda: tree.query_device(dq.ptr, n, k, od.ptr, oi.ptr, stream.handle), steps, hip)
+    out["knn_independent_queries"] = {"queries_per_s": n / sec, "ms": sec * 1e3, "k": k,
+                                      "queries": n, "query_seed": synth.SEED_QUERIES}
+    log(f"suite: independent queries {n / sec:.3e} q/s")
+    # C3: radius count of every particle (self-queries), r = 0.01 L
+    r = args.radius * L
+    cnt = hip.DeviceArray((n,), np.uint32)
+    tree.ball_count_device(dev_pts.ptr, n, r, cnt.ptr, stream.handle)
+    capi.timing_reset()
+    capi.timing_enable(True)
+    sec = timed(lambda: tree.ball_count_device(dev_pts.ptr, n, r, cnt.ptr, stream.handle),
+                steps, hip)
+    kern_ms, _ = capi.timing_read("ball_count")
+    capi.timing_enable(False)
+    c = cnt.numpy()
+    expect = n * 4.0 / 3.0 * math.pi * args.radius ** 3
+    out["radius_count"] = {"queries_per_s": n / sec, "ms": sec * 1e3,
+                           "kernel_ms": kern_ms / steps, "r": r, "mean_count": float(c.mean()),
+                           "expected_mean_count": expect, "queries": n}
+    log(f"suite: radius count {n / sec:.3e} q/s, mean {c.mean():.1f} (expect {expect:.1f})")
+    # C3: CSR batch (host in / host out: PCIe-inclusive)
+    b = min(args.csr_batch, n)
+    qb = dev_pts.numpy_head(b)
+    t0 = time.perf_counter()
+    off, idx = tree.ball_csr(qb, r)
+    sec = time.perf_counter() - t0
+    ok = bool(np.array_equal(np.diff(off.astype(np.int64)), c[:b].astype(np.int64)))
+    out["radius_csr_batch"] = {"queries": b, "ms_host_to_host": sec * 1e3,
+                               "neighbours": int(off[-1]), "counts_match_count_pass": ok}
+    del off, idx, qb, c
+    cnt.free()
+    dq.free()
+    # C5-style log-normal set at the same N (GRF 512^3, P(k) ~ k^-2), self-queries
+    t0 = time.perf_counter()
+    lp = synth.lognormal(n, box=L, grid=args.lognormal_grid)
+    gen_s = time.perf_counter() - t0
+    dl = hip.DeviceArray.from_numpy(lp)
+    del lp
+    bt = []
+    for _ in range(2):
+        hip.synchronize()
+        t0 = time.perf_counter()
+        lt = capi.Tree(n=n, dev_ptr=dl.ptr, leafsize=args.leafsize, boxsize=L,
+                       stream=stream.handle)
+        hip.synchronize()
+        bt.append((time.perf_counter() - t0) * 1e3)
+        if _ == 0:
+            lt.close()
+    lt.query_device(dl.ptr, n, k, od.ptr, oi.ptr, stream.handle)
+    capi.timing_reset()
+    capi.timing_enable(True)
+    sec = timed(lambda: lt.query_device(dl.ptr, n, k, od.ptr, oi.ptr, stream.handle), steps, hip)
+    br = {nm: capi.timing_read(nm)[0] / steps for nm in
+          ("leaf_key", "sort", "knn_collect", "knn_select", "knn_retry_order", "knn_retry",
+           "knn_fallback")}
+    capi.timing_enable(False)
+    capi.stats_enable(True)
+    lt.query_device(dl.ptr, n, k, od.ptr, oi.ptr, stream.handle)
+    stream.synchronize()
+    st = capi.stats_read_all()
+    capi.stats_enable(False)
+    out["knn_lognormal"] = {"queries_per_s": n / sec, "ms": sec * 1e3, "build_ms": min(bt),
+                            "breakdown_ms": br, "retry_queries": st["retry_queries"],
+                            "fallback_queries": st["fallback_queries"],
+                            "grid": args.lognormal_grid, "generate_s": gen_s,
+                            "seed": synth.SEED_LOGNORMAL}
+    log(f"suite: log-normal kNN {n / sec:.3e} q/s, build {min(bt):.1f} ms")
+    lt.close()
+    dl.free()
+    return out
 
 
 def main():
@@ -225,6 +323,7 @@ def main():
     oob_ms, _ = capi.timing_read("knn_outside_box")
     fb_ms, _ = capi.timing_read("knn_fallback")
     rt_ms, _ = capi.timing_read("knn_retry")
+    rto_ms, _ = capi.timing_read("knn_retry_order")
     col_ms, col_launches = capi.timing_read("knn_collect")
     sel_ms, _ = capi.timing_read("knn_select")
     capi.timing_enable(False)
@@ -235,7 +334,7 @@ def main():
     step()
     stream.synchronize()
     st = capi.stats_read_all()
-    nodes_vis, pts_scanned = st["node_lane_visits"], st["pair_evals"]
+    pts_scanned = st["pair_evals"]
     capi.stats_enable(False)
 
     gpu_d = gpu_i = None
@@ -271,6 +370,9 @@ def main():
                 traffic = pm.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
+    extra = None
+    if world == 1 and args.suite:
+        extra = suite(args, capi, hip, tree, dev_pts, n, k, L, stream, od, oi)
     cpu = None
     parity = None
     if world == 1 and not args.no_cpu_baseline:
@@ -310,19 +412,23 @@ def main():
             "leaf_key": key_ms / args.steps, "sort": sort_ms / args.steps,
             "knn": knn_ms / args.steps, "knn_collect": col_ms / args.steps,
             "knn_select": sel_ms / args.steps, "outside_box_check": oob_ms / args.steps,
-            "retry": rt_ms / args.steps, "fallback": fb_ms / args.steps,
+            "retry": (rt_ms + rto_ms) / args.steps, "fallback": fb_ms / args.steps,
         },
-        "traversal_per_query": {"nodes_visited": nodes_vis / own,
-                                "distance_evals": pts_scanned / own},
+        # one packet = 64 queries walking the tree together: node visits are
+        # per packet walk; distance evaluations are per (query, point) pair
+        "traversal_per_query": {"distance_evals": pts_scanned / own,
+                                "candidates": st["candidates"] / own},
         "traversal_per_packet": {kk: st[kk] / max(st["packets"], 1)
-                                 for kk in ("dense_steps", "sparse_iters", "points_staged",
-                                            "candidates", "leaves_scanned")},
+                                 for kk in ("node_visits", "dense_steps", "sparse_iters",
+                                            "points_staged", "candidates", "leaves_scanned")},
         "fallback_queries": st["fallback_queries"], "retry_queries": st["retry_queries"],
         "cpu_baseline": None if cpu is None else {kk: cpu[kk] for kk in
                                                   ("value", "unit", "cores", "kind", "sample")},
         "cpu_build_ms": None if cpu is None else cpu["build_s"] * 1e3,
         "parity_vs_cpu": parity,
     }
+    if extra is not None:
+        out["suite"] = extra
     print(json.dumps(out), flush=True)
 
 

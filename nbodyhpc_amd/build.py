@@ -28,7 +28,8 @@ ARCH = os.environ.get("NBKD_ARCH", "gfx950")
 # squared distances stop being bit-identical.
 HIP_FLAGS = ["--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
              "-Wall", "-Wno-unused-function", "-Wno-unused-const-variable"]
-SOURCES = ["api.cpp", "build.hip", "query.hip", "knn_packet.hip", "knn_collect.hip", "slab.hip"]
+SOURCES = ["api.cpp", "build.hip", "query.hip", "knn_packet.hip", "knn_collect.hip", "ball.hip",
+           "slab.hip"]
 HEADERS = [os.path.join(CSRC, "internal.hpp"), os.path.join(CSRC, "metric.hpp"),
            os.path.join(CSRC, "packet.hpp"),
            os.path.join(ROOT, "include", "nbkd.h")]

@@ -224,7 +224,7 @@ def stats_read():
 # sparse (lane-compacted) iterations, leaf points staged, packets (waves),
 # candidates appended, leaves scanned, queries sent to the exact kernel,
 # queries retried with a larger seed ball
-STATS_NAMES = ("node_lane_visits", "pair_evals", "dense_steps", "sparse_iters", "points_staged",
+STATS_NAMES = ("node_visits", "pair_evals", "dense_steps", "sparse_iters", "points_staged",
                "packets", "candidates", "leaves_scanned", "fallback_queries", "retry_queries")
 
 

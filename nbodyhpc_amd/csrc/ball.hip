@@ -1,0 +1,283 @@
+// Radius queries (NEW, SURVEY.md §8(a) a14 / §8(f) rank 1: the reference has
+// no radius search): count, or list, the points with d2 <= r2 around each
+// query, d2 in the reference's f32 point metric (kdtree.hpp:20-121, the a10
+// formula: ((dx^2 + dy^2) + dz^2), periodic per-axis minimum image).
+//
+// Same packet walk as knn_collect_kernel with a fixed bound r2: one wave64 =
+// 64 kd-ordered queries walking the tree together, near child first by
+// majority vote; at a leaf the lanes whose ball reaches the leaf's tight box
+// take part.  A lane whose ball CONTAINS the tight box (an upper bound of the
+// f32 d2 over the box <= r2) counts the leaf's points without evaluating them;
+// the others evaluate the points staged in LDS.
+//
+// Periodic queries outside [0, L]^3 are excluded here (their minimum-image
+// pruning is not a bound) and answered by ball_brute_kernel below.
+#include "internal.hpp"
+#include "metric.hpp"
+#include "packet.hpp"
+
+namespace nbkd {
+namespace {
+using namespace dev;
+
+constexpr int TB = 256;
+constexpr int WPB = TB / 64;
+constexpr int CHUNK = 32;
+
+struct PadLeaves {
+    uint32_t id[NBKD_PAD_LEAVES];
+};
+
+struct alignas(16) BallLds {
+    float pb[3][CHUNK];
+    uint32_t pid[CHUNK];
+};
+
+// upper bound of the f32 d2 of point_d2_fast over every point of the box: per
+// axis |fl(x - q)| is monotone in x, so it is at most the larger end value; the
+// periodic minimum image only lowers it
+template <bool PER>
+__device__ __forceinline__ float box_ub2(float qx, float qy, float qz, const float b[6]) {
+    const float ux = fmaxf(fabsf(b[0] - qx), fabsf(b[1] - qx));
+    const float uy = fmaxf(fabsf(b[2] - qy), fabsf(b[3] - qy));
+    const float uz = fmaxf(fabsf(b[4] - qz), fabsf(b[5] - qz));
+    return (ux * ux + uy * uy) + uz * uz;
+}
+
+template <bool PER, bool FILL>
+__global__ void __launch_bounds__(TB, 8)
+ball_packet_kernel(DevTree t, const uint32_t *__restrict__ linfo, const float *__restrict__ q,
+                   const uint32_t *__restrict__ order, uint32_t m, float r2, PadLeaves pad,
+                   uint32_t *__restrict__ out_count, const uint64_t *__restrict__ row_offsets,
+                   uint32_t *__restrict__ out_idx) {
+    __shared__ BallLds Wl[WPB];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    BallLds &W = Wl[wave];
+    const uint32_t gq = (blockIdx.x * WPB + wave) * 64u + lane;
+    const bool valid = gq < m;
+    const uint32_t qo = valid ? order[gq] : 0u;
+    const float qx = valid ? q[3 * (size_t)qo] : 0.0f;
+    const float qy = valid ? q[3 * (size_t)qo + 1] : 0.0f;
+    const float qz = valid ? q[3 * (size_t)qo + 2] : 0.0f;
+    const float L = t.box;
+    const bool inside =
+        !PER || (qx >= 0.0f && qx <= L && qy >= 0.0f && qy <= L && qz >= 0.0f && qz <= L);
+    const bool active = valid && inside;
+    const float thr = active ? r2 : -INFINITY;
+    uint64_t wpos = (FILL && active) ? row_offsets[qo] : 0;
+    uint32_t cnt = 0;
+
+    uint32_t sk_node = 0;
+    float sk_b[6] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+    int sp = 0;
+    const cnode_ptr cnodes = (cnode_ptr)t.nodes;
+    uint32_t node = 0;
+    float bx[6];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        bx[2 * a] = PER ? 0.0f : -FLT_MAX;
+        bx[2 * a + 1] = PER ? L : FLT_MAX;
+    }
+    float tm[3] = {box_lb_axis<PER>(qx, bx[0], bx[1], L), box_lb_axis<PER>(qy, bx[2], bx[3], L),
+                   box_lb_axis<PER>(qz, bx[4], bx[5], L)};
+    uint64_t wm = __ballot((tm[0] + tm[1]) + tm[2] <= thr);
+    bool have = wm != 0;
+
+    for (;;) {
+        bool found = false;
+        uint32_t lpos = 0, lend = 0;
+        for (;;) {
+            if (!have) {
+                if (sp == 0) break;
+                --sp;
+                node = __builtin_amdgcn_readlane(sk_node, sp);
+#pragma unroll
+                for (int a = 0; a < 6; ++a) bx[a] = rdlane(sk_b[a], sp);
+                tm[0] = box_lb_axis<PER>(qx, bx[0], bx[1], L);
+                tm[1] = box_lb_axis<PER>(qy, bx[2], bx[3], L);
+                tm[2] = box_lb_axis<PER>(qz, bx[4], bx[5], L);
+                wm = __ballot((tm[0] + tm[1]) + tm[2] <= thr);
+                if (wm == 0) continue;
+            }
+            have = false;
+            const nbkd_node nd = cnodes[node];
+            const int dim = nd.dimension;
+            if (dim < 0) {
+                lpos = nd.left;
+                lend = nd.right;
+                found = true;
+                break;
+            }
+            const float split = nd.split;
+            const float qd = dim == 0 ? qx : (dim == 1 ? qy : qz);
+            const float lo = dim == 0 ? bx[0] : (dim == 1 ? bx[2] : bx[4]);
+            const float hi = dim == 0 ? bx[1] : (dim == 1 ? bx[3] : bx[5]);
+            const float tl = box_lb_axis<PER>(qd, lo, split, L);
+            const float tr = box_lb_axis<PER>(qd, split, hi, L);
+            const float dl = ((dim == 0 ? tl : tm[0]) + (dim == 1 ? tl : tm[1])) + (dim == 2 ? tl : tm[2]);
+            const float dr = ((dim == 0 ? tr : tm[0]) + (dim == 1 ? tr : tm[1])) + (dim == 2 ? tr : tm[2]);
+            const uint64_t wl = __ballot(dl <= thr), wr = __ballot(dr <= thr);
+            const uint32_t right_votes = (uint32_t)__popcll(wm & __ballot(qd > split));
+            const bool right_first = 2 * right_votes > (uint32_t)__popcll(wm);
+            const uint64_t wn = right_first ? wr : wl, wf = right_first ? wl : wr;
+            const int near_slot = right_first ? 2 * dim : 2 * dim + 1;
+            const int far_slot = right_first ? 2 * dim + 1 : 2 * dim;
+            const uint32_t sb = __float_as_uint(split);
+            if (wn != 0 && wf != 0) {
+                const uint32_t far_node = right_first ? nd.left : nd.right;
+                const bool me = lane == sp;
+                sk_node = me ? far_node : sk_node;
+#pragma unroll
+                for (int a = 0; a < 6; ++a) {
+                    const uint32_t fv =
+                        __builtin_amdgcn_readfirstlane(a == far_slot ? sb : __float_as_uint(bx[a]));
+                    sk_b[a] = me ? __uint_as_float(fv) : sk_b[a];
+                }
+                ++sp;
+            }
+            if (wn == 0 && wf == 0) continue;
+            const bool go_near = wn != 0;
+            const int slot = go_near ? near_slot : far_slot;
+            const bool go_right = go_near == right_first;
+            node = go_right ? nd.right : nd.left;
+            const float tnew = go_right ? tr : tl;
+#pragma unroll
+            for (int a = 0; a < 3; ++a) tm[a] = dim == a ? tnew : tm[a];
+#pragma unroll
+            for (int a = 0; a < 6; ++a)
+                bx[a] = __uint_as_float(__builtin_amdgcn_readfirstlane(a == slot ? sb : __float_as_uint(bx[a])));
+            wm = go_near ? wn : wf;
+            have = true;
+        }
+        if (!found) break;
+
+        // leaf: tight box first (lanes < 6), then the chunks
+        const uint32_t iw = lane < 6 ? linfo[8 * (size_t)node + lane] : 0u;
+        const float tb[6] = {rdlane(__uint_as_float(iw), 0), rdlane(__uint_as_float(iw), 3),
+                             rdlane(__uint_as_float(iw), 1), rdlane(__uint_as_float(iw), 4),
+                             rdlane(__uint_as_float(iw), 2), rdlane(__uint_as_float(iw), 5)};
+        const bool need = box_lb2<PER>(qx, qy, qz, tb, L) <= thr;
+        if (!__any(need)) continue;
+        // a leaf holding padding points (FLT_MAX, never inside) is always evaluated
+        bool padded = false;
+#pragma unroll
+        for (int j = 0; j < NBKD_PAD_LEAVES; ++j) padded |= pad.id[j] == node;
+        const bool full = need && !padded && box_ub2<PER>(qx, qy, qz, tb) <= thr;
+        const bool part = need && !full;
+        if constexpr (!FILL) {
+            if (full) cnt += lend - lpos;
+            if (!__any(part)) continue;
+        }
+        for (uint32_t c0 = lpos; c0 < lend; c0 += CHUNK) {
+            const uint32_t cn = min((uint32_t)CHUNK, lend - c0);
+            wave_sync();
+            glds_f32(t.x + c0, W.pb[0], lane, cn);
+            glds_f32(t.y + c0, W.pb[1], lane, cn);
+            glds_f32(t.z + c0, W.pb[2], lane, cn);
+            if constexpr (FILL)
+                glds_f32(reinterpret_cast<const float *>(t.idx) + c0,
+                         reinterpret_cast<float *>(W.pid), lane, cn);
+            wait_vm0();
+            wave_sync();
+            if constexpr (FILL) {
+                if (full) {
+#pragma unroll 1
+                    for (uint32_t u = 0; u < cn; ++u) out_idx[wpos + cnt + u] = W.pid[u];
+                    cnt += cn;
+                }
+            }
+            if (part) {
+                // 4 staged points per step (float4 LDS reads); slots past cn hold
+                // stale data and are masked
+#pragma unroll 1
+                for (uint32_t u0 = 0; u0 < cn; u0 += 4) {
+                    const float4 xv = *reinterpret_cast<const float4 *>(&W.pb[0][u0]);
+                    const float4 yv = *reinterpret_cast<const float4 *>(&W.pb[1][u0]);
+                    const float4 zv = *reinterpret_cast<const float4 *>(&W.pb[2][u0]);
+                    const float d[4] = {point_d2_fast<PER>(qx, qy, qz, xv.x, yv.x, zv.x, L),
+                                        point_d2_fast<PER>(qx, qy, qz, xv.y, yv.y, zv.y, L),
+                                        point_d2_fast<PER>(qx, qy, qz, xv.z, yv.z, zv.z, L),
+                                        point_d2_fast<PER>(qx, qy, qz, xv.w, yv.w, zv.w, L)};
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        if (u0 + j < cn && d[j] <= thr) {
+                            if constexpr (FILL) out_idx[wpos + cnt] = W.pid[u0 + j];
+                            ++cnt;
+                        }
+                    }
+                }
+            }
+        }
+    }
+    if (active && out_count) out_count[qo] = cnt;
+}
+
+// Periodic queries outside [0, L]^3 (unvalidated input, as in the reference's
+// kNN): no box bound is valid for the reference's per-axis metric there, so
+// every point is tested.  Grid: x = point tiles, y = listed query.  Counts
+// accumulate with atomics into out_count (zeroed first); a fill appends at
+// row_offsets[q] + atomicAdd(fill[j]) (rows are sets).
+constexpr int BR_ITEMS = 8;
+__global__ void __launch_bounds__(TB)
+ball_brute_kernel(DevTree t, const float *__restrict__ q, const uint32_t *__restrict__ list,
+                  float r2, uint32_t *__restrict__ out_count, uint32_t *__restrict__ fill,
+                  const uint64_t *__restrict__ row_offsets, uint32_t *__restrict__ out_idx) {
+    const uint32_t j = blockIdx.y, qo = list[j];
+    const float qx = q[3 * (size_t)qo], qy = q[3 * (size_t)qo + 1], qz = q[3 * (size_t)qo + 2];
+    const float L = t.box;
+    uint32_t c = 0;
+    const uint32_t base = blockIdx.x * (uint32_t)(TB * BR_ITEMS) + threadIdx.x;
+#pragma unroll
+    for (int u = 0; u < BR_ITEMS; ++u) {
+        const uint32_t p = base + u * TB;
+        if (p < t.n8 && point_d2<true>(qx, qy, qz, t.x[p], t.y[p], t.z[p], L) <= r2) {
+            if (out_idx) out_idx[row_offsets[qo] + atomicAdd(&fill[j], 1u)] = t.idx[p];
+            ++c;
+        }
+    }
+    if (out_count) {
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+        if ((threadIdx.x & 63) == 0 && c) atomicAdd(&out_count[qo], c);
+    }
+}
+
+__global__ void ball_zero_kernel(const uint32_t *__restrict__ list, uint32_t nout,
+                                 uint32_t *__restrict__ out_count, uint32_t *__restrict__ fill) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= nout) return;
+    if (out_count) out_count[list[j]] = 0;
+    if (fill) fill[j] = 0;
+}
+
+} // namespace
+
+void launch_ball_outside(const Tree &t, const float *q, const uint32_t *list, uint32_t nout,
+                         float r2, uint32_t *out_count, uint32_t *fill,
+                         const uint64_t *row_offsets, uint32_t *out_idx, hipStream_t s) {
+    if (nout == 0) return;
+    ball_zero_kernel<<<(nout + TB - 1) / TB, TB, 0, s>>>(list, nout, out_count, fill);
+    const dim3 grid((unsigned)((t.n8 + TB * BR_ITEMS - 1) / (TB * BR_ITEMS)), nout);
+    ball_brute_kernel<<<grid, TB, 0, s>>>(view(t), q, list, r2, out_count, fill, row_offsets,
+                                          out_idx);
+}
+
+void launch_ball_packet(const Tree &t, const float *q, const uint32_t *order, uint32_t m, float r2,
+                        uint32_t *out_count, const uint64_t *row_offsets, uint32_t *out_idx,
+                        hipStream_t s) {
+    const unsigned blocks = (unsigned)((m + TB - 1) / TB);
+    PadLeaves pad;
+    for (int j = 0; j < NBKD_PAD_LEAVES; ++j)
+        pad.id[j] = t.npad_leaves <= NBKD_PAD_LEAVES ? t.pad_leaves[j] : 0xFFFFFFFFu;
+#define NBKD_BALL(PER, FILL)                                                                   \
+    ball_packet_kernel<PER, FILL><<<blocks, TB, 0, s>>>(view(t), t.leafinfo, q, order, m, r2,  \
+                                                        pad, out_count, row_offsets, out_idx)
+    if (t.periodic) {
+        if (out_idx) NBKD_BALL(true, true); else NBKD_BALL(true, false);
+    } else {
+        if (out_idx) NBKD_BALL(false, true); else NBKD_BALL(false, false);
+    }
+#undef NBKD_BALL
+}
+
+} // namespace nbkd

@@ -505,13 +505,19 @@ leafinfo_kernel(const nbkd_node *__restrict__ nodes, uint64_t nn, const float *_
                 const float *__restrict__ y, const float *__restrict__ z,
                 const uint32_t *__restrict__ idx, uint64_t n, uint32_t *__restrict__ info,
                 uint32_t *__restrict__ bbox) {
+    // bbox[0..6): data bounding box keys; bbox[6]: number of leaves holding
+    // padding, bbox[7..7+NBKD_PAD_LEAVES): their node ids
     float blo[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, bhi[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
     for (uint64_t i = blockIdx.x * (uint64_t)TB + threadIdx.x; i < nn; i += (uint64_t)gridDim.x * TB) {
         const nbkd_node nd = nodes[i];
         if (nd.dimension >= 0) continue;
         float lo[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, hi[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+        bool pad = false;
         for (uint32_t j = nd.left; j < nd.right; ++j) {
-            if (idx[j] >= n) continue;
+            if (idx[j] >= n) {
+                pad = true;
+                continue;
+            }
             const float p[3] = {x[j], y[j], z[j]};
 #pragma unroll
             for (int a = 0; a < 3; ++a) {
@@ -523,6 +529,10 @@ leafinfo_kernel(const nbkd_node *__restrict__ nodes, uint64_t nn, const float *_
         for (int a = 0; a < 3; ++a) {
             blo[a] = fminf(blo[a], lo[a]);
             bhi[a] = fmaxf(bhi[a], hi[a]);
+        }
+        if (pad && bbox) {
+            const uint32_t slot = atomicAdd(&bbox[6], 1u);
+            if (slot < (uint32_t)NBKD_PAD_LEAVES) bbox[7 + slot] = (uint32_t)i;
         }
         uint32_t *o = info + 8 * i;
         const float4 w0 = make_float4(lo[0], lo[1], lo[2], hi[0]);
@@ -834,15 +844,21 @@ nbkd_status build_tree(Tree &t, const float *xyz, uint64_t n, int32_t leaf_size,
         NBKD_HIP(hipMalloc(&t.leafinfo, std::max<uint64_t>(t.nnodes, 1) * 32));
         uint64_t blocks = std::min<uint64_t>((t.nnodes + TB - 1) / TB, 16384);
         DevBuf d_bbox;
-        NBKD_HIP(d_bbox.alloc(6 * 4, s));
-        const uint32_t init[6] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u, 0u};
+        constexpr int NW = 7 + NBKD_PAD_LEAVES;
+        NBKD_HIP(d_bbox.alloc(NW * 4, s));
+        uint32_t init[NW] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u, 0u, 0u};
         NBKD_HIP(hipMemcpyAsync(d_bbox.p, init, sizeof(init), hipMemcpyHostToDevice, s));
         leafinfo_kernel<<<(unsigned)std::max<uint64_t>(blocks, 1), TB, 0, s>>>(
             t.nodes, t.nnodes, t.x, t.y, t.z, t.idx, t.n, t.leafinfo, d_bbox.as<uint32_t>());
         NBKD_HIP(hipGetLastError());
-        uint32_t hb[6];
+        uint32_t hb[NW];
         NBKD_HIP(hipMemcpyAsync(hb, d_bbox.p, sizeof(hb), hipMemcpyDeviceToHost, s));
         NBKD_HIP(hipStreamSynchronize(s));
+        // padding sits in the last leaf; should ties ever spread it, up to
+        // NBKD_PAD_LEAVES leaves are listed, beyond that the shortcut is off
+        t.npad_leaves = (int)hb[6];
+        for (int j = 0; j < NBKD_PAD_LEAVES; ++j)
+            t.pad_leaves[j] = j < (int)hb[6] ? hb[7 + j] : 0xFFFFFFFFu;
         for (int a = 0; a < 3; ++a) {
             t.bbox_lo[a] = hb[a] == 0xFFFFFFFFu ? 0.0f : fkey_inv(hb[a]);
             t.bbox_hi[a] = hb[3 + a] == 0u ? 0.0f : fkey_inv(hb[3 + a]);

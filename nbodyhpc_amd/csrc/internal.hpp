@@ -18,7 +18,7 @@ namespace nbkd {
 enum WsSlot {
     WS_Q = 0, WS_KEYS, WS_KEYS2, WS_ORDER, WS_TMP, WS_HIST, WS_SUMS, WS_OUTD, WS_OUTI,
     WS_COUNT, WS_OFF, WS_IDX, WS_STATS, WS_LIST, WS_LT, WS_TG, WS_CAND, WS_CCOUNT,
-    WS_LIST2, WS_NSLOTS
+    WS_LIST2, WS_RSORT, WS_NSLOTS
 };
 struct Workspace {
     std::mutex mu;
@@ -28,6 +28,8 @@ struct Workspace {
     void *get(int slot, size_t bytes, hipStream_t s);
     void release();
 };
+
+constexpr int NBKD_PAD_LEAVES = 8;
 
 // Device-resident tree.  Points are SoA in tree order (the reference layout,
 // kdtree/src/cpp/include/kdtree/position_array.hpp:166-271): x, y, z, original
@@ -55,6 +57,10 @@ struct Tree {
     // (hblk_blocks(depth) lines of 16 floats), or nullptr
     float *hsplit = nullptr;
     float bbox_lo[3] = {0.0f, 0.0f, 0.0f}, bbox_hi[3] = {0.0f, 0.0f, 0.0f}; // of the real points
+    // leaves holding padding points (FLT_MAX, n <= position id < n8): node ids
+    int npad_leaves = 0;
+    uint32_t pad_leaves[NBKD_PAD_LEAVES] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu,
+                                            0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
     mutable Workspace ws;
 };
 
@@ -132,14 +138,26 @@ void launch_knn_packet(const Tree &t, const float *q, const uint32_t *order, uin
 
 // knn_collect.hip: candidate column capacity for k, and one collect + select
 // pass over m queries (order[0..m) = query ids; tg = seed bounds, scaled by
-// seed_mul; qpp = queries per packet: 64 for kd-ordered batches, 1 for the
-// retry of scattered seed failures)
+// seed_mul; qpp = queries per packet, 64 or 1; failures are listed as query
+// ids, or as sorted positions pos_base + i when pos_base != ~0u; retry names
+// the timers)
 uint32_t collect_capacity(int k);
 nbkd_status launch_knn_collect(const Tree &t, const float *q, const uint32_t *order, uint32_t m,
                                int k, const float *tg, float seed_mul, uint32_t qpp, uint2 *cand,
                                uint32_t capg, uint32_t *ccount, float *od, uint32_t *oi,
-                               uint32_t *fail_list, uint32_t *fail_count,
-                               unsigned long long *stats, hipStream_t s);
+                               uint32_t *fail_list, uint32_t *fail_count, uint32_t pos_base,
+                               bool retry, unsigned long long *stats, hipStream_t s);
+
+// ball.hip: radius count (out_idx == nullptr) or CSR fill over m kd-ordered
+// queries (periodic queries outside [0, L]^3 are skipped: query.hip answers them)
+void launch_ball_packet(const Tree &t, const float *q, const uint32_t *order, uint32_t m, float r2,
+                        uint32_t *out_count, const uint64_t *row_offsets, uint32_t *out_idx,
+                        hipStream_t s);
+// the listed periodic queries outside [0, L]^3, every point tested (fill: nout
+// zeroed scratch words when out_idx is set)
+void launch_ball_outside(const Tree &t, const float *q, const uint32_t *list, uint32_t nout,
+                         float r2, uint32_t *out_count, uint32_t *fill,
+                         const uint64_t *row_offsets, uint32_t *out_idx, hipStream_t s);
 
 // query.hip
 nbkd_status query_knn(const Tree &t, const float *q, uint64_t m, int k, float *out_d,

@@ -337,8 +337,7 @@ knn_collect_kernel(DevTree t, const uint32_t *__restrict__ linfo, const float *_
     }
     if (valid) ccount[gq] = cnt;
     if (STATS && lane == 0) {
-        const uint32_t nvalid = (uint32_t)__popcll(__ballot(valid));
-        atomicAdd(&stats[0], (unsigned long long)n_nodes * nvalid);
+        atomicAdd(&stats[0], (unsigned long long)n_nodes); // node visits of the packet walk
         atomicAdd(&stats[1], (unsigned long long)n_evals);
         atomicAdd(&stats[2], (unsigned long long)n_dense);
         atomicAdd(&stats[3], (unsigned long long)n_sparse);
@@ -373,7 +372,7 @@ knn_select_kernel(DevTree t, const float *__restrict__ q, const uint32_t *__rest
                   uint32_t m, int k, uint32_t qpp, const uint2 *__restrict__ cand, uint32_t capg,
                   const uint32_t *__restrict__ ccount, float *__restrict__ out_d,
                   uint32_t *__restrict__ out_i, uint32_t *__restrict__ fail_list,
-                  uint32_t *__restrict__ fail_count) {
+                  uint32_t *__restrict__ fail_count, uint32_t pos_base) {
     constexpr int NS = 16;                  // candidates merged per pass
     constexpr int CC = KC < 32 ? KC : 32;   // top-k registers staged per output pass
     constexpr int SW = CC < 32 ? 32 * 64 : CC * 64; // >= 8 KB: one candidate block
@@ -389,8 +388,10 @@ knn_select_kernel(DevTree t, const float *__restrict__ q, const uint32_t *__rest
     const bool ok = valid && n >= (uint32_t)k && n <= capg;
     if (valid && !ok) {
         const float qx = q[3 * (size_t)qo], qy = q[3 * (size_t)qo + 1], qz = q[3 * (size_t)qo + 2];
-        // outside-box periodic queries are listed already (outside_box_kernel)
-        knn_fail_check<PER>(true, true, 0xFFFFFFFFu, qx, qy, qz, t.box, qo, fail_list, fail_count);
+        // outside-box periodic queries are listed already (outside_box_kernel);
+        // pos_base != ~0: list the sorted position (pos_base + gq), not the id
+        knn_fail_check<PER>(true, true, 0xFFFFFFFFu, qx, qy, qz, t.box,
+                            pos_base == 0xFFFFFFFFu ? qo : pos_base + gq, fail_list, fail_count);
     }
     const uint32_t nn = ok ? n : 0u;
     uint32_t maxn = nn;
@@ -527,11 +528,12 @@ template <int KC>
 void launch_select(const Tree &t, const float *q, const uint32_t *order, uint32_t m, int k,
                    uint32_t qpp, const uint2 *cand, uint32_t capg, const uint32_t *ccount,
                    float *od, uint32_t *oi, uint32_t *fail_list, uint32_t *fail_count,
-                   hipStream_t s) {
+                   uint32_t pos_base, hipStream_t s) {
     const unsigned blocks = (m + TB - 1) / TB;
 #define NBKD_SELECT(PER, WH)                                                                       \
     knn_select_kernel<KC, PER, WH><<<blocks, TB, 0, s>>>(view(t), q, order, m, k, qpp, cand, capg, \
-                                                        ccount, od, oi, fail_list, fail_count)
+                                                        ccount, od, oi, fail_list, fail_count,     \
+                                                        pos_base)
     if (t.periodic) {
         if (qpp == 64) NBKD_SELECT(true, true); else NBKD_SELECT(true, false);
     } else {
@@ -553,11 +555,11 @@ uint32_t collect_capacity(int k) {
 nbkd_status launch_knn_collect(const Tree &t, const float *q, const uint32_t *order, uint32_t m,
                                int k, const float *tg, float seed_mul, uint32_t qpp, uint2 *cand,
                                uint32_t capg, uint32_t *ccount, float *od, uint32_t *oi,
-                               uint32_t *fail_list, uint32_t *fail_count,
-                               unsigned long long *stats, hipStream_t s) {
+                               uint32_t *fail_list, uint32_t *fail_count, uint32_t pos_base,
+                               bool retry, unsigned long long *stats, hipStream_t s) {
     if (m == 0) return NBKD_OK;
     {
-        TimedScope ts(qpp == 64 ? "knn_collect" : "knn_retry", s);
+        TimedScope ts(retry ? "knn_retry" : "knn_collect", s);
         if (t.periodic)
             launch_collect<true>(t, q, order, m, k, tg, seed_mul, qpp, cand, capg, ccount, stats, s);
         else
@@ -565,16 +567,16 @@ nbkd_status launch_knn_collect(const Tree &t, const float *q, const uint32_t *or
         NBKD_HIP(hipGetLastError());
     }
     {
-        TimedScope ts(qpp == 64 ? "knn_select" : "knn_retry", s);
+        TimedScope ts(retry ? "knn_retry" : "knn_select", s);
         if (k <= 16)
             launch_select<16>(t, q, order, m, k, qpp, cand, capg, ccount, od, oi, fail_list,
-                              fail_count, s);
+                              fail_count, pos_base, s);
         else if (k <= 32)
             launch_select<32>(t, q, order, m, k, qpp, cand, capg, ccount, od, oi, fail_list,
-                              fail_count, s);
+                              fail_count, pos_base, s);
         else
             launch_select<64>(t, q, order, m, k, qpp, cand, capg, ccount, od, oi, fail_list,
-                              fail_count, s);
+                              fail_count, pos_base, s);
         NBKD_HIP(hipGetLastError());
     }
     return NBKD_OK;

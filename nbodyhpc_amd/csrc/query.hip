@@ -554,89 +554,6 @@ nbkd_status radix_sort(Workspace &ws, uint32_t *k0, uint32_t *v0, uint32_t *k1, 
     return NBKD_OK;
 }
 
-// radius count: same packet traversal, fixed threshold r2
-template <bool PER>
-__global__ void __launch_bounds__(TB)
-ball_count_kernel(DevTree t, const float *__restrict__ q, const uint32_t *__restrict__ order,
-                  uint32_t m, float r2, uint32_t *__restrict__ out_count,
-                  uint64_t *__restrict__ row_offsets, uint32_t *__restrict__ out_idx) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint32_t gq = (blockIdx.x * WPB + wave) * 64u + lane;
-    const bool valid = gq < m;
-    const uint32_t qo = valid ? order[gq] : 0u;
-    const float qx = valid ? q[3 * (size_t)qo] : 0.0f;
-    const float qy = valid ? q[3 * (size_t)qo + 1] : 0.0f;
-    const float qz = valid ? q[3 * (size_t)qo + 2] : 0.0f;
-    const float L = t.box;
-    const float thr = valid ? r2 : -INFINITY;
-    uint64_t wpos = (out_idx && valid) ? row_offsets[qo] : 0;
-    uint32_t cnt = 0;
-    WaveStack stk;
-    stk.node = 0;
-    stk.b0 = stk.b1 = stk.b2 = stk.b3 = stk.b4 = stk.b5 = 0.0f;
-    int sp = 0;
-    {
-        float box[6];
-#pragma unroll
-        for (int a = 0; a < 3; ++a) {
-            box[2 * a] = PER ? 0.0f : -FLT_MAX;
-            box[2 * a + 1] = PER ? L : FLT_MAX;
-        }
-        NBKD_PUSH(sp, 0u, box);
-    }
-    while (sp > 0) {
-        --sp;
-        const uint32_t node = __builtin_amdgcn_readlane(stk.node, sp);
-        float box[6] = {rdlane(stk.b0, sp), rdlane(stk.b1, sp), rdlane(stk.b2, sp),
-                        rdlane(stk.b3, sp), rdlane(stk.b4, sp), rdlane(stk.b5, sp)};
-        const float bdist = box_d2<PER>(qx, qy, qz, box, L);
-        if (!__any(bdist <= thr)) continue;
-        const nbkd_node nd = t.nodes[node];
-        const int dim = (int)uni((uint32_t)nd.dimension);
-        if (dim < 0) {
-            const uint32_t b = uni(nd.left), e = uni(nd.right);
-            for (uint32_t j = b; j < e; j += 8) {
-                float px[8], py[8], pz[8];
-#pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    px[u] = t.x[j + u];
-                    py[u] = t.y[j + u];
-                    pz[u] = t.z[j + u];
-                }
-#pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    const float d = point_d2<PER>(qx, qy, qz, px[u], py[u], pz[u], L);
-                    const bool in = d <= thr;
-                    if (out_idx && in) out_idx[wpos + cnt] = t.idx[j + u];
-                    cnt += in;
-                }
-            }
-            continue;
-        }
-        const float split = unif(nd.split);
-        const uint32_t lchild = uni(nd.left), rchild = uni(nd.right);
-        float lbox[6], rbox[6];
-#pragma unroll
-        for (int a = 0; a < 6; ++a) {
-            lbox[a] = box[a];
-            rbox[a] = box[a];
-        }
-        if (dim == 0) {
-            lbox[1] = split;
-            rbox[0] = split;
-        } else if (dim == 1) {
-            lbox[3] = split;
-            rbox[2] = split;
-        } else {
-            lbox[5] = split;
-            rbox[4] = split;
-        }
-        NBKD_PUSH(sp, rchild, rbox);
-        NBKD_PUSH(sp, lchild, lbox);
-    }
-    if (valid && out_count) out_count[qo] = cnt;
-}
-
 // ------------------------------------------------------------------ reference-exact traversal
 // One lane per query, replaying KDTreeQuery::compute (kdtree_impl.hpp:620-662)
 // step for step: near child first (left unless q[dim] > split), near visited iff
@@ -794,6 +711,14 @@ outside_box_kernel(const float *__restrict__ q, uint32_t m, float L, uint32_t *_
     const float x = q[3 * (size_t)i], y = q[3 * (size_t)i + 1], z = q[3 * (size_t)i + 2];
     const bool inside = x >= 0.0f && x <= L && y >= 0.0f && y <= L && z >= 0.0f && z <= L;
     if (!inside) list[atomicAdd(count, 1u)] = i;
+}
+
+// out[i] = ord[pos[i]]: sorted positions back to query ids
+__global__ void __launch_bounds__(TB)
+gather_kernel(const uint32_t *__restrict__ pos, uint32_t n, const uint32_t *__restrict__ ord,
+              uint32_t *__restrict__ out) {
+    const uint32_t i = blockIdx.x * TB + threadIdx.x;
+    if (i < n) out[i] = ord[pos[i]];
 }
 
 int key_bits(const Tree &t) {
@@ -967,8 +892,10 @@ nbkd_status query_knn(const Tree &t, const float *q, uint64_t m, int k, float *o
             uint2 *cand = (uint2 *)t.ws.get(WS_CAND, batch * capg * 8u, s);
             uint32_t *ccount = (uint32_t *)t.ws.get(WS_CCOUNT, batch * 4u, s);
             // seed failures (fewer than k points in the seed ball, or more than
-            // the column holds) are retried with a 4x seed (2x radius), one
-            // query per wave; what still fails joins the exact kernel's list
+            // the column holds) are retried with a 4x seed (2x radius): listed
+            // by sorted position, put back in kd order, and walked as packets
+            // of 64 (one query per wave when there are few); what still fails
+            // joins the exact kernel's list
             uint32_t *rlist = (uint32_t *)t.ws.get(WS_LIST2, (size_t)mm * 4 + 16, s);
             if (!cand || !ccount || !rlist) return NBKD_ENOMEM;
             uint32_t *rcount = rlist + mm;
@@ -978,7 +905,8 @@ nbkd_status query_knn(const Tree &t, const float *q, uint64_t m, int k, float *o
                 for (uint64_t b0 = 0; b0 < mm; b0 += batch) {
                     const uint32_t nb = (uint32_t)std::min<uint64_t>(batch, mm - b0);
                     rc = launch_knn_collect(t, dq, ord + b0, nb, k, tg, 1.0f, 64u, cand, capg,
-                                            ccount, dd, di, rlist, rcount, stats, s);
+                                            ccount, dd, di, rlist, rcount, (uint32_t)b0, false,
+                                            stats, s);
                     if (rc) return rc;
                 }
             }
@@ -987,16 +915,38 @@ nbkd_status query_knn(const Tree &t, const float *q, uint64_t m, int k, float *o
             NBKD_HIP(hipStreamSynchronize(s));
             if (stats) NBKD_HIP(hipMemcpyAsync(stats + 9, rcount, 4, hipMemcpyDeviceToDevice, s));
             if (nr > 0) {
+                // positions -> kd order -> query ids
+                uint32_t *rs = (uint32_t *)t.ws.get(WS_RSORT, (size_t)nr * 12, s);
+                if (!rs) return NBKD_ENOMEM;
+                int pbits = 1;
+                while (pbits < 32 && (1ull << pbits) < (uint64_t)mm) ++pbits;
+                const bool odd = nr > 1 && (((pbits + 7) / 8) & 1); // sorted keys in k1
+                uint32_t *rq = odd ? rs : rs + nr;
+                {
+                    TimedScope ts2("knn_retry_order", s);
+                    uint32_t *vdummy = nullptr;
+                    rc = radix_sort(t.ws, rlist, rs, rs + nr, rs + 2 * (size_t)nr, nr, pbits, s,
+                                    &vdummy);
+                    if (rc) return rc;
+                    gather_kernel<<<(nr + TB - 1) / TB, TB, 0, s>>>(odd ? rs + nr : rlist, nr, ord,
+                                                                   rq);
+                    NBKD_HIP(hipGetLastError());
+                }
+                // packets pay off only where failures are dense enough to be
+                // coherent (clustered inputs: ~4% of queries; uniform: ~0.005%,
+                // 3 ms as packets of 64 vs 0.2 ms one per wave)
+                const uint32_t rqpp = (uint64_t)nr * 256u >= (uint64_t)mm ? 64u : 1u;
                 const uint32_t capr = collect_capacity(k) * 8u;
-                const uint64_t rb = std::max<uint64_t>(
-                    1, std::min<uint64_t>(nr, budget / ((uint64_t)capr * 8u)));
+                uint64_t rb = budget / ((uint64_t)capr * 8u) / 64u * 64u;
+                rb = std::max<uint64_t>(std::min<uint64_t>(rb, ((uint64_t)nr + 63) / 64 * 64), 64);
                 uint2 *rcand = (uint2 *)t.ws.get(WS_CAND, rb * capr * 8u, s);
                 uint32_t *rcc = (uint32_t *)t.ws.get(WS_CCOUNT, rb * 4u, s);
                 if (!rcand || !rcc) return NBKD_ENOMEM;
                 for (uint64_t b0 = 0; b0 < nr; b0 += rb) {
                     const uint32_t nb = (uint32_t)std::min<uint64_t>(rb, nr - b0);
-                    rc = launch_knn_collect(t, dq, rlist + b0, nb, k, tg, 4.0f, 1u, rcand, capr,
-                                            rcc, dd, di, list, count, nullptr, s);
+                    rc = launch_knn_collect(t, dq, rq + b0, nb, k, tg, 4.0f, rqpp, rcand, capr,
+                                            rcc, dd, di, list, count, 0xFFFFFFFFu, true, nullptr,
+                                            s);
                     if (rc) return rc;
                 }
             }
@@ -1054,7 +1004,22 @@ static nbkd_status ball_common(const Tree &t, const float *q, uint64_t m, float 
     rc = sort_queries(t, dq, mm, ord, s);
     if (rc) return rc;
     const float r2 = r * r;
-    const unsigned blocks = (mm + TB - 1) / TB;
+    // periodic queries outside [0, L]^3: listed, every point tested for them
+    uint32_t *list = nullptr, nout = 0;
+    if (t.periodic) {
+        list = (uint32_t *)t.ws.get(WS_LIST, (size_t)mm * 8 + 16, s);
+        if (!list) return NBKD_ENOMEM;
+        NBKD_HIP(hipMemsetAsync(list + mm, 0, 4, s));
+        outside_box_kernel<<<(mm + TB - 1) / TB, TB, 0, s>>>(dq, mm, t.box, list, list + mm);
+        NBKD_HIP(hipMemcpyAsync(&nout, list + mm, 4, hipMemcpyDeviceToHost, s));
+        NBKD_HIP(hipStreamSynchronize(s));
+    }
+    auto run = [&](uint32_t *c, const uint64_t *off, uint32_t *idx) -> nbkd_status {
+        launch_ball_packet(t, dq, ord, mm, r2, c, off, idx, s);
+        launch_ball_outside(t, dq, list, nout, r2, c, list + mm + 4, off, idx, s);
+        NBKD_HIP(hipGetLastError());
+        return NBKD_OK;
+    };
     uint32_t *cnt = out_count;
     const bool dev_out = flags & NBKD_OUTPUT_DEVICE;
     if (!cnt || !dev_out) {
@@ -1063,13 +1028,8 @@ static nbkd_status ball_common(const Tree &t, const float *q, uint64_t m, float 
     }
     {
         TimedScope ts("ball_count", s);
-        if (t.periodic)
-            ball_count_kernel<true><<<blocks, TB, 0, s>>>(view(t), dq, ord, mm, r2, cnt, nullptr,
-                                                          nullptr);
-        else
-            ball_count_kernel<false><<<blocks, TB, 0, s>>>(view(t), dq, ord, mm, r2, cnt, nullptr,
-                                                           nullptr);
-        NBKD_HIP(hipGetLastError());
+        rc = run(cnt, nullptr, nullptr);
+        if (rc) return rc;
     }
     if (!offsets) { // count-only
         if (!dev_out) {
@@ -1100,13 +1060,8 @@ static nbkd_status ball_common(const Tree &t, const float *q, uint64_t m, float 
     }
     {
         TimedScope ts("ball_fill", s);
-        if (t.periodic)
-            ball_count_kernel<true><<<blocks, TB, 0, s>>>(view(t), dq, ord, mm, r2, nullptr, doff,
-                                                          di);
-        else
-            ball_count_kernel<false><<<blocks, TB, 0, s>>>(view(t), dq, ord, mm, r2, nullptr, doff,
-                                                           di);
-        NBKD_HIP(hipGetLastError());
+        rc = run(nullptr, doff, di);
+        if (rc) return rc;
     }
     if (!dev_out) {
         NBKD_HIP(hipMemcpyAsync(out_idx, di, offsets[m] * 4, hipMemcpyDeviceToHost, s));

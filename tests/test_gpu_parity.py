@@ -241,3 +241,44 @@ def test_knn_seed_retry_and_no_seed(gpu, oracle, monkeypatch, seed_param, box):
         d, i = t.query(q, k)
         dr, ir = o.query(q, k)
         assert_knn_equal(d, i, dr, ir, pts, q, box)
+
+
+@pytest.mark.parametrize("box", [None, 1.0])
+def test_knn_lognormal_vs_oracle(gpu, oracle, box):
+    """Clustered inputs (SURVEY §8(d) config C5 recipe, small grid): dense knots
+    and near-empty voids stress the density-based seed (retry and exact paths)."""
+    from nbodyhpc_amd import synth
+    pts = synth.lognormal(300_000, grid=64)
+    rng = np.random.Generator(np.random.PCG64(33))
+    q = np.concatenate([pts[:3000], rng.uniform(0, 1.0, (2000, 3)).astype(np.float32)])
+    t = gpu.Tree(pts, leafsize=32, boxsize=box)
+    o = oracle.tree(pts, 32, box)
+    for k in (8, 32):
+        d, i = t.query(q, k)
+        dr, ir = o.query(q, k)
+        assert_knn_equal(d, i, dr, ir, pts, q, box)
+
+
+@pytest.mark.parametrize("box", [None, 1.0])
+def test_ball_whole_leaf_shortcut_and_padding(gpu, oracle, box):
+    """A radius several leaves wide: most leaves lie wholly inside the balls and
+    are counted without evaluating their points; n % 8 != 0 puts padding
+    points in the last leaf, which must never be counted.  Periodic queries
+    outside [0, L]^3 take the per-query kernel."""
+    pts = uniform(100_003, 8)
+    rng = np.random.Generator(np.random.PCG64(9))
+    q = np.concatenate([pts[:600], rng.uniform(0, 1.0, (300, 3)).astype(np.float32),
+                        np.array([[1.0, 1.0, 1.0], [0.0, 0.0, 0.0], [1.0, 0.5, 0.0]], np.float32)])
+    if box:
+        q = np.concatenate([q, rng.uniform(-0.3, 1.3, (100, 3)).astype(np.float32)])
+    r = 0.09
+    t = gpu.Tree(pts, leafsize=16, boxsize=box)
+    c = t.ball_count(q, r)
+    cb = oracle.ball_count_brute(pts, q, r, box)
+    assert np.array_equal(c, cb)
+    off, idx = t.ball_csr(q, r)
+    assert np.array_equal(np.diff(off.astype(np.int64)), cb.astype(np.int64))
+    for j in range(0, len(q), 53):
+        row = np.sort(idx[off[j]:off[j + 1]])
+        d2 = d2_ref(q[j], pts, box)
+        assert np.array_equal(row, np.nonzero(d2 <= np.float32(r) * np.float32(r))[0].astype(np.uint32))
