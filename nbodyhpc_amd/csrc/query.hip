@@ -745,7 +745,8 @@ SeedParams seed_params(const Tree &t, int k) {
     p.on = a > 0.0f;
     const float mu = (float)k + a * sqrtf((float)k) + a;
     p.mu_c = mu / (4.0f / 3.0f * 3.14159265f);
-    p.anchor = (uint32_t)t.leaf * 4u;
+    const char *ea = getenv("NBKD_KNN_ANCHOR"); // tuning only: anchor subtree in leaves
+    p.anchor = (uint32_t)t.leaf * (ea ? (uint32_t)std::max(1, atoi(ea)) : 4u);
     return p;
 }
 

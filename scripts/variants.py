@@ -14,9 +14,14 @@ ap.add_argument("--leafsize", type=int, default=32)
 ap.add_argument("--variants", default="0")
 ap.add_argument("--reps", type=int, default=2)
 ap.add_argument("--stats", action="store_true")
+ap.add_argument("--dist", default="uniform", choices=["uniform", "lognormal"])
 a = ap.parse_args()
 n, k = int(a.n), a.k
-pts = gen_uniform(n, 20261015, 1.0)
+if a.dist == "uniform":
+    pts = gen_uniform(n, 20261015, 1.0)
+else:
+    from nbodyhpc_amd import synth
+    pts = synth.lognormal(n)
 dp = hip.DeviceArray.from_numpy(pts)
 s = hip.Stream()
 tree = capi.Tree(n=n, dev_ptr=dp.ptr, leafsize=a.leafsize, boxsize=1.0, stream=s.handle)
@@ -32,7 +37,7 @@ for spec in a.variants.split(","):
     v = parts[0]
     os.environ["NBKD_KNN_VARIANT"] = v
     for i, var in ((1, "NBKD_KNN_SEED"), (2, "NBKD_KNN_COLLECT"), (3, "NBKD_DENSE_MIN"),
-                   (4, "NBKD_COLLECT_OCC")):
+                   (4, "NBKD_COLLECT_OCC"), (5, "NBKD_KNN_ANCHOR")):
         if len(parts) > i and parts[i] != "":
             os.environ[var] = parts[i]
         else:
@@ -50,10 +55,12 @@ for spec in a.variants.split(","):
     lk_ms, _ = capi.timing_read("leaf_key")
     rt_ms, _ = capi.timing_read("knn_retry")
     so_ms, _ = capi.timing_read("sort")
+    ro_ms, _ = capi.timing_read("knn_retry_order")
     capi.timing_enable(False)
     r = {"knn_ms": ms / cnt, "collect_ms": col_ms / cnt, "select_ms": sel_ms / cnt,
          "fallback_ms": fb_ms / cnt, "retry_ms": rt_ms / cnt, "leaf_key_ms": lk_ms / cnt,
-         "sort_ms": so_ms / cnt,
+         "sort_ms": so_ms / cnt, "retry_order_ms": ro_ms / cnt,
+         "total_ms": (ms + fb_ms + rt_ms + ro_ms + lk_ms + so_ms) / cnt,
          "qps_kernel": n / (ms / cnt * 1e-3)}
     head = od.numpy_head(200000)
     if ref is None:
@@ -70,5 +77,5 @@ for spec in a.variants.split(","):
         r["fallback_queries"] = st["fallback_queries"]
         r["retry_queries"] = st["retry_queries"]
     res[spec] = r
-    print(v, json.dumps(r), flush=True)
+    print(spec, json.dumps(r), flush=True)
 json.dump(res, open(os.path.join(ROOT, "gpurun_out", "variants.json"), "w"), indent=1)
