@@ -42,9 +42,9 @@ constexpr int NB = 16; // distance buckets of the bound histogram
 
 struct CollectLds {
     // sparse mode, indexed by slot (the rank of a needing lane): its query xyz +
-    // bound, its bucket scale (S/NB, NB/S) and its lane
+    // bound, its bucket factor (d2_bucket) and its lane
     float4 sq[64];
-    float2 ssc[64];
+    float scl[64];
     uint8_t owners[64];
     uint32_t cnt[64];          // per lane: candidates appended
     uint32_t hist[NB / 4][64]; // per lane: NB 8-bit counts of candidates by d2 bucket
@@ -54,14 +54,16 @@ struct CollectLds {
 
 // Bound tightening without a top-k: the seed ball [0, S) is cut into NB
 // buckets of width S/NB in d2; a candidate is counted in bucket j only if
-// d2 < (j+1)*S/NB as computed here in f32.  Once the buckets 0..j hold >= k
-// candidates, k points lie strictly inside (j+1)*S/NB, so the k-th distance
-// does too and it becomes the lane's new bound (candidates already appended
-// beyond it are harmless: select keeps the k smallest).
-__device__ __forceinline__ uint32_t d2_bucket(float d, float nb_over_s, float s_over_nb) {
-    uint32_t j = min((uint32_t)(d * nb_over_s), (uint32_t)(NB - 1));
-    if (!(d < (float)(j + 1) * s_over_nb) && j < (uint32_t)(NB - 1)) ++j;
-    return j;
+// d2 < fl((j+1) * fl(S/NB)).  Once the buckets 0..j hold >= k candidates, k
+// points lie strictly inside that edge, so the k-th distance does too and it
+// becomes the lane's new bound (candidates already appended beyond it are
+// harmless: select keeps the k smallest).  The bucket is floor(d2 * c) with
+// c = fl(fl(NB/S) * (1 + 2^-20)): the 2^-20 margin exceeds the few roundings
+// (2^-24 each) between d2 * c and the edge, so the property holds without a
+// check (a candidate near an edge may land one bucket high: a looser bound).
+// Non-finite or tiny seeds: c = 0 and edge scale +inf (no tightening).
+__device__ __forceinline__ uint32_t d2_bucket(float d, float c) {
+    return min((uint32_t)(d * c), (uint32_t)(NB - 1));
 }
 
 // Candidate columns, entries {d2 bits, tree position}: packet pk owns
@@ -172,11 +174,10 @@ knn_collect_kernel(DevTree t, const uint32_t *__restrict__ linfo, const float *_
     const float L = t.box;
     const float seed = valid ? fminf(tg[qo] * seed_mul, FLT_MAX) : -INFINITY;
     float kth = seed;
-    // bucket scale of the bound histogram (0 when the seed is not finite: no
-    // tightening, everything lands in the last bucket)
-    const bool fin = seed < FLT_MAX;
-    const float s_over_nb = fin ? seed * (1.0f / NB) : 0.0f;
-    const float nb_over_s = (fin && seed > 0.0f) ? (float)NB / seed : 0.0f;
+    // bound histogram scales (d2_bucket): bucket edge unit and bucket factor
+    const bool fin = seed < FLT_MAX && seed >= 1e-30f;
+    const float s_over_nb = fin ? seed * (1.0f / NB) : (seed > 0.0f ? INFINITY : 0.0f);
+    const float nb_over_s = fin ? (float)NB / seed * 1.00000095367431640625f : 0.0f;
 #pragma unroll
     for (int w = 0; w < NB / 4; ++w) W.hist[w][lane] = 0u;
     uint2 *const col = cand + (size_t)pk * qpp * capg; // qpp rows x capg slots, blocked by 16
@@ -267,7 +268,7 @@ knn_collect_kernel(DevTree t, const uint32_t *__restrict__ linfo, const float *_
                                 float d = dg[0];
     #pragma unroll
                                 for (int v = 1; v < G; ++v) d = u == (uint32_t)v ? dg[v] : d;
-                                const uint32_t j = d2_bucket(d, nb_over_s, s_over_nb);
+                                const uint32_t j = d2_bucket(d, nb_over_s);
                                 atomicAdd(&W.hist[j >> 2][lane], 1u << (8 * (j & 3)));
                                 if (cnt < capg)
                                     col[((cnt >> 4) * qpp + lane) * 16u + (cnt & 15u)] =
@@ -284,7 +285,7 @@ knn_collect_kernel(DevTree t, const uint32_t *__restrict__ linfo, const float *_
                         const uint32_t r = mbcnt64(need);
                         W.owners[r] = (uint8_t)lane;
                         W.sq[r] = make_float4(qx, qy, qz, kth);
-                        W.ssc[r] = make_float2(s_over_nb, nb_over_s);
+                        W.scl[r] = nb_over_s;
                     }
                     wave_sync();
                     uint32_t c2 = 1;
@@ -302,8 +303,7 @@ knn_collect_kernel(DevTree t, const uint32_t *__restrict__ linfo, const float *_
                                                                pb[1][pr], pb[2][pr], L);
                             if (d < qq.w) {
                                 const uint32_t owner = W.owners[slot];
-                                const float2 sc = W.ssc[slot];
-                                const uint32_t j = d2_bucket(d, sc.y, sc.x);
+                                const uint32_t j = d2_bucket(d, W.scl[slot]);
                                 atomicAdd(&W.hist[j >> 2][owner], 1u << (8 * (j & 3)));
                                 const uint32_t sl = atomicAdd(&W.cnt[owner], 1u);
                                 if (sl < capg)

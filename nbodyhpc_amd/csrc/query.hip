@@ -69,13 +69,27 @@ constexpr int SHAPE_MAX = 256;
 // bound instead of +inf and sends every query that finds fewer than k points
 // inside it to the reference-exact kernel, so a bad guess costs time, never
 // correctness.
+// Degenerate subtrees (points on a plane or a line: a zero extent) use the
+// density of their dimension: pi r^2 = mu A / count, 2 r = mu len / count.
 __device__ __forceinline__ float guess_r2(uint32_t count, const float lo[3], const float hi[3],
                                           float mu_c) {
-    const float v = (hi[0] - lo[0]) * (hi[1] - lo[1]) * (hi[2] - lo[2]);
-    if (!(v > 0.0f) || !(v < FLT_MAX) || count == 0) return FLT_MAX;
-    const float r3 = mu_c * v / (float)count;
-    const float r2 = cbrtf(r3 * r3);
-    return r2 < FLT_MAX ? r2 : FLT_MAX;
+    const float e0 = hi[0] - lo[0], e1 = hi[1] - lo[1], e2 = hi[2] - lo[2];
+    if (count == 0 || !(e0 >= 0.0f) || !(e1 >= 0.0f) || !(e2 >= 0.0f)) return FLT_MAX;
+    const int dd = (e0 > 0.0f) + (e1 > 0.0f) + (e2 > 0.0f);
+    float r2;
+    if (dd == 3) {
+        const float r3 = mu_c * ((e0 * e1) * e2) / (float)count;
+        r2 = cbrtf(r3 * r3);
+    } else if (dd == 2) { // mu_c * 4/3 = mu / pi
+        const float a = (e0 > 0.0f ? e0 : 1.0f) * (e1 > 0.0f ? e1 : 1.0f) * (e2 > 0.0f ? e2 : 1.0f);
+        r2 = mu_c * (4.0f / 3.0f) * a / (float)count;
+    } else if (dd == 1) { // mu_c * 2 pi / 3 = mu / 2
+        const float r = mu_c * (2.0f * 3.14159265f / 3.0f) * (e0 + e1 + e2) / (float)count;
+        r2 = r * r;
+    } else {
+        return FLT_MAX; // all points identical: no scale
+    }
+    return (r2 > 0.0f && r2 < FLT_MAX) ? r2 : FLT_MAX;
 }
 
 // Bucketing descent over the blocked heap of splits (internal.hpp hblk_*,

@@ -282,3 +282,20 @@ def test_ball_whole_leaf_shortcut_and_padding(gpu, oracle, box):
         row = np.sort(idx[off[j]:off[j + 1]])
         d2 = d2_ref(q[j], pts, box)
         assert np.array_equal(row, np.nonzero(d2 <= np.float32(r) * np.float32(r))[0].astype(np.uint32))
+
+
+@pytest.mark.parametrize("box", [None, 1.0])
+def test_knn_degenerate_planar_points(gpu, oracle, box):
+    """All points on one plane (zero-volume subtrees): the density seed is
+    undefined (+inf), so no seed bound and no histogram tightening may apply."""
+    rng = np.random.Generator(np.random.PCG64(41))
+    pts = rng.uniform(0, 1.0, (40_000, 3)).astype(np.float32)
+    pts[:, 2] = np.float32(0.5)
+    pts[:5000, 1] = np.float32(0.25)  # a line inside the plane too
+    q = np.concatenate([pts[:1500], rng.uniform(0, 1.0, (1500, 3)).astype(np.float32)])
+    t = gpu.Tree(pts, leafsize=32, boxsize=box)
+    o = oracle.tree(pts, 32, box)
+    for k in (8, 32):
+        d, i = t.query(q, k)
+        dr, ir = o.query(q, k)
+        assert_knn_equal(d, i, dr, ir, pts, q, box)
