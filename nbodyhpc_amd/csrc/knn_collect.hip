@@ -393,12 +393,17 @@ knn_collect_kernel(DevTree t, const uint32_t *__restrict__ linfo, const float *_
 // LDS by direct loads, no VGPR staging: LDS piece x = i*64 + lane takes the
 // block's row r = x/8, piece (x%8) ^ (r%8), so row r's piece j sits at
 // r*8 + (j ^ (r & 7)) and the per-row reads are bank-conflict free.
-__device__ __forceinline__ void issue_block(const uint4 *b4, uint4 *lds4, int lane) {
+__device__ __forceinline__ void issue_block(const uint4 *b4, uint4 *lds4, int lane, uint64_t rows) {
+    // rows: bit r set = row r holds candidates in this block; the other rows'
+    // 128-B lines are not read (their LDS slots keep stale data, masked by count)
     const uint32_t r0 = (uint32_t)lane >> 3, jj = (uint32_t)lane & 7u;
     const uint4 *src = b4 + r0 * 8 + (jj ^ r0);
+    // bits r0, r0+8, .., r0+56 of rows -> bits 0..7 of m
+    const uint32_t m = (uint32_t)((((rows >> r0) & 0x0101010101010101ull) * 0x0102040810204080ull) >> 56);
 #pragma unroll
     for (int i = 0; i < 8; ++i)
-        __builtin_amdgcn_global_load_lds((gas_ptr)(src + 64 * i), (las_ptr)(lds4 + 64 * i), 16, 0, 0);
+        if (m & (1u << i))
+            __builtin_amdgcn_global_load_lds((gas_ptr)(src + 64 * i), (las_ptr)(lds4 + 64 * i), 16, 0, 0);
 }
 
 // One lane per query: the k smallest of its candidate column, sorted, as rows.
@@ -408,7 +413,7 @@ knn_select_kernel(DevTree t, const float *__restrict__ q, const uint32_t *__rest
                   uint32_t m, int k, uint32_t qpp, const uint2 *__restrict__ cand, uint32_t capg,
                   const uint32_t *__restrict__ ccount, float *__restrict__ out_d,
                   uint32_t *__restrict__ out_i, uint32_t *__restrict__ fail_list,
-                  uint32_t *__restrict__ fail_count, uint32_t pos_base) {
+                  uint32_t *__restrict__ fail_count, uint32_t pos_base, uint64_t all_rows) {
     constexpr int NS = 16;                  // candidates merged per pass
     constexpr int CC = KC < 32 ? KC : 32;   // top-k registers staged per output pass
     constexpr int SW = CC < 32 ? 32 * 64 : CC * 64; // >= 8 KB: one candidate block
@@ -447,7 +452,8 @@ knn_select_kernel(DevTree t, const float *__restrict__ q, const uint32_t *__rest
     const uint4 *blk = reinterpret_cast<const uint4 *>(
         cand + (whole ? (size_t)(gq >> 6) * 64u * capg : (size_t)gq * capg));
     uint4 *const lds4 = reinterpret_cast<uint4 *>(stage);
-    if (whole && maxn > 0) issue_block(blk, lds4, lane);
+    // all_rows: read every row's line (A/B of the per-row masking)
+    if (whole && maxn > 0) issue_block(blk, lds4, lane, __ballot(nn > 0u) | all_rows);
     for (uint32_t s0 = 0; s0 < maxn; s0 += NS) {
         float bd[NS];
         uint32_t bi[NS];
@@ -480,7 +486,9 @@ knn_select_kernel(DevTree t, const float *__restrict__ q, const uint32_t *__rest
             // the reads have retired before the next block's DMA overwrites the buffer
             __builtin_amdgcn_s_waitcnt(0xC07F); // lgkmcnt(0)
             wave_sync();
-            if (s0 + NS < maxn) issue_block(blk + (size_t)((s0 + NS) >> 4) * 512u, lds4, lane);
+            if (s0 + NS < maxn)
+                issue_block(blk + (size_t)((s0 + NS) >> 4) * 512u, lds4, lane,
+                            __ballot(nn > s0 + NS) | all_rows);
         }
         // a block with nothing below any lane's current k-th changes nothing
         bool useful = false;
@@ -576,10 +584,14 @@ void launch_select(const Tree &t, const float *q, const uint32_t *order, uint32_
                    float *od, uint32_t *oi, uint32_t *fail_list, uint32_t *fail_count,
                    uint32_t pos_base, hipStream_t s) {
     const unsigned blocks = (m + TB - 1) / TB;
+    static const uint64_t all_rows = [] { // NBKD_SELECT_ROWMASK=0: read whole blocks
+        const char *e = getenv("NBKD_SELECT_ROWMASK");
+        return (e && atoi(e) == 0) ? ~0ull : 0ull;
+    }();
 #define NBKD_SELECT(PER, WH)                                                                       \
     knn_select_kernel<KC, PER, WH><<<blocks, TB, 0, s>>>(view(t), q, order, m, k, qpp, cand, capg, \
                                                         ccount, od, oi, fail_list, fail_count,     \
-                                                        pos_base)
+                                                        pos_base, all_rows)
     if (t.periodic) {
         if (qpp == 64) NBKD_SELECT(true, true); else NBKD_SELECT(true, false);
     } else {
