@@ -61,6 +61,9 @@ def parse():
     p.add_argument("--radius", type=float, default=0.01, help="C3 radius, units of L")
     p.add_argument("--csr-batch", type=int, default=1_000_000)
     p.add_argument("--lognormal-grid", type=int, default=512)
+    p.add_argument("--input", default=None,
+                   help="raw float32 (N, 3) particle file (reference main.cpp -f format) "
+                        "instead of the synthetic set; N > 1 streams each rank's slab")
     return p.parse_args()
 
 
@@ -226,6 +229,14 @@ def main():
         if dist is not None:
             dist.barrier()
 
+    def allsum(v):
+        if dist is None:
+            return v
+        import torch
+        t = torch.tensor([v], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        return float(t.item())
+
     def allmax(v):
         if dist is None:
             return v
@@ -241,15 +252,24 @@ def main():
     ds = None
     halo = None
     if world == 1:
-        points = gen_uniform(n, args.seed, L)
+        if args.input:
+            from nbodyhpc_amd import io as nio
+            points = nio.read_positions(args.input, mmap=False)
+            n = points.shape[0]
+        else:
+            points = gen_uniform(n, args.seed, L)
         own = n
         dev_pts = hip.DeviceArray.from_numpy(points)
         n_local = n
     else:
         from nbodyhpc_amd import slab
         points = None
-        own_xyz, own_ids = slab.gen_slab_points(n, args.seed, L, rank, world)
-        own = n
+        if args.input:
+            from nbodyhpc_amd import io as nio
+            own_xyz, own_ids = nio.read_slab(args.input, rank, world, L)
+        else:
+            own_xyz, own_ids = slab.gen_slab_points(n, args.seed, L, rank, world)
+        own = own_xyz.shape[0]
         comm = None if same_dev else slab.init_comm(dist, rank, world, local_rank, log)
         ds = slab.DeviceSlab(own_xyz, own_ids, rank, world, L, local_rank, dist, comm, log)
         del own_xyz, own_ids
@@ -328,6 +348,7 @@ def main():
     sel_ms, _ = capi.timing_read("knn_select")
     capi.timing_enable(False)
     elapsed_max = allmax(elapsed)
+    own_total = int(allsum(float(own)))  # file inputs: slabs differ in size
 
     # work counters of our own traversal (one extra, untimed pass)
     capi.stats_enable(True)
@@ -345,7 +366,7 @@ def main():
 
     if rank != 0:
         return
-    total_q = own * world * args.steps
+    total_q = own_total * args.steps
     value = total_q / elapsed_max
     ms_per_step = elapsed_max / args.steps * 1e3
     bq = bytes_per_query(k)
@@ -389,12 +410,17 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic: numpy PCG64 uniform [0,L)^3, L=1, float32; self-queries",
+        "data": (f"file: {os.path.basename(args.input)} (raw float32 (N, 3)); self-queries"
+                 if args.input else
+                 "synthetic: numpy PCG64 uniform [0,L)^3, L=1, float32; self-queries"),
         "config": {
-            "workload": f"kNN k={k} self-query of every particle, {n:.0e} uniform periodic "
-                        f"particles per GPU (L={L}), leafsize {args.leafsize}",
+            "workload": (f"kNN k={k} self-query of every particle of {os.path.basename(args.input)}"
+                         f" ({own_total} particles, periodic L={L}), leafsize {args.leafsize}"
+                         if args.input else
+                         f"kNN k={k} self-query of every particle, {n:.0e} uniform periodic "
+                         f"particles per GPU (L={L}), leafsize {args.leafsize}"),
             "n_particles_per_gpu": own, "k": k, "leafsize": args.leafsize,
-            "queries_per_step": own * world,
+            "queries_per_step": own_total,
             "parallelism": "single" if world == 1 else f"x-slab x{world} + RCCL halo",
         },
         "halo": halo,

@@ -1,0 +1,48 @@
+"""Raw particle files (reference main.cpp:103-114 format) and slab streaming."""
+import numpy as np
+
+from nbodyhpc_amd import io, slab
+
+
+def test_roundtrip_and_trailing_bytes(tmp_path):
+    rng = np.random.Generator(np.random.PCG64(3))
+    a = rng.uniform(0, 1, (1001, 3)).astype(np.float32)
+    p = str(tmp_path / "p.bin")
+    io.write_positions(p, a)
+    with open(p, "ab") as f:
+        f.write(b"\x01\x02\x03\x04\x05")  # a partial row is ignored, as in the reference
+    assert io.count_rows(p) == 1001
+    assert np.array_equal(np.asarray(io.read_positions(p)), a)
+    assert np.array_equal(io.read_positions(p, mmap=False), a)
+
+
+def test_read_slab_partitions_rows(tmp_path):
+    rng = np.random.Generator(np.random.PCG64(4))
+    a = rng.uniform(0, 2.0, (5000, 3)).astype(np.float32)
+    a[:7, 0] = np.float32(2.0)  # x == L belongs to the last slab
+    a[7:9, 0] = np.float32(0.0)
+    p = str(tmp_path / "p.bin")
+    io.write_positions(p, a)
+    seen = []
+    for world in (1, 3):
+        seen = []
+        for r in range(world):
+            xyz, ids = io.read_slab(p, r, world, 2.0, chunk_rows=333)
+            lo, hi = slab.slab_bounds(r, world, 2.0)
+            assert np.array_equal(xyz, a[ids])
+            assert np.all(xyz[:, 0] >= np.float32(lo))
+            if r < world - 1:
+                assert np.all(xyz[:, 0] < np.float32(hi))
+            assert np.all(np.diff(ids.astype(np.int64)) > 0)  # file order
+            seen.append(ids)
+        allids = np.sort(np.concatenate(seen))
+        assert np.array_equal(allids, np.arange(5000, dtype=np.uint32))
+    assert set(range(7)) <= set(seen[-1].tolist())
+
+
+def test_empty_file(tmp_path):
+    p = str(tmp_path / "e.bin")
+    open(p, "wb").close()
+    assert io.read_positions(p).shape == (0, 3)
+    xyz, ids = io.read_slab(p, 0, 2, 1.0)
+    assert xyz.shape == (0, 3) and ids.shape == (0,)
