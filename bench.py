@@ -136,6 +136,15 @@ def suite(args, capi, hip, tree, dev_pts, n, k, L, stream, od, oi):
     out["knn_independent_queries"] = {"queries_per_s": n / sec, "ms": sec * 1e3, "k": k,
                                       "queries": n, "query_seed": synth.SEED_QUERIES}
     log(f"suite: independent queries {n / sec:.3e} q/s")
+    # k-th neighbour distance only (densities / smoothing radii): same search,
+    # m floats out instead of the (m, k) rows
+    rk = hip.DeviceArray((n,), np.float32)
+    tree.query_kth_device(dev_pts.ptr, n, k, rk.ptr, stream.handle)
+    sec = timed(lambda: tree.query_kth_device(dev_pts.ptr, n, k, rk.ptr, stream.handle), steps, hip)
+    out["knn_kth_distance_only"] = {"queries_per_s": n / sec, "ms": sec * 1e3, "k": k,
+                                    "queries": n}
+    log(f"suite: k-th distance only {n / sec:.3e} q/s")
+    rk.free()
     # C3: radius count of every particle (self-queries), r = 0.01 L
     r = args.radius * L
     cnt = hip.DeviceArray((n,), np.uint32)

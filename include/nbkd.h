@@ -82,6 +82,17 @@ nbkd_status nbkd_query_knn(const nbkd_tree *tree, const float *q, uint64_t m, in
                            float *out_dist, uint32_t *out_idx, uint32_t flags, void *stream);
 
 /*
+ * Distance to the k-th nearest neighbour of each query (m floats): exactly
+ * column k-1 of nbkd_query_knn's out_dist, without writing the (m, k) rows.
+ * For local densities k / (4/3 pi r_k^3) and SPH-style smoothing lengths
+ * (the per-point radii the reference's rasterizer consumes:
+ * rasterization/src/python/nbodyhpc/rasterizer/__init__.py:104-143).
+ * Replaces: row[k-1] of PyKDTree::query (pybind.cpp:90-189).  NEW.
+ */
+nbkd_status nbkd_query_kth(const nbkd_tree *tree, const float *q, uint64_t m, int32_t k,
+                           float *out_dist, uint32_t flags, void *stream);
+
+/*
  * NEW (no reference counterpart): number of points with d2 <= r*r of each
  * query (periodic metric when the tree is periodic).  out_count is (m,) uint32.
  */

@@ -36,6 +36,7 @@ _PROTOS = {
     "nbkd_build": (_i32, [_c_p, _u64, _i32, _i32, ctypes.c_float, _i32, _u32, _c_p,
                           ctypes.POINTER(_c_p)]),
     "nbkd_query_knn": (_i32, [_c_p, _c_p, _u64, _i32, _c_p, _c_p, _u32, _c_p]),
+    "nbkd_query_kth": (_i32, [_c_p, _c_p, _u64, _i32, _c_p, _u32, _c_p]),
     "nbkd_query_ball_count": (_i32, [_c_p, _c_p, _u64, ctypes.c_float, _c_p, _u32, _c_p]),
     "nbkd_query_ball_csr": (_i32, [_c_p, _c_p, _u64, ctypes.c_float, _c_p, _c_p, _u64, _u32,
                                    _c_p]),
@@ -162,6 +163,18 @@ class Tree:
     def query_device(self, q_ptr, m, k, d_ptr, i_ptr, stream=None, input_device=True):
         flags = NBKD_OUTPUT_DEVICE | (NBKD_INPUT_DEVICE if input_device else 0)
         _check(lib().nbkd_query_knn(self.h, q_ptr, int(m), int(k), d_ptr, i_ptr, flags, stream))
+
+    def query_kth(self, q, k):
+        """Distance to the k-th neighbour (column k-1 of query()), float32 (m,)."""
+        q = _host_f32(q)
+        out = np.empty(q.shape[0], np.float32)
+        _check(lib().nbkd_query_kth(self.h, q.ctypes.data, q.shape[0], int(k), out.ctypes.data, 0,
+                                    None))
+        return out
+
+    def query_kth_device(self, q_ptr, m, k, d_ptr, stream=None, input_device=True):
+        flags = NBKD_OUTPUT_DEVICE | (NBKD_INPUT_DEVICE if input_device else 0)
+        _check(lib().nbkd_query_kth(self.h, q_ptr, int(m), int(k), d_ptr, flags, stream))
 
     def set_ids(self, ids=None, *, dev_ptr=None, stream=None):
         """Map the tree's point ids through `ids` (host array or device pointer)."""

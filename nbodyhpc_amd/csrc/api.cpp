@@ -195,6 +195,27 @@ nbkd_status nbkd_query_knn(const nbkd_tree *tree, const float *q, uint64_t m, in
     NBKD_GUARD_END
 }
 
+nbkd_status nbkd_query_kth(const nbkd_tree *tree, const float *q, uint64_t m, int32_t k,
+                           float *out_dist, uint32_t flags, void *stream) {
+    NBKD_GUARD_BEGIN
+    g_err.clear();
+    if (!tree) {
+        set_error("nbkd_query_kth: NULL tree");
+        return NBKD_EINVAL;
+    }
+    if (k <= 0) {
+        set_error("k must be positive integer");
+        return NBKD_EINVAL;
+    }
+    if (m > 0 && (!q || !out_dist)) {
+        set_error("nbkd_query_kth: NULL argument");
+        return NBKD_EINVAL;
+    }
+    DeviceGuard g(tree->t.device);
+    return query_kth(tree->t, q, m, k, out_dist, flags, (hipStream_t)stream);
+    NBKD_GUARD_END
+}
+
 nbkd_status nbkd_query_ball_count(const nbkd_tree *tree, const float *q, uint64_t m, float r,
                                   uint32_t *out_count, uint32_t flags, void *stream) {
     NBKD_GUARD_BEGIN

@@ -18,7 +18,7 @@ namespace nbkd {
 enum WsSlot {
     WS_Q = 0, WS_KEYS, WS_KEYS2, WS_ORDER, WS_TMP, WS_HIST, WS_SUMS, WS_OUTD, WS_OUTI,
     WS_COUNT, WS_OFF, WS_IDX, WS_STATS, WS_LIST, WS_LT, WS_TG, WS_CAND, WS_CCOUNT,
-    WS_LIST2, WS_RSORT, WS_NSLOTS
+    WS_LIST2, WS_RSORT, WS_KTHD, WS_KTHI, WS_NSLOTS
 };
 struct Workspace {
     std::mutex mu;
@@ -136,6 +136,7 @@ void launch_knn_packet(const Tree &t, const float *q, const uint32_t *order, uin
                        const float *tg, float *od, uint32_t *oi, uint32_t *fail_list,
                        uint32_t *fail_count, unsigned long long *stats, hipStream_t s);
 
+// (oi == nullptr: od receives only the k-th distance of each query, m floats)
 // knn_collect.hip: candidate column capacity for k, and one collect + select
 // pass over m queries (order[0..m) = query ids; tg = seed bounds, scaled by
 // seed_mul; qpp = queries per packet, 64 or 1; failures are listed as query
@@ -162,6 +163,9 @@ void launch_ball_outside(const Tree &t, const float *q, const uint32_t *list, ui
 // query.hip
 nbkd_status query_knn(const Tree &t, const float *q, uint64_t m, int k, float *out_d,
                       uint32_t *out_i, uint32_t flags, hipStream_t s);
+// distance to the k-th neighbour only (out_d: m floats)
+nbkd_status query_kth(const Tree &t, const float *q, uint64_t m, int k, float *out_d,
+                      uint32_t flags, hipStream_t s);
 nbkd_status query_ball_count(const Tree &t, const float *q, uint64_t m, float r,
                              uint32_t *out_count, uint32_t flags, hipStream_t s);
 nbkd_status query_ball_csr(const Tree &t, const float *q, uint64_t m, float r, uint64_t *offsets,

@@ -506,6 +506,10 @@ knn_select_kernel(DevTree t, const float *__restrict__ q, const uint32_t *__rest
         bitonic_merge<KC>(td, ti);
     }
 
+    if (out_i == nullptr) { // k-th distance only (nbkd_query_kth): column k-1
+        if (valid) out_d[qo] = sqrtf(td[KC - 1]);
+        return;
+    }
     rowq[lane] = valid ? qo : 0xFFFFFFFFu;
 #pragma unroll
     for (int j0 = 0; j0 < KC; j0 += CC) {

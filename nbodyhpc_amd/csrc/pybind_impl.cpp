@@ -98,6 +98,23 @@ class PyKDTree {
         return {dist, idx};
     }
 
+    // distance to the k-th neighbour only (nbkd_query_kth), float32 (m,)
+    py::array_t<float> query_kth(farray points, int k) {
+        if (k <= 0) throw std::runtime_error("k must be positive integer");
+        check_shape(points);
+        const py::ssize_t m = points.shape(0);
+        py::array_t<float> out(m);
+        const float *q = points.data();
+        float *o = out.mutable_data();
+        nbkd_status st;
+        {
+            py::gil_scoped_release nogil;
+            st = nbkd_query_kth(h_, q, (uint64_t)m, k, o, 0u, nullptr);
+        }
+        check(st);
+        return out;
+    }
+
     py::array_t<uint32_t> query_ball_count(farray points, float r) {
         check_shape(points);
         const py::ssize_t m = points.shape(0);
@@ -160,6 +177,7 @@ PYBIND11_MODULE(_impl, m) {
              py::arg("boxsize") = std::nullopt, py::arg("device") = -1)
         .def("query", &PyKDTree::query, py::arg("points"), py::arg("k") = 1,
              py::arg("workers") = 1)
+        .def("query_kth", &PyKDTree::query_kth, py::arg("points"), py::arg("k"))
         .def("query_ball_count", &PyKDTree::query_ball_count, py::arg("points"), py::arg("r"))
         .def("query_ball_csr", &PyKDTree::query_ball_csr, py::arg("points"), py::arg("r"))
         .def("export", &PyKDTree::export_tree)

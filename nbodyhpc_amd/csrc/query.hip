@@ -707,6 +707,10 @@ knn_exact_kernel(DevTree t, const float *__restrict__ q, const uint32_t *__restr
             }
             res[j] = v;
         }
+        if (!out_i) { // k-th distance only
+            out_d[qi] = sqrtf(res[k - 1].d);
+            continue;
+        }
         const size_t row = (size_t)qi * (size_t)k;
         for (int j = 0; j < k; ++j) {
             out_d[row + j] = sqrtf(res[j].d);
@@ -822,19 +826,23 @@ nbkd_status stage_queries(const Tree &t, const float *q, uint64_t m, uint32_t fl
 
 } // namespace
 
-nbkd_status query_knn(const Tree &t, const float *q, uint64_t m, int k, float *out_d,
-                      uint32_t *out_i, uint32_t flags, hipStream_t s) {
-    if (k <= 0) {
-        set_error("k must be positive integer");
-        return NBKD_EINVAL;
-    }
-    if (m == 0) return NBKD_OK;
-    if (m >= (1ull << 32)) {
-        set_error("more than 2^32 - 1 queries per call are not supported");
-        return NBKD_EINVAL;
-    }
+namespace {
+
+bool collect_disabled() {
+    static const bool off = [] {
+        const char *e = getenv("NBKD_KNN_COLLECT");
+        return e && atoi(e) == 0;
+    }();
+    return off;
+}
+
+// out_i == nullptr: k-th distance only (out_d: m floats); the caller
+// (query_kth) uses it only where the collect/select path runs
+nbkd_status knn_locked(const Tree &t, const float *q, uint64_t m, int k, float *out_d,
+                       uint32_t *out_i, uint32_t flags, hipStream_t s) {
     const uint32_t mm = (uint32_t)m;
-    std::lock_guard<std::mutex> lk(t.ws.mu);
+    const bool kth_only = out_i == nullptr;
+    const size_t row_words = kth_only ? 1 : (size_t)k;
     const float *dq = nullptr;
     nbkd_status rc = stage_queries(t, q, m, flags, dq, s);
     if (rc) return rc;
@@ -851,9 +859,9 @@ nbkd_status query_knn(const Tree &t, const float *q, uint64_t m, int k, float *o
     float *dd = out_d;
     uint32_t *di = out_i;
     if (!(flags & NBKD_OUTPUT_DEVICE)) {
-        dd = (float *)t.ws.get(WS_OUTD, m * (size_t)k * 4, s);
-        di = (uint32_t *)t.ws.get(WS_OUTI, m * (size_t)k * 4, s);
-        if (!dd || !di) return NBKD_ENOMEM;
+        dd = (float *)t.ws.get(WS_OUTD, m * row_words * 4, s);
+        di = kth_only ? nullptr : (uint32_t *)t.ws.get(WS_OUTI, m * (size_t)k * 4, s);
+        if (!dd || (!di && !kth_only)) return NBKD_ENOMEM;
     }
     unsigned long long *stats = nullptr;
     if (stats_enabled()) {
@@ -892,11 +900,7 @@ nbkd_status query_knn(const Tree &t, const float *q, uint64_t m, int k, float *o
                                                                  lt, dd, di);
         NBKD_HIP(hipGetLastError());
     } else {
-        static const bool collect_off = [] {
-            const char *e = getenv("NBKD_KNN_COLLECT");
-            return e && atoi(e) == 0;
-        }();
-        if (tg && !collect_off) {
+        if (tg && !collect_disabled()) {
             // collect + select in batches sized to the candidate-column budget
             const uint32_t capg = collect_capacity(k);
             const char *eb = getenv("NBKD_CAND_BYTES");
@@ -992,8 +996,66 @@ nbkd_status query_knn(const Tree &t, const float *q, uint64_t m, int k, float *o
         stats_store(h);
     }
     if (!(flags & NBKD_OUTPUT_DEVICE)) {
-        NBKD_HIP(hipMemcpyAsync(out_d, dd, m * (size_t)k * 4, hipMemcpyDeviceToHost, s));
-        NBKD_HIP(hipMemcpyAsync(out_i, di, m * (size_t)k * 4, hipMemcpyDeviceToHost, s));
+        NBKD_HIP(hipMemcpyAsync(out_d, dd, m * row_words * 4, hipMemcpyDeviceToHost, s));
+        if (!kth_only)
+            NBKD_HIP(hipMemcpyAsync(out_i, di, m * (size_t)k * 4, hipMemcpyDeviceToHost, s));
+        NBKD_HIP(hipStreamSynchronize(s));
+    }
+    return NBKD_OK;
+}
+
+nbkd_status knn_args(int k, uint64_t m) {
+    if (k <= 0) {
+        set_error("k must be positive integer");
+        return NBKD_EINVAL;
+    }
+    if (m >= (1ull << 32)) {
+        set_error("more than 2^32 - 1 queries per call are not supported");
+        return NBKD_EINVAL;
+    }
+    return NBKD_OK;
+}
+
+// out[i] = rows[i * k + k - 1]
+__global__ void __launch_bounds__(TB)
+kth_column_kernel(const float *__restrict__ rows, uint32_t m, int k, float *__restrict__ out) {
+    const uint32_t i = blockIdx.x * TB + threadIdx.x;
+    if (i < m) out[i] = rows[(size_t)i * k + (k - 1)];
+}
+
+} // namespace
+
+nbkd_status query_knn(const Tree &t, const float *q, uint64_t m, int k, float *out_d,
+                      uint32_t *out_i, uint32_t flags, hipStream_t s) {
+    nbkd_status rc = knn_args(k, m);
+    if (rc || m == 0) return rc;
+    std::lock_guard<std::mutex> lk(t.ws.mu);
+    return knn_locked(t, q, m, k, out_d, out_i, flags, s);
+}
+
+nbkd_status query_kth(const Tree &t, const float *q, uint64_t m, int k, float *out_d,
+                      uint32_t flags, hipStream_t s) {
+    nbkd_status rc = knn_args(k, m);
+    if (rc || m == 0) return rc;
+    std::lock_guard<std::mutex> lk(t.ws.mu);
+    // the collect/select path writes the k-th distance alone; elsewhere the
+    // rows go to scratch and column k-1 is copied out
+    if (k <= 64 && seed_params(t, k).on && !collect_disabled())
+        return knn_locked(t, q, m, k, out_d, nullptr, flags, s);
+    float *rd = (float *)t.ws.get(WS_KTHD, m * (size_t)k * 4, s);
+    uint32_t *ri = (uint32_t *)t.ws.get(WS_KTHI, m * (size_t)k * 4, s);
+    if (!rd || !ri) return NBKD_ENOMEM;
+    rc = knn_locked(t, q, m, k, rd, ri, flags | NBKD_OUTPUT_DEVICE, s);
+    if (rc) return rc;
+    float *dst = out_d;
+    if (!(flags & NBKD_OUTPUT_DEVICE)) {
+        dst = (float *)t.ws.get(WS_OUTD, m * 4, s);
+        if (!dst) return NBKD_ENOMEM;
+    }
+    kth_column_kernel<<<(unsigned)((m + TB - 1) / TB), TB, 0, s>>>(rd, (uint32_t)m, k, dst);
+    NBKD_HIP(hipGetLastError());
+    if (!(flags & NBKD_OUTPUT_DEVICE)) {
+        NBKD_HIP(hipMemcpyAsync(out_d, dst, m * 4, hipMemcpyDeviceToHost, s));
         NBKD_HIP(hipStreamSynchronize(s));
     }
     return NBKD_OK;

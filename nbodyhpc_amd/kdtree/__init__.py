@@ -96,6 +96,14 @@ class KDTree(cKDTree):
             rows[i] = np.sort(row) if return_sorted else row
         return rows.reshape(out_shape)
 
+    def kth_distance(self, points: np.ndarray, k: int):
+        """Distance to the k-th nearest neighbour of each point: column k-1 of
+        query(points, k)[0], without materialising the (M, k) rows.  Scaled,
+        these are the per-point smoothing radii the rasterizer takes."""
+        points, shape = _flatten(points)
+        out_shape = tuple(shape[:-1]) if shape is not None else (np.asarray(points).shape[0],)
+        return super().query_kth(points, int(k)).reshape(out_shape)
+
     def density(self, points: np.ndarray, k: Optional[int] = None, r: Optional[float] = None):
         """Local number density at each query point.
 
@@ -105,8 +113,7 @@ class KDTree(cKDTree):
         if (k is None) == (r is None):
             raise ValueError("give exactly one of k or r")
         if k is not None:
-            d, _ = self.query(points, k=k)
-            rk = d[..., -1].astype(np.float64)
+            rk = self.kth_distance(points, k).astype(np.float64)
             return k / (4.0 / 3.0 * math.pi * rk ** 3)
         c = self.query_ball(points, r, return_length=True).astype(np.float64)
         return c / (4.0 / 3.0 * math.pi * float(r) ** 3)

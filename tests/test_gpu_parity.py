@@ -201,6 +201,11 @@ def test_python_surface(gpu):
     assert [len(r) for r in rows] == counts.tolist()
     dens = t.density(pts[:100], k=8)
     assert np.all(np.isfinite(dens)) and np.all(dens > 0)
+    rk = t.kth_distance(pts[:12].reshape(3, 4, 3), 8)
+    assert rk.shape == (3, 4)
+    assert np.array_equal(rk.reshape(-1), t.query(pts[:12], k=8)[0][:, 7])
+    with pytest.raises(RuntimeError, match="k must be positive integer"):
+        t.kth_distance(pts[:3], 0)
 
 
 def test_device_pointer_path(gpu):
@@ -299,3 +304,23 @@ def test_knn_degenerate_planar_points(gpu, oracle, box):
         d, i = t.query(q, k)
         dr, ir = o.query(q, k)
         assert_knn_equal(d, i, dr, ir, pts, q, box)
+
+
+@pytest.mark.parametrize("box", [None, 1.0])
+def test_kth_distance_equals_row_column(gpu, monkeypatch, box):
+    """nbkd_query_kth == column k-1 of nbkd_query_knn, bit for bit: the
+    collect/select k-th-only output, the exact-kernel fallback (out-of-box
+    periodic queries, forced seed failures) and the k > 64 row path."""
+    pts = uniform(60_000, 51, L=box or 1.0)
+    rng = np.random.Generator(np.random.PCG64(52))
+    q = np.concatenate([pts[:2000], rng.uniform(0, box or 1.0, (2000, 3)).astype(np.float32)])
+    if box:
+        q = np.concatenate([q, rng.uniform(-0.4, 1.4, (300, 3)).astype(np.float32)])
+    t = gpu.Tree(pts, leafsize=32, boxsize=box)
+    for k in (1, 8, 32, 64, 100):
+        d, _ = t.query(q, k)
+        assert np.array_equal(t.query_kth(q, k), d[:, k - 1]), k
+    monkeypatch.setenv("NBKD_KNN_SEED", "0.05")  # most queries retried / exact
+    for k in (16, 32):
+        d, _ = t.query(q, k)
+        assert np.array_equal(t.query_kth(q, k), d[:, k - 1]), k
