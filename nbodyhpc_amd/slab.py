@@ -35,6 +35,33 @@ def slab_bounds(rank: int, world: int, box: float):
     return float(lo), float(hi)
 
 
+def bounds_list(world: int, box: float):
+    """The W + 1 slab cuts of the equal-width decomposition."""
+    return [slab_bounds(r, world, box)[0] for r in range(world)] + [float(np.float32(box))]
+
+
+def check_halo(h: float, bounds) -> None:
+    """A halo strip comes from the adjacent slab only, so h may not exceed the
+    narrowest slab; with two ranks both strips of a rank go to the same
+    neighbour, so they may not overlap either (2h <= width), or its points
+    would arrive twice."""
+    w = np.diff(np.asarray(bounds, np.float64))
+    world = len(w)
+    if world < 2:
+        return
+    lim = float(w.min()) / (2.0 if world == 2 else 1.0)
+    if h > lim:
+        raise ValueError(f"halo width {h:.4g} exceeds the slab limit {lim:.4g} "
+                         f"({world} slabs, narrowest {float(w.min()):.4g})")
+
+
+def ball_halo(r: float, box: float) -> float:
+    """Halo width that holds every point within r (periodic min-image) of an
+    own particle: r plus a relative 1e-4 and a few box ulps, so that neither
+    the f32 strip cut nor the f32 d2 <= r2 test at the edge can drop one."""
+    return float(r) * (1.0 + 1e-4) + 4.0 * float(np.spacing(np.float32(box)))
+
+
 def halo_width(n_total: int, k: int, box: float, factor: float = 2.5) -> float:
     """factor x the mean k-th neighbour radius of a uniform density."""
     rho = n_total / box ** 3
@@ -103,13 +130,16 @@ def _host_sendrecv(dist, rank, world, send_r, send_l, n_fl, n_fr, dtype, cols):
     return rl.numpy(), rr.numpy()
 
 
-def exchange_host(own_xyz, own_ids, rank, world, box, h, dist):
+def exchange_host(own_xyz, own_ids, rank, world, box, h, dist, bounds=None):
     """Host-array halo exchange over gloo.  Returns (local_xyz, local_ids) with
     the own particles first, then the strip from the left neighbour, then the
-    strip from the right neighbour."""
+    strip from the right neighbour.  `bounds`: the W + 1 slab cuts (default:
+    equal widths)."""
     if world == 1:
         return own_xyz, own_ids
-    lo, hi = slab_bounds(rank, world, box)
+    bounds = bounds_list(world, box) if bounds is None else bounds
+    check_halo(h, bounds)
+    lo, hi = float(bounds[rank]), float(bounds[rank + 1])
     x = own_xyz[:, 0]
     mr = x >= np.float32(hi - h)
     ml = x < np.float32(lo + h)
@@ -125,11 +155,14 @@ def exchange_host(own_xyz, own_ids, rank, world, box, h, dist):
     return xyz, ids
 
 
-def violations_host(q_xyz, kth_dist, rank, world, box, h):
+def violations_host(q_xyz, kth_dist, rank, world, box, h, bounds=None):
     """numpy statement of nbkd_slab_violations (slab.hip violations_kernel)."""
     if world == 1:
         return 0
-    lo, hi = slab_bounds(rank, world, box)
+    if bounds is None:
+        lo, hi = slab_bounds(rank, world, box)
+    else:
+        lo, hi = float(bounds[rank]), float(bounds[rank + 1])
     x = q_xyz[:, 0].astype(np.float32)
     margin = np.minimum(x - np.float32(lo - h), np.float32(hi + h) - x)
     ok = kth_dist.astype(np.float32) < margin * np.float32(1.0 - 4e-7)
@@ -141,14 +174,15 @@ class DeviceSlab:
     """Own particles + halo on the GPU for one rank (device arrays via hip.py)."""
 
     def __init__(self, own_xyz, own_ids, rank, world, box, device, dist=None, comm=None,
-                 log=None):
+                 log=None, bounds=None):
         from . import hip
 
         self.rank, self.world, self.box, self.device = rank, world, box, device
         self.dist, self.comm = dist, comm
         self.log = log or (lambda *a: None)
         self.n_own = len(own_xyz)
-        self.lo, self.hi = slab_bounds(rank, world, box)
+        self.bounds = bounds_list(world, box) if bounds is None else [float(b) for b in bounds]
+        self.lo, self.hi = self.bounds[rank], self.bounds[rank + 1]
         self.own_xyz = hip.DeviceArray.from_numpy(own_xyz)
         self.own_ids = hip.DeviceArray.from_numpy(own_ids)
         self.xyz = self.ids = None
@@ -160,6 +194,8 @@ class DeviceSlab:
         """(Re)build the local arrays with halo width h."""
         from . import capi, hip
 
+        if self.world > 1:
+            check_halo(float(h), self.bounds)
         self.h = float(h)
         if self.world == 1:
             self.xyz, self.ids, self.n_local = self.own_xyz, self.own_ids, self.n_own

@@ -89,7 +89,8 @@ def test_slab_knn_equals_single_tree(world, tmp_path, oracle):
     from tests.parity import assert_knn_equal
 
     n_per, k = 4000, 8
-    res = _run_world(world, n_per, k, 2.5, tmp_path)
+    # h = 1.5 x halo_width: inside the two-rank limit (2h <= slab width)
+    res = _run_world(world, n_per, k, 1.5, tmp_path)
     parts = [slab.gen_slab_points(n_per, 11, 1.0, r, world)[0] for r in range(world)]
     allp = np.concatenate(parts)
     gd, gi = oracle.tree(allp, 16, 1.0).query(allp, k, workers=4)
@@ -103,3 +104,79 @@ def test_slab_knn_equals_single_tree(world, tmp_path, oracle):
 def test_narrow_halo_is_flagged(tmp_path):
     res = _run_world(2, 4000, 8, 0.05, tmp_path)
     assert sum(int(r["v"]) for r in res) > 0
+
+
+def _c5_worker(rank, world, port, n, grid, r, k, outdir):
+    """Config C5 in miniature: log-normal slabs at count-quantile cuts, one
+    halo of width max(ball_halo(r), kNN halo) serving the radius count and the
+    k-th distance (widened until no row reaches past it)."""
+    import torch.distributed as dist
+
+    from nbodyhpc_amd import synth
+    from oracle.oracle import Oracle
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        h_r = slab.ball_halo(r, 1.0)
+        xyz, ids, bounds = synth.lognormal_slab(n, rank, world, grid=grid, min_width=4 * h_r)
+        h = max(h_r, slab.halo_width(n, k, 1.0))
+        orc = Oracle()
+        for _ in range(6):
+            lx, li = slab.exchange_host(xyz, ids, rank, world, 1.0, h, dist, bounds=bounds)
+            tree = orc.tree(lx, 16, 1.0)
+            d, i = tree.query(xyz, k, workers=1)
+            v = slab.violations_host(xyz, d[:, -1], rank, world, 1.0, h, bounds=bounds)
+            import torch
+            t = torch.tensor([v], dtype=torch.int64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            if int(t[0]) == 0:
+                break
+            try:
+                slab.check_halo(2 * h, bounds)
+            except ValueError:
+                break
+            h *= 2
+        cnt = orc.ball_count(tree, xyz, r)
+        np.savez(os.path.join(outdir, f"c5r{rank}.npz"), d=d, i=li[i], v=v, cnt=cnt, xyz=xyz,
+                 ids=ids, h=h, nloc=len(lx))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_lognormal_slab_radius_and_knn_equal_single_tree(world, tmp_path, oracle):
+    """Radius counts of every particle and its kNN rows, computed per slab over
+    own + halo, equal the single-tree (brute-force for counts) results over
+    the union of all slabs."""
+    import torch.multiprocessing as mp
+
+    from tests.parity import assert_knn_equal
+
+    n, grid, r, k = 12_000, 16, 0.04, 8
+    port = _free_port()
+    mp.start_processes(_c5_worker, args=(world, port, n, grid, r, k, str(tmp_path)),
+                       nprocs=world, join=True, start_method="spawn")
+    res = [np.load(os.path.join(tmp_path, f"c5r{q}.npz")) for q in range(world)]
+    allp = np.concatenate([x["xyz"] for x in res])
+    ids = np.concatenate([x["ids"] for x in res])
+    assert np.array_equal(ids, np.arange(n, dtype=np.uint32))
+    cnt = oracle.ball_count_brute(allp, allp, r, 1.0)
+    gd, gi = oracle.tree(allp, 16, 1.0).query(allp, k, workers=4)
+    o = 0
+    for x in res:
+        m = len(x["ids"])
+        assert x["nloc"] > m  # received a halo
+        assert np.array_equal(x["cnt"], cnt[o:o + m])
+        assert int(x["v"]) == 0
+        assert_knn_equal(x["d"], x["i"], gd[o:o + m], gi[o:o + m], allp, x["xyz"], 1.0)
+        o += m
+
+
+def test_halo_wider_than_a_slab_is_refused():
+    with pytest.raises(ValueError):
+        slab.check_halo(0.3, [0.0, 0.5, 1.0])  # two ranks: 2h > width
+    slab.check_halo(0.25, [0.0, 0.5, 1.0])
+    with pytest.raises(ValueError):
+        slab.check_halo(0.2, [0.0, 0.1, 0.6, 1.0])
