@@ -31,6 +31,7 @@ struct PadLeaves {
 struct alignas(16) BallLds {
     float pb[3][CHUNK];
     uint32_t pid[CHUNK];
+    float4 qs[64]; // the wave's query coordinates, for the transposed count
 };
 
 // upper bound of the f32 d2 of point_d2_fast over every point of the box: per
@@ -49,7 +50,7 @@ __global__ void __launch_bounds__(TB, 8)
 ball_packet_kernel(DevTree t, const uint32_t *__restrict__ linfo, const float *__restrict__ q,
                    const uint32_t *__restrict__ order, uint32_t m, float r2, PadLeaves pad,
                    uint32_t *__restrict__ out_count, const uint64_t *__restrict__ row_offsets,
-                   uint32_t *__restrict__ out_idx) {
+                   uint32_t *__restrict__ out_idx, uint32_t tnum) {
     __shared__ BallLds Wl[WPB];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     BallLds &W = Wl[wave];
@@ -66,6 +67,7 @@ ball_packet_kernel(DevTree t, const uint32_t *__restrict__ linfo, const float *_
     const float thr = active ? r2 : -INFINITY;
     uint64_t wpos = (FILL && active) ? row_offsets[qo] : 0;
     uint32_t cnt = 0;
+    if constexpr (!FILL) W.qs[lane] = make_float4(qx, qy, qz, 0.0f);
 
     uint32_t sk_node = 0;
     float sk_b[6] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
@@ -186,7 +188,40 @@ ball_packet_kernel(DevTree t, const uint32_t *__restrict__ linfo, const float *_
                     cnt += cn;
                 }
             }
-            if (part) {
+            // count mode, few partial lanes: transpose the loop.  Lanes hold
+            // the staged points (lane & 31), each step tests them against two
+            // partial queries at once (lower / upper half of the wave, query
+            // coordinates broadcast from LDS), and a ballot's
+            // popcount per half is that query's hit count.  One step is
+            // ~14 VALU per query against ~16 per point for the whole wave
+            // below, so it pays while #partial <= tnum/8 x #points.
+            bool trans = false;
+            if constexpr (!FILL) {
+                const uint64_t pm = __ballot(part);
+                trans = (uint32_t)__popcll(pm) * 8u <= cn * tnum;
+                if (trans) {
+                    const uint32_t u = (uint32_t)lane & 31u;
+                    const bool pv = u < cn;
+                    const float px = W.pb[0][u], py = W.pb[1][u], pz = W.pb[2][u];
+                    const bool upper = lane >= 32;
+                    uint64_t rem = pm;
+                    while (rem) {
+                        const int j0 = __builtin_ctzll(rem);
+                        rem &= rem - 1;
+                        const bool two = rem != 0;
+                        const int j1 = two ? __builtin_ctzll(rem) : j0;
+                        rem &= rem - 1;
+                        const float4 sq = W.qs[upper ? j1 : j0]; // LDS broadcast
+                        const float d = point_d2_fast<PER>(sq.x, sq.y, sq.z, px, py, pz, L);
+                        const uint64_t hits = __ballot(pv && d <= r2);
+                        const uint32_t c0 = (uint32_t)__popc((uint32_t)hits);
+                        const uint32_t c1 = two ? (uint32_t)__popc((uint32_t)(hits >> 32)) : 0u;
+                        cnt += lane == j0 ? c0 : 0u;
+                        cnt += lane == j1 ? c1 : 0u;
+                    }
+                }
+            }
+            if (part && !trans) {
                 // 4 staged points per step (float4 LDS reads); slots past cn hold
                 // stale data and are masked
 #pragma unroll 1
@@ -266,12 +301,18 @@ void launch_ball_packet(const Tree &t, const float *q, const uint32_t *order, ui
                         uint32_t *out_count, const uint64_t *row_offsets, uint32_t *out_idx,
                         hipStream_t s) {
     const unsigned blocks = (unsigned)((m + TB - 1) / TB);
+    // transposed count threshold (x/8 partial lanes per staged point); 0 = off
+    static const uint32_t tnum = [] {
+        const char *e = getenv("NBKD_BALL_T");
+        return e ? (uint32_t)atoi(e) : 6u;
+    }();
     PadLeaves pad;
     for (int j = 0; j < NBKD_PAD_LEAVES; ++j)
         pad.id[j] = t.npad_leaves <= NBKD_PAD_LEAVES ? t.pad_leaves[j] : 0xFFFFFFFFu;
 #define NBKD_BALL(PER, FILL)                                                                   \
     ball_packet_kernel<PER, FILL><<<blocks, TB, 0, s>>>(view(t), t.leafinfo, q, order, m, r2,  \
-                                                        pad, out_count, row_offsets, out_idx)
+                                                        pad, out_count, row_offsets, out_idx, \
+                                                        tnum)
     if (t.periodic) {
         if (out_idx) NBKD_BALL(true, true); else NBKD_BALL(true, false);
     } else {
