@@ -143,6 +143,9 @@ void launch_knn_packet(const Tree &t, const float *q, const uint32_t *order, uin
 // ids, or as sorted positions pos_base + i when pos_base != ~0u; retry names
 // the timers)
 uint32_t collect_capacity(int k);
+// seed-failure retry: adaptive per-query seeds written by the first select
+// pass (on by default) instead of a fixed 4x seed
+bool retry_adaptive();
 nbkd_status launch_knn_collect(const Tree &t, const float *q, const uint32_t *order, uint32_t m,
                                int k, const float *tg, float seed_mul, uint32_t qpp, uint2 *cand,
                                uint32_t capg, uint32_t *ccount, float *od, uint32_t *oi,

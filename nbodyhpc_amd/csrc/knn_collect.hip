@@ -413,7 +413,8 @@ knn_select_kernel(DevTree t, const float *__restrict__ q, const uint32_t *__rest
                   uint32_t m, int k, uint32_t qpp, const uint2 *__restrict__ cand, uint32_t capg,
                   const uint32_t *__restrict__ ccount, float *__restrict__ out_d,
                   uint32_t *__restrict__ out_i, uint32_t *__restrict__ fail_list,
-                  uint32_t *__restrict__ fail_count, uint32_t pos_base, uint64_t all_rows) {
+                  uint32_t *__restrict__ fail_count, uint32_t pos_base, uint64_t all_rows,
+                  float *__restrict__ tg_fix, float mu) {
     constexpr int NS = 16;                  // candidates merged per pass
     constexpr int CC = KC < 32 ? KC : 32;   // top-k registers staged per output pass
     constexpr int SW = CC < 32 ? 32 * 64 : CC * 64; // >= 8 KB: one candidate block
@@ -433,6 +434,19 @@ knn_select_kernel(DevTree t, const float *__restrict__ q, const uint32_t *__rest
         // pos_base != ~0: list the sorted position (pos_base + gq), not the id
         knn_fail_check<PER>(true, true, 0xFFFFFFFFu, qx, qy, qz, t.box,
                             pos_base == 0xFFFFFFFFu ? qo : pos_base + gq, fail_list, fail_count);
+        // the retry's seed (tg_fix: first pass only); n counted every point
+        // inside the seed ball, so it measured the local density.  n < k:
+        // grow the volume to hold ~1.5 mu at that density (2x..8x).  An
+        // overflowing column (n > capg): the retry's column is 8 capg, so keep
+        // the seed while n fits half of it, else shrink it to that.
+        if (tg_fix) {
+            float fv;
+            if (n < (uint32_t)k)
+                fv = fminf(8.0f, fmaxf(2.0f, 1.5f * mu / fmaxf((float)n, 0.5f)));
+            else
+                fv = fminf(1.0f, 4.0f * (float)capg / (float)n);
+            tg_fix[qo] = fminf(tg_fix[qo] * cbrtf(fv * fv), FLT_MAX);
+        }
     }
     const uint32_t nn = ok ? n : 0u;
     uint32_t maxn = nn;
@@ -586,7 +600,7 @@ template <int KC>
 void launch_select(const Tree &t, const float *q, const uint32_t *order, uint32_t m, int k,
                    uint32_t qpp, const uint2 *cand, uint32_t capg, const uint32_t *ccount,
                    float *od, uint32_t *oi, uint32_t *fail_list, uint32_t *fail_count,
-                   uint32_t pos_base, hipStream_t s) {
+                   uint32_t pos_base, float *tg_fix, float mu, hipStream_t s) {
     const unsigned blocks = (m + TB - 1) / TB;
     static const uint64_t all_rows = [] { // NBKD_SELECT_ROWMASK=0: read whole blocks
         const char *e = getenv("NBKD_SELECT_ROWMASK");
@@ -595,7 +609,7 @@ void launch_select(const Tree &t, const float *q, const uint32_t *order, uint32_
 #define NBKD_SELECT(PER, WH)                                                                       \
     knn_select_kernel<KC, PER, WH><<<blocks, TB, 0, s>>>(view(t), q, order, m, k, qpp, cand, capg, \
                                                         ccount, od, oi, fail_list, fail_count,     \
-                                                        pos_base, all_rows)
+                                                        pos_base, all_rows, tg_fix, mu)
     if (t.periodic) {
         if (qpp == 64) NBKD_SELECT(true, true); else NBKD_SELECT(true, false);
     } else {
@@ -605,6 +619,14 @@ void launch_select(const Tree &t, const float *q, const uint32_t *order, uint32_
 }
 
 } // namespace
+
+bool retry_adaptive() {
+    static const bool on = [] { // NBKD_RETRY_ADAPT=0: every retry seed is 4x (A/B)
+        const char *e = getenv("NBKD_RETRY_ADAPT");
+        return !(e && atoi(e) == 0);
+    }();
+    return on;
+}
 
 uint32_t collect_capacity(int k) {
     // seed balls hold mu = k + 4 sqrt(k) + 4 points on average; the column
@@ -630,15 +652,18 @@ nbkd_status launch_knn_collect(const Tree &t, const float *q, const uint32_t *or
     }
     {
         TimedScope ts(retry ? "knn_retry" : "knn_select", s);
+        // first pass with the adaptive retry: failures rewrite their seed
+        float *tg_fix = (!retry && retry_adaptive()) ? const_cast<float *>(tg) : nullptr;
+        const float mu = (float)k + 4.0f * sqrtf((float)k) + 4.0f;
         if (k <= 16)
             launch_select<16>(t, q, order, m, k, qpp, cand, capg, ccount, od, oi, fail_list,
-                              fail_count, pos_base, s);
+                              fail_count, pos_base, tg_fix, mu, s);
         else if (k <= 32)
             launch_select<32>(t, q, order, m, k, qpp, cand, capg, ccount, od, oi, fail_list,
-                              fail_count, pos_base, s);
+                              fail_count, pos_base, tg_fix, mu, s);
         else
             launch_select<64>(t, q, order, m, k, qpp, cand, capg, ccount, od, oi, fail_list,
-                              fail_count, pos_base, s);
+                              fail_count, pos_base, tg_fix, mu, s);
         NBKD_HIP(hipGetLastError());
     }
     return NBKD_OK;

@@ -963,7 +963,8 @@ nbkd_status knn_locked(const Tree &t, const float *q, uint64_t m, int k, float *
                 if (!rcand || !rcc) return NBKD_ENOMEM;
                 for (uint64_t b0 = 0; b0 < nr; b0 += rb) {
                     const uint32_t nb = (uint32_t)std::min<uint64_t>(rb, nr - b0);
-                    rc = launch_knn_collect(t, dq, rq + b0, nb, k, tg, 4.0f, rqpp, rcand, capr,
+                    rc = launch_knn_collect(t, dq, rq + b0, nb, k, tg,
+                                            retry_adaptive() ? 1.0f : 4.0f, rqpp, rcand, capr,
                                             rcc, dd, di, list, count, 0xFFFFFFFFu, true, nullptr,
                                             s);
                     if (rc) return rc;
