@@ -954,7 +954,13 @@ nbkd_status knn_locked(const Tree &t, const float *q, uint64_t m, int k, float *
                 // packets pay off only where failures are dense enough to be
                 // coherent (clustered inputs: ~4% of queries; uniform: ~0.005%,
                 // 3 ms as packets of 64 vs 0.2 ms one per wave)
-                const uint32_t rqpp = (uint64_t)nr * 256u >= (uint64_t)mm ? 64u : 1u;
+                static const int force_qpp = [] { // NBKD_RETRY_QPP=1|64: A/B only
+                    const char *e = getenv("NBKD_RETRY_QPP");
+                    return e ? atoi(e) : 0;
+                }();
+                const uint32_t rqpp = force_qpp == 1 || force_qpp == 64
+                                          ? (uint32_t)force_qpp
+                                          : ((uint64_t)nr * 256u >= (uint64_t)mm ? 64u : 1u);
                 const uint32_t capr = collect_capacity(k) * 8u;
                 uint64_t rb = budget / ((uint64_t)capr * 8u) / 64u * 64u;
                 rb = std::max<uint64_t>(std::min<uint64_t>(rb, ((uint64_t)nr + 63) / 64 * 64), 64);
