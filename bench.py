@@ -61,6 +61,10 @@ def parse():
     p.add_argument("--radius", type=float, default=0.01, help="C3 radius, units of L")
     p.add_argument("--csr-batch", type=int, default=1_000_000)
     p.add_argument("--lognormal-grid", type=int, default=512)
+    p.add_argument("--redistribute", action="store_true",
+                   help="with --input at N > 1: each rank reads a contiguous row chunk and the "
+                        "particles go to their slab owners by all-to-all-v (RCCL), instead of "
+                        "every rank scanning the file for its slab")
     p.add_argument("--workload", choices=("knn", "c5"), default="knn",
                    help="knn: the headline line (default).  c5: config C5 - log-normal "
                         "particles sharded at count-quantile x-slabs, radius count at "
@@ -430,16 +434,25 @@ def main():
     else:
         from nbodyhpc_amd import slab
         points = None
-        if args.input:
+        comm = None if same_dev else slab.init_comm(dist, rank, world, local_rank, log)
+        if args.input and args.redistribute:
+            # each rank reads its contiguous row chunk; all-to-all-v to the owners
+            from nbodyhpc_amd import io as nio
+            rows = nio.read_positions(args.input)
+            lo_r, hi_r = rank * rows.shape[0] // world, (rank + 1) * rows.shape[0] // world
+            own_xyz, own_ids = slab.redistribute(
+                np.array(rows[lo_r:hi_r]), np.arange(lo_r, hi_r, dtype=np.uint32), rank, world,
+                L, dist, comm=comm, device=local_rank, log=log)
+            del rows
+        elif args.input:
             from nbodyhpc_amd import io as nio
             own_xyz, own_ids = nio.read_slab(args.input, rank, world, L)
         else:
             own_xyz, own_ids = slab.gen_slab_points(n, args.seed, L, rank, world)
         own = own_xyz.shape[0]
-        comm = None if same_dev else slab.init_comm(dist, rank, world, local_rank, log)
         ds = slab.DeviceSlab(own_xyz, own_ids, rank, world, L, local_rank, dist, comm, log)
         del own_xyz, own_ids
-        h = slab.halo_width(n * world, k, L)
+        h = slab.halo_width(int(allsum(float(own))), k, L)  # file inputs: the real total
         barrier()
         t_x = time.perf_counter()
         ds.exchange(h, stream.handle)

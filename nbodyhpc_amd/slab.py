@@ -169,6 +169,111 @@ def violations_host(q_xyz, kth_dist, rank, world, box, h, bounds=None):
     return int((~ok).sum())
 
 
+# ------------------------------------------------------ redistribution to owners
+def slab_of(x, bounds):
+    """Owner rank of each x (float32 compares against the f32 cuts): rank r
+    owns [b_r, b_r+1); the last slab also owns x == L (periodic points lie in
+    [0, L])."""
+    inner = np.asarray(bounds[1:-1], np.float32)
+    return np.searchsorted(inner, np.asarray(x, np.float32), side="right").astype(np.int64)
+
+
+def _count_matrix(dist, world, send_counts):
+    import torch
+
+    mine = torch.as_tensor(np.asarray(send_counts, np.int64))
+    allc = [torch.zeros(world, dtype=torch.int64) for _ in range(world)]
+    dist.all_gather(allc, mine)
+    return np.stack([a.numpy() for a in allc])  # [src, dst]
+
+
+def redistribute(xyz, ids, rank, world, box, dist, comm=None, bounds=None, device=0, log=None):
+    """all-to-all-v of arbitrary per-rank particle
+    chunks (e.g. contiguous file rows) to their slab owners.
+
+    Each rank orders its particles by owner (host, stable), the W x W count
+    matrix goes over gloo, and the payload moves as one grouped RCCL
+    send/recv set with every peer (`nbkd_comm_exchange` on device buffers)
+    when `comm` is given, else as gloo point-to-point messages.  Returns
+    (own_xyz, own_ids) as host arrays, in (source rank, source order) order;
+    they feed DeviceSlab.  Exact: every particle lands on exactly one rank."""
+    xyz = np.ascontiguousarray(xyz, np.float32).reshape(-1, 3)
+    ids = np.ascontiguousarray(ids, np.uint32).reshape(-1)
+    if world == 1:
+        return xyz, ids
+    bounds = bounds_list(world, box) if bounds is None else bounds
+    dest = slab_of(xyz[:, 0], bounds)
+    order = np.argsort(dest, kind="stable")
+    sx, si = xyz[order], ids[order]
+    send = np.bincount(dest, minlength=world).astype(np.int64)
+    mat = _count_matrix(dist, world, send)
+    recv = mat[:, rank].astype(np.int64)
+    soff = np.concatenate([[0], np.cumsum(send)])
+    roff = np.concatenate([[0], np.cumsum(recv)])
+    n_own = int(roff[-1])
+    if comm is not None:
+        try:
+            return _redistribute_rccl(sx, si, rank, world, comm, soff, roff, n_own, device)
+        except Exception as e:  # reported; the gloo path below is exact too
+            (log or (lambda *a: None))(f"rank {rank}: RCCL redistribution failed ({e}); gloo")
+    import torch
+
+    out_x = np.empty((n_own, 3), np.float32)
+    out_i = np.empty(n_own, np.uint32)
+    out_x[roff[rank]:roff[rank + 1]] = sx[soff[rank]:soff[rank + 1]]
+    out_i[roff[rank]:roff[rank + 1]] = si[soff[rank]:soff[rank + 1]]
+    reqs, bufs = [], []
+    for j in range(world):
+        if j == rank:
+            continue
+        if send[j]:
+            for a, tag in ((sx[soff[j]:soff[j + 1]], 31),
+                           (si[soff[j]:soff[j + 1]].view(np.int32), 32)):
+                reqs.append(dist.isend(torch.from_numpy(np.ascontiguousarray(a)), j, tag=tag))
+        if recv[j]:
+            bx = torch.empty((int(recv[j]), 3), dtype=torch.float32)
+            bi = torch.empty(int(recv[j]), dtype=torch.int32)
+            reqs.append(dist.irecv(bx, j, tag=31))
+            reqs.append(dist.irecv(bi, j, tag=32))
+            bufs.append((j, bx, bi))
+    for r in reqs:
+        r.wait()
+    for j, bx, bi in bufs:
+        out_x[roff[j]:roff[j + 1]] = bx.numpy()
+        out_i[roff[j]:roff[j + 1]] = bi.numpy().view(np.uint32)
+    return out_x, out_i
+
+
+def _redistribute_rccl(sx, si, rank, world, comm, soff, roff, n_own, device):
+    from . import hip
+
+    dsx = hip.DeviceArray.from_numpy(sx if len(sx) else np.zeros((1, 3), np.float32))
+    dsi = hip.DeviceArray.from_numpy(si if len(si) else np.zeros(1, np.uint32))
+    drx = hip.DeviceArray((max(n_own, 1), 3), np.float32)
+    dri = hip.DeviceArray((max(n_own, 1),), np.uint32)
+    try:
+        pairs = []
+        for j in range(world):
+            if j == rank:
+                continue
+            ns, nr = int(soff[j + 1] - soff[j]), int(roff[j + 1] - roff[j])
+            # per peer: coordinates, then ids (matched in posting order)
+            pairs.append((dsx.ptr + int(soff[j]) * 12, ns * 12, j,
+                          drx.ptr + int(roff[j]) * 12, nr * 12, j))
+            pairs.append((dsi.ptr + int(soff[j]) * 4, ns * 4, j,
+                          dri.ptr + int(roff[j]) * 4, nr * 4, j))
+        n_self = int(soff[rank + 1] - soff[rank])
+        if n_self:
+            hip.memcpy(drx.ptr + int(roff[rank]) * 12, dsx.ptr + int(soff[rank]) * 12, n_self * 12)
+            hip.memcpy(dri.ptr + int(roff[rank]) * 4, dsi.ptr + int(soff[rank]) * 4, n_self * 4)
+        comm.exchange(pairs)
+        hip.synchronize()
+        return drx.numpy_head(n_own), dri.numpy_head(n_own)
+    finally:
+        for a in (dsx, dsi, drx, dri):
+            a.free()
+
+
 # ------------------------------------------------------------------ device path
 class DeviceSlab:
     """Own particles + halo on the GPU for one rank (device arrays via hip.py)."""

@@ -180,3 +180,51 @@ def test_halo_wider_than_a_slab_is_refused():
     slab.check_halo(0.25, [0.0, 0.5, 1.0])
     with pytest.raises(ValueError):
         slab.check_halo(0.2, [0.0, 0.1, 0.6, 1.0])
+
+
+def _redist_worker(rank, world, port, n, outdir, quantile):
+    import torch.distributed as dist
+
+    from nbodyhpc_amd import synth
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        pts = synth.uniform(n, 77, 1.0)
+        pts[:7, 0] = 1.0  # points exactly at L belong to the last slab
+        bounds = [0.0, 0.1, 0.75, 1.0] if quantile else None  # quantile: world 3
+        # arbitrary (file-row) chunks, not slabs
+        lo, hi = rank * n // world, (rank + 1) * n // world
+        ids = np.arange(lo, hi, dtype=np.uint32)
+        ox, oi = slab.redistribute(pts[lo:hi], ids, rank, world, 1.0, dist, bounds=bounds)
+        np.savez(os.path.join(outdir, f"rd{rank}.npz"), x=ox, i=oi)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,quantile", [(2, False), (3, False), (3, True)])
+def test_redistribute_to_slab_owners(world, quantile, tmp_path):
+    """All-to-all-v of contiguous row chunks: every particle arrives at the
+    owner of its x, exactly once, with its global id."""
+    import torch.multiprocessing as mp
+
+    from nbodyhpc_amd import synth
+
+    n = 20_000
+    port = _free_port()
+    mp.start_processes(_redist_worker, args=(world, port, n, str(tmp_path), quantile),
+                       nprocs=world, join=True, start_method="spawn")
+    pts = synth.uniform(n, 77, 1.0)
+    pts[:7, 0] = 1.0
+    bounds = slab.bounds_list(world, 1.0) if not quantile else [0.0, 0.1, 0.75, 1.0]
+    owner = slab.slab_of(pts[:, 0], bounds)
+    seen = np.zeros(n, np.int64)
+    for r in range(world):
+        res = np.load(os.path.join(tmp_path, f"rd{r}.npz"))
+        assert np.array_equal(res["x"], pts[res["i"]])
+        assert (owner[res["i"]] == r).all()
+        assert (res["x"][:, 0] >= np.float32(bounds[r])).all()
+        seen[res["i"]] += 1
+    assert (seen == 1).all()
+    assert (owner[:7] == world - 1).all()
