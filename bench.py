@@ -35,6 +35,9 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 # N = nodes visited, P = points scanned by the REFERENCE traversal at leafsize 32
 # (its KDTreeQueryStatistics), uniform periodic k=32 at 1e8 points: N=61.8, P=307.9.
 REF_NODES_1E8, REF_POINTS_1E8 = 61.8, 307.9
+# Radius count (C3: 1e8 uniform periodic, r = 0.01 L, leafsize 32): B_r = 16*N + 12*P + 16
+# with N, P of the one-query DFS (scripts/ref_ball_counters.py --n 1e8: N=175.19, P=1302.53)
+REF_BALL_NODES_1E8, REF_BALL_POINTS_1E8 = 175.19, 1302.53
 
 
 def bytes_per_query(k, nodes=REF_NODES_1E8, points=REF_POINTS_1E8):
@@ -169,6 +172,15 @@ def suite(args, capi, hip, tree, dev_pts, n, k, L, stream, od, oi):
     out["radius_count"] = {"queries_per_s": n / sec, "ms": sec * 1e3,
                            "kernel_ms": kern_ms / steps, "r": r, "mean_count": float(c.mean()),
                            "expected_mean_count": expect, "queries": n}
+    if n == 100_000_000 and abs(args.radius - 0.01) < 1e-12 and args.leafsize == 32:
+        # algorithmic bytes per query / kernel time; frac > 1 means the leaves are
+        # re-read from cache (the kernel is VALU-bound: profiles/r01k_ball_pmc.txt)
+        br = 16.0 * REF_BALL_NODES_1E8 + 12.0 * REF_BALL_POINTS_1E8 + 16.0
+        ach = br * n / (kern_ms / steps * 1e-3) / 1e9
+        out["radius_count"]["roofline"] = {
+            "bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": ach / HBM_PEAK_GBS, "bytes_per_query": br,
+            "kernel": "ball_packet_kernel<periodic, count> (nbodyhpc_amd/csrc/ball.hip)"}
     log(f"suite: radius count {n / sec:.3e} q/s, mean {c.mean():.1f} (expect {expect:.1f})")
     # C3: CSR batch (host in / host out: PCIe-inclusive)
     b = min(args.csr_batch, n)

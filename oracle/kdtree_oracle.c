@@ -583,10 +583,14 @@ ORC_EXPORT int orc_ball_count_brute(const float *aos, int64_t n, int32_t periodi
 
 /* NEW (no reference): radius count through the tree.  Same DFS, pruning by
  * box distance > r*r. Used as the CPU baseline of the ball path. */
+static uint64_t g_ball_nodes, g_ball_points; /* orc_ball_count_stats (single thread) */
+
 static uint32_t ball_rec(const orc_tree *t, const orc_node *node, const float q[3], float bounds[6],
                          float r2) {
+    ++g_ball_nodes;
     if (node->dim == -1) {
         uint32_t c = 0;
+        g_ball_points += node->right - node->left;
         for (uint32_t i = node->left; i < node->right; ++i) {
             float d = t->periodic ? d2_per(q[0], q[1], q[2], t->x[i], t->y[i], t->z[i], t->box)
                                   : d2_l2(q[0], q[1], q[2], t->x[i], t->y[i], t->z[i]);
@@ -619,4 +623,17 @@ ORC_EXPORT int orc_ball_count(const orc_tree *t, const float *q, int64_t m, floa
         out_count[j] = t->nnodes ? ball_rec(t, t->nodes, q + 3 * j, bounds, r2) : 0;
     }
     return ORC_OK;
+}
+
+/* The counters SURVEY.md §8(d) prices the radius query with (B_r = 16 N + 12 P
+ * + 16): nodes visited and points scanned by the one-query-at-a-time DFS
+ * above, summed over the m queries.  Not thread-safe (file-static counters). */
+ORC_EXPORT int orc_ball_count_stats(const orc_tree *t, const float *q, int64_t m, float r,
+                                    uint32_t *out_count, uint64_t *nodes, uint64_t *points) {
+    g_ball_nodes = 0;
+    g_ball_points = 0;
+    int rc = orc_ball_count(t, q, m, r, out_count);
+    *nodes = g_ball_nodes;
+    *points = g_ball_points;
+    return rc;
 }

@@ -153,6 +153,9 @@ class Oracle(_Lib):
         L.orc_ball_count_brute.argtypes = [_fp, ctypes.c_int64, ctypes.c_int32, ctypes.c_float,
                                            _fp, ctypes.c_int64, ctypes.c_float, _up]
         L.orc_ball_count.argtypes = [ctypes.c_void_p, _fp, ctypes.c_int64, ctypes.c_float, _up]
+        L.orc_ball_count_stats.argtypes = [ctypes.c_void_p, _fp, ctypes.c_int64, ctypes.c_float,
+                                           _up, ctypes.POINTER(ctypes.c_uint64),
+                                           ctypes.POINTER(ctypes.c_uint64)]
         L.orc_point_d2.argtypes = [_fp, _fp, ctypes.c_int32, ctypes.c_float]
         L.orc_point_d2.restype = ctypes.c_float
         L.orc_box_d2.argtypes = [_fp, _fp, ctypes.c_int32, ctypes.c_float]
@@ -186,6 +189,15 @@ class Oracle(_Lib):
         out = np.empty(q.shape[0], np.uint32)
         self.lib.orc_ball_count(tree._h, _ptr(q, _fp), q.shape[0], float(r), _ptr(out, _up))
         return out
+
+    def ball_count_stats(self, tree: Tree, q, r):
+        """(counts, nodes visited, points scanned) of the one-query DFS."""
+        q = _f32(q)
+        out = np.empty(q.shape[0], np.uint32)
+        nn, npt = ctypes.c_uint64(), ctypes.c_uint64()
+        self.lib.orc_ball_count_stats(tree._h, _ptr(q, _fp), q.shape[0], float(r),
+                                      _ptr(out, _up), ctypes.byref(nn), ctypes.byref(npt))
+        return out, int(nn.value), int(npt.value)
 
     def point_d2(self, q, p, boxsize=None):
         q = _f32(q)

@@ -159,3 +159,17 @@ def test_tree_shape_function():
     g = np.load(os.path.join(os.path.dirname(__file__), "golden", "g5_nodes.npz"))
     for key, (pts, leaf, box) in g5_inputs().items():
         assert nodes(int(g["n8_" + key]), max(leaf, 16)) == g["nodes_" + key].shape[0]
+
+
+def test_ball_count_stats_counters(oracle):
+    """orc_ball_count_stats: same counts as orc_ball_count; the counters that
+    price the radius query (bench.py REF_BALL_*) are the DFS's visits: at
+    least the leaves whose points were scanned, and every point counted was scanned."""
+    pts = uniform(20_000, 5)
+    q = uniform(300, 6)
+    t = oracle.tree(pts, 32, 1.0)
+    c0 = oracle.ball_count(t, q, 0.05)
+    c, nodes, points = oracle.ball_count_stats(t, q, 0.05)
+    assert np.array_equal(c, c0)
+    assert points >= int(c.sum()) and points % 8 == 0
+    assert nodes >= points // 32
