@@ -92,8 +92,6 @@ __device__ __forceinline__ float guess_r2(uint32_t count, const float lo[3], con
     return (r2 > 0.0f && r2 < FLT_MAX) ? r2 : FLT_MAX;
 }
 
-constexpr uint32_t KEY_LDS_LINES = 273; // 1 + 16 + 256 lines: 17.5 KB
-
 // Bucketing descent over the blocked heap of splits (internal.hpp hblk_*,
 // build.hip heap_splits_kernel): same turns, same leaf key and seed as
 // leaf_key2_kernel, one 64-B line (4 levels) per load instead of one dependent
@@ -102,12 +100,7 @@ __global__ void __launch_bounds__(TB)
 leaf_key3_kernel(const float4 *__restrict__ hb, int o, uint32_t n8, uint32_t leaf,
                  const float *__restrict__ q, uint32_t m, uint32_t *__restrict__ keys,
                  uint32_t *__restrict__ vals, float *__restrict__ tg, float mu_c, uint32_t anchor,
-                 float3 box_lo, float3 box_hi, uint32_t nl) {
-    // the first nl lines (the top three line levels, <= KEY_LDS_LINES) are read
-    // from LDS: half of a 1e8 descent's six dependent line loads
-    __shared__ float4 top[KEY_LDS_LINES * 4];
-    for (uint32_t j = threadIdx.x; j < nl * 4; j += TB) top[j] = hb[j];
-    __syncthreads();
+                 float3 box_lo, float3 box_hi) {
     for (uint32_t i = blockIdx.x * TB + threadIdx.x; i < m; i += gridDim.x * TB) {
         const float p[3] = {q[3 * (size_t)i], q[3 * (size_t)i + 1], q[3 * (size_t)i + 2]};
         uint32_t left = 0, count = n8;
@@ -119,18 +112,8 @@ leaf_key3_kernel(const float4 *__restrict__ hb, int o, uint32_t n8, uint32_t lea
         uint32_t b = 0, base = 0, nb = 1;
         int l0 = o;
         while (count > leaf) {
-            float4 a0, a1, a2, a3;
-            if (b < nl) {
-                a0 = top[4 * b];
-                a1 = top[4 * b + 1];
-                a2 = top[4 * b + 2];
-                a3 = top[4 * b + 3];
-            } else {
-                a0 = hb[4 * (size_t)b];
-                a1 = hb[4 * (size_t)b + 1];
-                a2 = hb[4 * (size_t)b + 2];
-                a3 = hb[4 * (size_t)b + 3];
-            }
+            const float4 a0 = hb[4 * (size_t)b], a1 = hb[4 * (size_t)b + 1];
+            const float4 a2 = hb[4 * (size_t)b + 2], a3 = hb[4 * (size_t)b + 3];
             uint32_t pos = 0; // position within the line's current level
 #pragma unroll
             for (int l = 0; l < 4; ++l) {
@@ -802,18 +785,10 @@ nbkd_status sort_queries(const Tree &t, const float *dq, uint32_t m, uint32_t *&
                                          : make_float3(t.bbox_lo[0], t.bbox_lo[1], t.bbox_lo[2]);
             const float3 hi = t.periodic ? make_float3(t.box, t.box, t.box)
                                          : make_float3(t.bbox_hi[0], t.bbox_hi[1], t.bbox_hi[2]);
-            static const bool key_lds = [] { // NBKD_KEY_LDS=0: no LDS top levels (A/B)
-                const char *e = getenv("NBKD_KEY_LDS");
-                return !(e && atoi(e) == 0);
-            }();
-            const int o = hblk_offset(t.depth);
-            uint64_t nl = 0;
-            for (int j = 0; j < 3; ++j) nl += hblk_level_lines(j, o);
-            nl = std::min<uint64_t>({nl, hblk_blocks(t.depth), (uint64_t)KEY_LDS_LINES});
-            leaf_key3_kernel<<<blocks, TB, 0, s>>>((const float4 *)t.hsplit, o, (uint32_t)t.n8,
-                                                   (uint32_t)t.leaf, dq, m, keys, order, tg,
-                                                   sp ? sp->mu_c : 0.0f, sp ? sp->anchor : 0u,
-                                                   lo, hi, key_lds ? (uint32_t)nl : 0u);
+            leaf_key3_kernel<<<blocks, TB, 0, s>>>((const float4 *)t.hsplit, hblk_offset(t.depth),
+                                                   (uint32_t)t.n8, (uint32_t)t.leaf, dq, m,
+                                                   keys, order, tg, sp ? sp->mu_c : 0.0f,
+                                                   sp ? sp->anchor : 0u, lo, hi);
         } else if (t.shape_len <= SHAPE_MAX) {
             const unsigned blocks = (unsigned)std::min<uint64_t>((m + TB - 1) / TB, 8192);
             // periodic: the box; otherwise the real points' bounding box (the
