@@ -150,7 +150,8 @@ nbkd_status launch_knn_collect(const Tree &t, const float *q, const uint32_t *or
                                int k, const float *tg, float seed_mul, uint32_t qpp, uint2 *cand,
                                uint32_t capg, uint32_t *ccount, float *od, uint32_t *oi,
                                uint32_t *fail_list, uint32_t *fail_count, uint32_t pos_base,
-                               bool retry, unsigned long long *stats, hipStream_t s);
+                               bool retry, bool fix_seed, unsigned long long *stats,
+                               hipStream_t s);
 
 // ball.hip: radius count (out_idx == nullptr) or CSR fill over m kd-ordered
 // queries (periodic queries outside [0, L]^3 are skipped: query.hip answers them)

@@ -640,7 +640,8 @@ nbkd_status launch_knn_collect(const Tree &t, const float *q, const uint32_t *or
                                int k, const float *tg, float seed_mul, uint32_t qpp, uint2 *cand,
                                uint32_t capg, uint32_t *ccount, float *od, uint32_t *oi,
                                uint32_t *fail_list, uint32_t *fail_count, uint32_t pos_base,
-                               bool retry, unsigned long long *stats, hipStream_t s) {
+                               bool retry, bool fix_seed, unsigned long long *stats,
+                               hipStream_t s) {
     if (m == 0) return NBKD_OK;
     {
         TimedScope ts(retry ? "knn_retry" : "knn_collect", s);
@@ -652,8 +653,8 @@ nbkd_status launch_knn_collect(const Tree &t, const float *q, const uint32_t *or
     }
     {
         TimedScope ts(retry ? "knn_retry" : "knn_select", s);
-        // first pass with the adaptive retry: failures rewrite their seed
-        float *tg_fix = (!retry && retry_adaptive()) ? const_cast<float *>(tg) : nullptr;
+        // a retry round follows: failures rewrite their seed for it
+        float *tg_fix = fix_seed ? const_cast<float *>(tg) : nullptr;
         const float mu = (float)k + 4.0f * sqrtf((float)k) + 4.0f;
         if (k <= 16)
             launch_select<16>(t, q, order, m, k, qpp, cand, capg, ccount, od, oi, fail_list,

@@ -925,7 +925,7 @@ nbkd_status knn_locked(const Tree &t, const float *q, uint64_t m, int k, float *
                     const uint32_t nb = (uint32_t)std::min<uint64_t>(batch, mm - b0);
                     rc = launch_knn_collect(t, dq, ord + b0, nb, k, tg, 1.0f, 64u, cand, capg,
                                             ccount, dd, di, rlist, rcount, (uint32_t)b0, false,
-                                            stats, s);
+                                            retry_adaptive(), stats, s);
                     if (rc) return rc;
                 }
             }
@@ -967,13 +967,42 @@ nbkd_status knn_locked(const Tree &t, const float *q, uint64_t m, int k, float *
                 uint2 *rcand = (uint2 *)t.ws.get(WS_CAND, rb * capr * 8u, s);
                 uint32_t *rcc = (uint32_t *)t.ws.get(WS_CCOUNT, rb * 4u, s);
                 if (!rcand || !rcc) return NBKD_ENOMEM;
+                // adaptive: the retry's failures (query ids) go to rlist for a
+                // second round; rlist's sorted positions were consumed by the
+                // gather above (stream order)
+                const bool second = retry_adaptive();
+                if (second) NBKD_HIP(hipMemsetAsync(rcount, 0, 4, s));
                 for (uint64_t b0 = 0; b0 < nr; b0 += rb) {
                     const uint32_t nb = (uint32_t)std::min<uint64_t>(rb, nr - b0);
-                    rc = launch_knn_collect(t, dq, rq + b0, nb, k, tg,
-                                            retry_adaptive() ? 1.0f : 4.0f, rqpp, rcand, capr,
-                                            rcc, dd, di, list, count, 0xFFFFFFFFu, true, nullptr,
-                                            s);
+                    rc = launch_knn_collect(t, dq, rq + b0, nb, k, tg, second ? 1.0f : 4.0f,
+                                            rqpp, rcand, capr, rcc, dd, di,
+                                            second ? rlist : list, second ? rcount : count,
+                                            0xFFFFFFFFu, true, second, nullptr, s);
                     if (rc) return rc;
+                }
+                uint32_t nr2 = 0;
+                if (second) {
+                    NBKD_HIP(hipMemcpyAsync(&nr2, rcount, 4, hipMemcpyDeviceToHost, s));
+                    NBKD_HIP(hipStreamSynchronize(s));
+                }
+                if (nr2 > 0) {
+                    // second round, one query per wave: the seed each failure
+                    // rewrote (2x..8x volume when short, same seed when the 8x
+                    // column overflowed) and a 64x column; what still fails
+                    // joins the exact kernel's list
+                    const uint32_t capr2 = collect_capacity(k) * 64u;
+                    uint64_t rb2 = std::max<uint64_t>(budget / ((uint64_t)capr2 * 8u), 64);
+                    rb2 = std::min<uint64_t>(rb2, nr2);
+                    uint2 *rcand2 = (uint2 *)t.ws.get(WS_CAND, rb2 * capr2 * 8u, s);
+                    uint32_t *rcc2 = (uint32_t *)t.ws.get(WS_CCOUNT, rb2 * 4u, s);
+                    if (!rcand2 || !rcc2) return NBKD_ENOMEM;
+                    for (uint64_t b0 = 0; b0 < nr2; b0 += rb2) {
+                        const uint32_t nb = (uint32_t)std::min<uint64_t>(rb2, nr2 - b0);
+                        rc = launch_knn_collect(t, dq, rlist + b0, nb, k, tg, 1.0f, 1u, rcand2,
+                                                capr2, rcc2, dd, di, list, count, 0xFFFFFFFFu,
+                                                true, false, nullptr, s);
+                        if (rc) return rc;
+                    }
                 }
             }
         } else {
