@@ -234,7 +234,8 @@ def test_device_pointer_path(gpu):
 @pytest.mark.parametrize("box", [None, 1.0])
 def test_knn_seed_retry_and_no_seed(gpu, oracle, monkeypatch, seed_param, box):
     """A tiny seed ball (NBKD_KNN_SEED=0.05) makes most queries fail the collect
-    pass: they go through the 4x-seed retry and, failing that, the exact kernel.
+    pass: they go through the adaptive-seed retry, its second round (one query
+    per wave, 64x column) and, failing those, the exact kernel.
     NBKD_KNN_SEED=0 switches the seed off (register top-k packet kernel)."""
     monkeypatch.setenv("NBKD_KNN_SEED", seed_param)
     pts = uniform(60_000, 31, L=box or 1.0)
