@@ -141,3 +141,32 @@ def test_two_rank_slab_knn_on_one_gpu(gpu, oracle, tmp_path):
         assert str(res["transport"]) == "gloo-staged"
         sl = slice(r * n_per, (r + 1) * n_per)
         assert_knn_equal(res["d"], res["i"], gd[sl], gi[sl], allp, parts[r], 1.0)
+
+
+def test_bench_c5_line_small(gpu, oracle, monkeypatch, capsys):
+    """bench.py --workload c5 in-process at a small size: the JSON line's
+    radius counts and k-th densities agree with the oracle on the same
+    log-normal set (synth.lognormal_slab, one rank)."""
+    import json
+    import sys
+
+    import bench
+    from nbodyhpc_amd import synth
+
+    n, grid, r, k = 200_000, 32, 0.02, 8
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--workload", "c5", "--particles", str(n),
+                                      "--lognormal-grid", str(grid), "--radius", str(r),
+                                      "--k", str(k), "--leafsize", "32", "--steps", "1",
+                                      "--warmup", "0"])
+    args = bench.parse()
+    bench.run_c5(args, 0, 1, 0, None, False, lambda: None, lambda v: v)
+    line = json.loads(capsys.readouterr().out.strip().splitlines()[-1])
+    assert line["n_gpus"] == 1 and line["config"]["n_particles"] == n
+    pts, _, _ = synth.lognormal_slab(n, 0, 1, grid=grid)
+    t = oracle.tree(pts, 32, 1.0)
+    cnt = oracle.ball_count(t, pts, r)
+    assert abs(line["radius_count"]["mean_count"] - cnt.mean()) < 1e-6 * cnt.mean()
+    d, _ = t.query(pts, k, workers=8)
+    dens = k / (4.0 / 3.0 * np.pi * d[:, -1].astype(np.float64) ** 3) / n
+    got = line["kth_density"]["mean_density_over_mean"]
+    assert abs(got - dens.mean()) < 1e-6 * dens.mean()
