@@ -36,7 +36,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 # (its KDTreeQueryStatistics), uniform periodic k=32 at 1e8 points: N=61.8, P=307.9.
 REF_NODES_1E8, REF_POINTS_1E8 = 61.8, 307.9
 # Radius count (C3: 1e8 uniform periodic, r = 0.01 L, leafsize 32): B_r = 16*N + 12*P + 16
-# with N, P of the one-query DFS (scripts/ref_ball_counters.py --n 1e8: N=175.19, P=1302.53)
+# with N, P of the one-query DFS (tests/tools/ref_ball_counters.py --n 1e8: N=175.19, P=1302.53)
 REF_BALL_NODES_1E8, REF_BALL_POINTS_1E8 = 175.19, 1302.53
 
 

@@ -5,7 +5,7 @@ the radius query with: B_r = 16 N + 12 P + 12 + 4.
 
 Config C3 (1e8 uniform periodic, r = 0.01 L, leafsize 32) is reproduced at a
 smaller N with r scaled by (1e8 / N)^(-1/3) (same mean count, same leaf-to-ball
-geometry):  python scripts/ref_ball_counters.py --n 1e7 --queries 100000
+geometry):  python tests/tools/ref_ball_counters.py --n 1e7 --queries 100000
 """
 import argparse
 import os
@@ -13,7 +13,7 @@ import sys
 
 import numpy as np
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from nbodyhpc_amd import synth  # noqa: E402
 from oracle.oracle import Oracle  # noqa: E402
 
