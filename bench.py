@@ -505,13 +505,19 @@ def main():
     stream.synchronize()
     if ds is not None:
         # exactness of the slab-local result; widen the halo until every row is exact
-        for attempt in range(4):
+        # (checked after every rebuild, so the reported count is that of the timed tree)
+        for attempt in range(5):
             step()
             stream.synchronize()
             v = int(allmax(float(ds.violations(od.ptr, k, stream.handle))))
             halo["violations"] = v
-            if v == 0:
+            if v == 0 or attempt == 4:
                 break
+            try:
+                slab.check_halo(2.0 * ds.h, ds.bounds)
+            except ValueError as e:
+                log(f"{v} rows reach past the halo and it cannot widen: {e}")
+                break  # reported as halo.violations: rows that are not exact
             log(f"{v} rows reach past the halo (h={ds.h:.3g}); widening")
             tree.close()
             ds.exchange(ds.h * 2.0, stream.handle)

@@ -9,6 +9,7 @@
 #include <dlfcn.h>
 #include <rccl/rccl.h>
 
+#include <cmath>
 #include <cstring>
 #include <mutex>
 #include <new>
@@ -98,7 +99,7 @@ __global__ void remap_ids_kernel(uint32_t *__restrict__ idx, uint64_t n8, uint64
 // x-faces of the local domain [lo - h, hi + h): every point outside is then
 // strictly farther than the k-th neighbour found
 __global__ void violations_kernel(const float *__restrict__ q, const float *__restrict__ dist,
-                                  uint64_t m, int k, float lo, float hi, float h,
+                                  uint64_t m, int k, float lo, float hi, float h, float slack,
                                   unsigned long long *__restrict__ count) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     bool bad = false;
@@ -106,8 +107,9 @@ __global__ void violations_kernel(const float *__restrict__ q, const float *__re
         const float x = q[3 * i];
         const float dk = dist[i * (uint64_t)k + (uint64_t)(k - 1)];
         const float margin = fminf(x - (lo - h), (hi + h) - x);
-        // the f32 margin may be rounded up by an ulp or two: demand a relative gap
-        bad = !(dk < margin * (1.0f - 4e-7f));
+        // the f32 margin may be rounded up by an ulp or two, relative to the margin
+        // and to x itself: demand a relative gap plus a few ulps of the domain
+        bad = !(dk < margin * (1.0f - 4e-7f) - slack);
     }
     const uint64_t bal = __ballot(bad);
     if ((threadIdx.x & 63) == 0 && bal) atomicAdd(count, (unsigned long long)__popcll(bal));
@@ -295,8 +297,12 @@ nbkd_status nbkd_slab_violations(const float *q, const float *dist, uint64_t m, 
     DevBuf dc;
     NBKD_HIP(dc.alloc(8, s));
     NBKD_HIP(hipMemsetAsync(dc.p, 0, 8, s));
+    // absolute slack: 4 ulps of the largest |x| of the local domain, so a k-th
+    // distance within an ulp of the face is flagged even when h << the box
+    const float mag = std::fmax(std::fabs(lo - h), std::fabs(hi + h));
+    const float slack = 4.0f * (std::nextafter(mag, INFINITY) - mag);
     violations_kernel<<<(unsigned)((m + 255) / 256), 256, 0, s>>>(
-        q, dist, m, k, lo, hi, h, dc.as<unsigned long long>());
+        q, dist, m, k, lo, hi, h, slack, dc.as<unsigned long long>());
     NBKD_HIP(hipGetLastError());
     NBKD_HIP(hipMemcpyAsync(count, dc.p, 8, hipMemcpyDeviceToHost, s));
     NBKD_HIP(hipStreamSynchronize(s));

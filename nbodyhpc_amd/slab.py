@@ -26,6 +26,8 @@ import sys
 import numpy as np
 
 _TAG_RIGHTWARD, _TAG_LEFTWARD = 17, 18
+# device buffers a failed RCCL group may still touch: kept alive, never freed
+_ABANDONED = []
 
 
 def slab_bounds(rank: int, world: int, box: float):
@@ -88,6 +90,32 @@ def gen_slab_points(n_per: int, seed: int, box: float, rank: int, world: int):
     if n_per and ids[-1] > np.uint64(0xFFFFFFFE):
         raise ValueError("global ids exceed uint32")
     return out, ids.astype(np.uint32)
+
+
+def _enqueue_agreed(dist, rank, what, enqueue):
+    """Run `enqueue` (an RCCL grouped send/recv, enqueue only) and agree over
+    gloo whether it succeeded everywhere.  Returns None when every rank
+    enqueued, the local error when every rank failed (the caller may then fall
+    back to gloo on every rank), and raises when only some ranks failed: their
+    peers' queued operations can never complete, and mixing transports could
+    deliver the same range twice."""
+    import torch
+
+    err = None
+    try:
+        enqueue()
+    except Exception as e:  # agreed on below
+        err = e
+    ok = 0 if err is not None else 1
+    t = torch.tensor([ok, -ok], dtype=torch.int64)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    all_ok, any_ok = int(t[0]) == 1, -int(t[1]) == 1
+    if all_ok:
+        return None
+    if any_ok:
+        raise RuntimeError(f"rank {rank}: RCCL {what} failed on some ranks only "
+                           f"(here: {err or 'ok'}); refusing to mix transports")
+    return err
 
 
 def neighbours(rank: int, world: int):
@@ -164,8 +192,12 @@ def violations_host(q_xyz, kth_dist, rank, world, box, h, bounds=None):
     else:
         lo, hi = float(bounds[rank]), float(bounds[rank + 1])
     x = q_xyz[:, 0].astype(np.float32)
-    margin = np.minimum(x - np.float32(lo - h), np.float32(hi + h) - x)
-    ok = kth_dist.astype(np.float32) < margin * np.float32(1.0 - 4e-7)
+    f32 = np.float32
+    lo_h, hi_h = f32(f32(lo) - f32(h)), f32(f32(hi) + f32(h))
+    margin = np.minimum(x - lo_h, hi_h - x)
+    mag = np.maximum(np.abs(lo_h), np.abs(hi_h))
+    slack = np.float32(4.0) * np.spacing(mag)
+    ok = kth_dist.astype(np.float32) < margin * np.float32(1.0 - 4e-7) - slack
     return int((~ok).sum())
 
 
@@ -212,10 +244,10 @@ def redistribute(xyz, ids, rank, world, box, dist, comm=None, bounds=None, devic
     roff = np.concatenate([[0], np.cumsum(recv)])
     n_own = int(roff[-1])
     if comm is not None:
-        try:
-            return _redistribute_rccl(sx, si, rank, world, comm, soff, roff, n_own, device)
-        except Exception as e:  # reported; the gloo path below is exact too
-            (log or (lambda *a: None))(f"rank {rank}: RCCL redistribution failed ({e}); gloo")
+        out = _redistribute_rccl(sx, si, rank, world, comm, soff, roff, n_own, device, dist)
+        if out is not None:
+            return out
+        (log or (lambda *a: None))(f"rank {rank}: RCCL redistribution failed on every rank; gloo")
     import torch
 
     out_x = np.empty((n_own, 3), np.float32)
@@ -244,7 +276,9 @@ def redistribute(xyz, ids, rank, world, box, dist, comm=None, bounds=None, devic
     return out_x, out_i
 
 
-def _redistribute_rccl(sx, si, rank, world, comm, soff, roff, n_own, device):
+def _redistribute_rccl(sx, si, rank, world, comm, soff, roff, n_own, device, dist):
+    """None when the grouped send/recv failed to enqueue on every rank (the
+    caller then moves the payload over gloo into its own host buffers)."""
     from . import hip
 
     dsx = hip.DeviceArray.from_numpy(sx if len(sx) else np.zeros((1, 3), np.float32))
@@ -266,12 +300,18 @@ def _redistribute_rccl(sx, si, rank, world, comm, soff, roff, n_own, device):
         if n_self:
             hip.memcpy(drx.ptr + int(roff[rank]) * 12, dsx.ptr + int(soff[rank]) * 12, n_self * 12)
             hip.memcpy(dri.ptr + int(roff[rank]) * 4, dsi.ptr + int(soff[rank]) * 4, n_self * 4)
-        comm.exchange(pairs)
+        err = _enqueue_agreed(dist, rank, "redistribution", lambda: comm.exchange(pairs))
+        if err is not None:
+            # a failed group may still read or write these: never free them
+            _ABANDONED.extend((dsx, dsi, drx, dri))
+            dsx = dsi = drx = dri = None
+            return None
         hip.synchronize()
         return drx.numpy_head(n_own), dri.numpy_head(n_own)
     finally:
         for a in (dsx, dsi, drx, dri):
-            a.free()
+            if a is not None:
+                a.free()
 
 
 # ------------------------------------------------------------------ device path
@@ -308,7 +348,9 @@ class DeviceSlab:
         lo, hi = self.lo, self.hi
         dev, s = self.device, stream
         sel = {}
-        for name, (a, b) in (("r", (hi - h, hi)), ("l", (lo, lo + h))):
+        # open outer bounds, as exchange_host: the last rank owns x == L too
+        # (slab_of, io.read_slab), and such a point sits at x = 0 for rank 0
+        for name, (a, b) in (("r", (hi - h, math.inf)), ("l", (-math.inf, lo + h))):
             n = capi.slab_select(self.own_xyz.ptr, self.own_ids.ptr, self.n_own, a, b,
                                  device=dev, stream=s)
             bx = hip.DeviceArray((max(n, 1), 3), np.float32)
@@ -334,13 +376,22 @@ class DeviceSlab:
                 (ri.ptr, nr * 4, right, ids.ptr + o_fl * 4, n_fl * 4, left),
                 (li.ptr, nl * 4, left, ids.ptr + o_fr * 4, n_fr * 4, right),
             ]
-            try:
-                self.comm.exchange(pairs, stream=s)
+            err = _enqueue_agreed(self.dist, self.rank, "halo exchange",
+                                  lambda: self.comm.exchange(pairs, stream=s))
+            if err is None:
                 hip.synchronize()
                 done = True
                 self.transport = "rccl"
-            except Exception as e:  # reported; the host path below is exact too
-                self.log(f"rank {self.rank}: RCCL exchange failed ({e}); staging over gloo")
+            else:
+                # every rank failed: the gloo path below is exact too.  RCCL may
+                # have queued part of the group before failing, so the staged
+                # strips go to fresh buffers and the old ones are never freed.
+                self.log(f"rank {self.rank}: RCCL exchange failed ({err}); staging over gloo")
+                _ABANDONED.extend((xyz, ids) + tuple(b for v in sel.values() for b in v[1:]))
+                xyz = hip.DeviceArray((n_loc, 3), np.float32)
+                ids = hip.DeviceArray((n_loc,), np.uint32)
+                hip.memcpy(xyz.ptr, self.own_xyz.ptr, self.n_own * 12)
+                hip.memcpy(ids.ptr, self.own_ids.ptr, self.n_own * 4)
         if not done:
             sr = (sel["r"][1].numpy_head(sel["r"][0]), sel["r"][2].numpy_head(sel["r"][0]))
             sl = (sel["l"][1].numpy_head(sel["l"][0]), sel["l"][2].numpy_head(sel["l"][0]))
@@ -358,9 +409,10 @@ class DeviceSlab:
                 a = np.ascontiguousarray(arr).view(np.uint32)
                 hip.memcpy(ids.ptr + off * 4, a.ctypes.data, a.nbytes, hip.H2D)
             self.transport = "gloo-staged"
-        for v in sel.values():
-            v[1].free()
-            v[2].free()
+        if self.transport != "gloo-staged" or self.comm is None:
+            for v in sel.values():
+                v[1].free()
+                v[2].free()
         self.xyz, self.ids, self.n_local = xyz, ids, n_loc
 
     def violations(self, dist_ptr, k, stream=None):

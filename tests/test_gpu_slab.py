@@ -89,7 +89,16 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, n_per, k, outdir):
+def _rank_points(n_per, rank, world):
+    """The last rank also owns particles exactly at x = L (slab_of,
+    io.read_slab); periodically they sit at x = 0, in rank 0's domain."""
+    xyz, ids = slab.gen_slab_points(n_per, 21, 1.0, rank, world)
+    if rank == world - 1:
+        xyz[:32, 0] = 1.0
+    return xyz, ids
+
+
+def _worker(rank, world, port, n_per, k, outdir, rccl=False):
     from nbodyhpc_amd import capi, hip
 
     hip.preload()  # the ROCm 7.2 runtime must load before torch's bundled one
@@ -98,13 +107,17 @@ def _worker(rank, world, port, n_per, k, outdir):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    dev = rank if rccl else 0
     try:
-        hip.set_device(0)
-        xyz, ids = slab.gen_slab_points(n_per, 21, 1.0, rank, world)
-        ds = slab.DeviceSlab(xyz, ids, rank, world, 1.0, 0, dist, comm=None)
+        hip.set_device(dev)
+        xyz, ids = _rank_points(n_per, rank, world)
+        comm = slab.init_comm(dist, rank, world, dev) if rccl else None
+        if rccl and comm is None:
+            raise RuntimeError("RCCL communicator did not start")
+        ds = slab.DeviceSlab(xyz, ids, rank, world, 1.0, dev, dist, comm=comm)
         h = slab.halo_width(n_per * world, k, 1.0)
         ds.exchange(h)
-        t = capi.Tree(n=ds.n_local, dev_ptr=ds.xyz.ptr, leafsize=32, boxsize=1.0, device=0)
+        t = capi.Tree(n=ds.n_local, dev_ptr=ds.xyz.ptr, leafsize=32, boxsize=1.0, device=dev)
         t.set_ids(dev_ptr=ds.ids.ptr)
         od = hip.DeviceArray((n_per, k), np.float32)
         oi = hip.DeviceArray((n_per, k), np.uint32)
@@ -114,33 +127,53 @@ def _worker(rank, world, port, n_per, k, outdir):
         np.savez(os.path.join(outdir, f"r{rank}.npz"), d=od.numpy(), i=oi.numpy(), v=v,
                  nloc=ds.n_local, transport=ds.transport)
         t.close()
+        if comm is not None:
+            comm.close()
     finally:
         dist.destroy_process_group()
 
 
-def test_two_rank_slab_knn_on_one_gpu(gpu, oracle, tmp_path):
+def _run_two_ranks(tmp_path, oracle, rccl):
     import multiprocessing as mp
 
     from tests.parity import assert_knn_equal
     world, n_per, k = 2, 60_000, 32
     ctx = mp.get_context("spawn")  # plain multiprocessing: torch must not load first
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, n_per, k, str(tmp_path)))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n_per, k, str(tmp_path), rccl))
              for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
         p.join(timeout=300)
+    for p in procs:
+        if p.exitcode is None:
+            p.kill()
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
-    parts = [slab.gen_slab_points(n_per, 21, 1.0, r, world)[0] for r in range(world)]
+    parts = [_rank_points(n_per, r, world)[0] for r in range(world)]
     allp = np.concatenate(parts)
     gd, gi = oracle.tree(allp, 32, 1.0).query(allp, k, workers=8)
     for r in range(world):
         res = np.load(os.path.join(tmp_path, f"r{r}.npz"))
         assert int(res["v"]) == 0 and res["nloc"] > n_per
-        assert str(res["transport"]) == "gloo-staged"
+        assert str(res["transport"]) == ("rccl" if rccl else "gloo-staged")
         sl = slice(r * n_per, (r + 1) * n_per)
         assert_knn_equal(res["d"], res["i"], gd[sl], gi[sl], allp, parts[r], 1.0)
+    # the x = L particles of the last rank are rank 0's neighbours at x = 0
+    assert np.isin(np.arange((world - 1) * n_per, (world - 1) * n_per + 32),
+                   np.load(os.path.join(tmp_path, "r0.npz"))["i"]).any()
+
+
+def test_two_rank_slab_knn_on_one_gpu(gpu, oracle, tmp_path):
+    _run_two_ranks(tmp_path, oracle, rccl=False)
+
+
+def test_two_rank_slab_knn_rccl(gpu, oracle, tmp_path):
+    """The RCCL halo path proper: one GPU per rank, grouped ncclSend/ncclRecv
+    with both ring neighbours being the same peer (W = 2).  Needs two GPUs."""
+    if gpu.device_count() < 2:
+        pytest.skip("the RCCL halo path needs two GPUs (one per rank)")
+    _run_two_ranks(tmp_path, oracle, rccl=True)
 
 
 def test_bench_c5_line_small(gpu, oracle, monkeypatch, capsys):

@@ -25,6 +25,16 @@ def _free_port():
     return p
 
 
+def _slab_points(n_per, seed, rank, world):
+    """gen_slab_points, with a few particles of the last rank exactly at x = L:
+    the last slab owns them (io.read_slab, slab_of), and periodically they sit
+    at x = 0, inside rank 0's domain."""
+    xyz, ids = slab.gen_slab_points(n_per, seed, 1.0, rank, world)
+    if rank == world - 1:
+        xyz[:5, 0] = 1.0
+    return xyz, ids
+
+
 def test_slab_bounds_partition_the_box():
     for world in (1, 2, 3, 8):
         bounds = [slab.slab_bounds(r, world, 1.0) for r in range(world)]
@@ -62,7 +72,7 @@ def _worker(rank, world, port, n_per, k, hscale, outdir):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        xyz, ids = slab.gen_slab_points(n_per, 11, 1.0, rank, world)
+        xyz, ids = _slab_points(n_per, 11, rank, world)
         h = slab.halo_width(n_per * world, k, 1.0) * hscale
         lx, li = slab.exchange_host(xyz, ids, rank, world, 1.0, h, dist)
         tree = Oracle().tree(lx, 16, 1.0)
@@ -91,7 +101,7 @@ def test_slab_knn_equals_single_tree(world, tmp_path, oracle):
     n_per, k = 4000, 8
     # h = 1.5 x halo_width: inside the two-rank limit (2h <= slab width)
     res = _run_world(world, n_per, k, 1.5, tmp_path)
-    parts = [slab.gen_slab_points(n_per, 11, 1.0, r, world)[0] for r in range(world)]
+    parts = [_slab_points(n_per, 11, r, world)[0] for r in range(world)]
     allp = np.concatenate(parts)
     gd, gi = oracle.tree(allp, 16, 1.0).query(allp, k, workers=4)
     for r in range(world):
@@ -228,3 +238,54 @@ def test_redistribute_to_slab_owners(world, quantile, tmp_path):
         seen[res["i"]] += 1
     assert (seen == 1).all()
     assert (owner[:7] == world - 1).all()
+
+
+def _agree_worker(rank, world, port, fail_ranks, outdir):
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        def enqueue():
+            if rank in fail_ranks:
+                raise RuntimeError("enqueue failed")
+        try:
+            err = slab._enqueue_agreed(dist, rank, "test", enqueue)
+            out = "ok" if err is None else "fallback"
+        except RuntimeError:
+            out = "raised"
+        with open(os.path.join(outdir, f"a{rank}.txt"), "w") as f:
+            f.write(out)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("fail_ranks,want", [((), "ok"), ((0, 1), "fallback"),
+                                             ((1,), "raised")])
+def test_rccl_fallback_is_agreed_by_every_rank(fail_ranks, want, tmp_path):
+    """The RCCL -> gloo fallback is taken only when every rank failed to
+    enqueue; a partial failure raises on every rank instead of mixing
+    transports (a peer with queued sends would otherwise deadlock)."""
+    import torch.multiprocessing as mp
+
+    port = _free_port()
+    mp.start_processes(_agree_worker, args=(2, port, fail_ranks, str(tmp_path)), nprocs=2,
+                       join=True, start_method="spawn")
+    got = [open(os.path.join(tmp_path, f"a{r}.txt")).read() for r in range(2)]
+    assert got == [want, want]
+
+
+def test_violations_absolute_slack_for_thin_halos():
+    """When h << L the relative slack is below one ulp of x: a k-th distance
+    within a few ulps of the domain face must still be flagged."""
+    world, rank, box = 2, 1, 1.0
+    lo, hi = slab.slab_bounds(rank, world, box)
+    h = 1e-6
+    x = np.float32(0.75)
+    q = np.array([[x, 0.5, 0.5]], np.float32)
+    face = np.float32(np.float32(hi) + np.float32(h)) - x
+    near = np.float32(face) - np.float32(2.0) * np.spacing(np.float32(1.0))
+    assert slab.violations_host(q, np.array([near], np.float32), rank, world, box, h) == 1
+    ok = np.float32(face) * np.float32(0.5)
+    assert slab.violations_host(q, np.array([ok], np.float32), rank, world, box, h) == 0
