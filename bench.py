@@ -40,6 +40,12 @@ REF_NODES_1E8, REF_POINTS_1E8 = 61.8, 307.9
 REF_BALL_NODES_1E8, REF_BALL_POINTS_1E8 = 175.19, 1302.53
 
 
+def _phase_frac(st):
+    keys = ("clk_walk", "clk_wait", "clk_leaf_test", "clk_dense", "clk_sparse", "clk_tighten")
+    tot = sum(st.get(kk, 0) for kk in keys)
+    return {kk[4:]: st[kk] / tot for kk in keys} if tot else None
+
+
 def bytes_per_query(k, nodes=REF_NODES_1E8, points=REF_POINTS_1E8):
     return 16.0 * nodes + 12.0 * points + 12.0 + 8.0 * k
 
@@ -51,7 +57,9 @@ def parse():
     p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--particles", dest="n", type=float, default=1e8, help="particles per GPU")
     p.add_argument("--k", type=int, default=32)
-    p.add_argument("--leafsize", type=int, default=32)
+    p.add_argument("--leafsize", type=int, default=64,
+                   help="tree leaf size (default 64: the reference _impl.KDTree default, "
+                        "kdtree/src/cpp/pybind.cpp:200-205)")
     p.add_argument("--box", type=float, default=1.0)
     p.add_argument("--seed", type=int, default=20261015)
     p.add_argument("--cpu-sample", type=int, default=10_000_000,
@@ -172,7 +180,7 @@ def suite(args, capi, hip, tree, dev_pts, n, k, L, stream, od, oi):
     out["radius_count"] = {"queries_per_s": n / sec, "ms": sec * 1e3,
                            "kernel_ms": kern_ms / steps, "r": r, "mean_count": float(c.mean()),
                            "expected_mean_count": expect, "queries": n}
-    if n == 100_000_000 and abs(args.radius - 0.01) < 1e-12 and args.leafsize == 32:
+    if n == 100_000_000 and abs(args.radius - 0.01) < 1e-12:
         # algorithmic bytes per query / kernel time; frac > 1 means the leaves are
         # re-read from cache (the kernel is VALU-bound: profiles/r01k_ball_pmc.txt)
         br = 16.0 * REF_BALL_NODES_1E8 + 12.0 * REF_BALL_POINTS_1E8 + 16.0
@@ -215,8 +223,8 @@ def suite(args, capi, hip, tree, dev_pts, n, k, L, stream, od, oi):
     capi.timing_enable(True)
     sec = timed(lambda: lt.query_device(dl.ptr, n, k, od.ptr, oi.ptr, stream.handle), steps, hip)
     br = {nm: capi.timing_read(nm)[0] / steps for nm in
-          ("leaf_key", "sort", "knn_collect", "knn_select", "knn_retry_order", "knn_retry",
-           "knn_fallback")}
+          ("leaf_key", "sort", "knn_collect", "knn_select", "knn_retry_order",
+           "knn_retry", "knn_fallback")}
     capi.timing_enable(False)
     capi.stats_enable(True)
     lt.query_device(dl.ptr, n, k, od.ptr, oi.ptr, stream.handle)
@@ -567,9 +575,10 @@ def main():
     value = total_q / elapsed_max
     ms_per_step = elapsed_max / args.steps * 1e3
     bq = bytes_per_query(k)
-    # dominant kernel: knn_collect_kernel, launched once per query batch (the
-    # candidate-column budget); achieved = algorithmic bytes of the queries one
-    # launch processes / that launch's average duration (HIP events, launch stream)
+    # dominant kernel: the collect kernel (knn_collect_grp_kernel), launched once
+    # per query batch (the candidate-column budget); achieved = algorithmic bytes
+    # of the queries one launch processes / that launch's average duration (HIP
+    # events on the launch stream)
     col_launches = max(col_launches, 1)
     col_avg_ms = col_ms / col_launches
     q_per_launch = own * args.steps / col_launches
@@ -625,7 +634,7 @@ def main():
         "roofline": {
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-            "kernel": "knn_collect_kernel<periodic> (nbodyhpc_amd/csrc/knn_collect.hip)",
+            "kernel": "knn_collect_grp_kernel<periodic> (nbodyhpc_amd/csrc/knn_collect.hip)",
             "kernel_ms_per_launch": col_avg_ms,
             "launches_per_step": col_launches / args.steps,
             "queries_per_launch": q_per_launch,
@@ -645,6 +654,8 @@ def main():
                                  for kk in ("node_visits", "dense_steps", "sparse_iters",
                                             "points_staged", "candidates", "leaves_scanned")},
         "fallback_queries": st["fallback_queries"], "retry_queries": st["retry_queries"],
+        # where a collect wave's cycles go (work-counter pass, s_memtime clocks)
+        "collect_phase_frac": _phase_frac(st),
         "cpu_baseline": None if cpu is None else {kk: cpu[kk] for kk in
                                                   ("value", "unit", "cores", "kind", "sample")},
         "cpu_build_ms": None if cpu is None else cpu["build_s"] * 1e3,

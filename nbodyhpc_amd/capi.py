@@ -11,7 +11,8 @@ import re
 import numpy as np
 
 PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG, "lib", "libnbkd.so")
+# NBKD_LIB: an alternative build of the library (A/B experiments)
+LIB_PATH = os.environ.get("NBKD_LIB") or os.path.join(PKG, "lib", "libnbkd.so")
 HEADER = os.path.join(os.path.dirname(PKG), "include", "nbkd.h")
 
 NBKD_OK, NBKD_EINVAL, NBKD_EBOX, NBKD_ETOOMANY, NBKD_ENOMEM, NBKD_EDEVICE = range(6)
@@ -236,9 +237,12 @@ def stats_read():
 # entered x packet lanes, (query, point) distance evaluations, dense point steps,
 # sparse (lane-compacted) iterations, leaf points staged, packets (waves),
 # candidates appended, leaves scanned, queries sent to the exact kernel,
-# queries retried with a larger seed ball
+# queries retried with a larger seed ball; then the collect kernel's phase
+# clocks (shader cycles summed over waves): tree walk, leaf staging wait, leaf
+# need test, dense scan, sparse scan, bound update
 STATS_NAMES = ("node_visits", "pair_evals", "dense_steps", "sparse_iters", "points_staged",
-               "packets", "candidates", "leaves_scanned", "fallback_queries", "retry_queries")
+               "packets", "candidates", "leaves_scanned", "fallback_queries", "retry_queries",
+               "clk_walk", "clk_wait", "clk_leaf_test", "clk_dense", "clk_sparse", "clk_tighten")
 
 
 def stats_read_all():

@@ -50,6 +50,8 @@ void free_tree(Tree &t) {
     if (t.shape_n) (void)hipFree(t.shape_n);
     if (t.leafinfo) (void)hipFree(t.leafinfo);
     if (t.hsplit) (void)hipFree(t.hsplit);
+    if (t.ginfo) (void)hipFree(t.ginfo);
+    t.ginfo = nullptr;
     t.leafinfo = nullptr;
     t.hsplit = nullptr;
     t.splits = nullptr;

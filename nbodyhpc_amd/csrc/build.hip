@@ -562,6 +562,134 @@ leafinfo_kernel(const nbkd_node *__restrict__ nodes, uint64_t nn, const float *_
     }
 }
 
+// Sub-leaf groups (internal.hpp Tree::ginfo).  One wave per leaf, up to
+// GPL points per lane, per run of NBKD_GBLOCK positions: the run is cut
+// recursively like the tree itself (m = floor(count / 2 / 8) * 8, so every
+// piece is a multiple of 8) but on the widest axis of the piece's real points,
+// each piece ordered by (coordinate, position), until pieces hold NBKD_GROUP
+// points; then each group's tight box is written.  Only the order inside a
+// leaf changes: leaf membership, the node table and every query result stay
+// the same (the kNN parity contract compares leaves and tie groups as sets),
+// and padding rows (FLT_MAX) sort last and are left out of the boxes.
+constexpr int GPL = NBKD_GBLOCK / 64; // points per lane
+
+__global__ void __launch_bounds__(TB)
+group_kernel(const nbkd_node *__restrict__ nodes, uint64_t nn, float *__restrict__ x,
+             float *__restrict__ y, float *__restrict__ z, uint32_t *__restrict__ idx, uint64_t n,
+             float *__restrict__ ginfo) {
+    constexpr int WPB = TB / 64;
+    __shared__ float sp[WPB][3][NBKD_GBLOCK];
+    __shared__ uint32_t sr[WPB][NBKD_GBLOCK];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    float (*const P)[NBKD_GBLOCK] = sp[wave];
+    uint32_t *const R = sr[wave];
+    const uint64_t nw = (uint64_t)gridDim.x * WPB;
+    for (uint64_t i = (uint64_t)blockIdx.x * WPB + wave; i < nn; i += nw) {
+        const nbkd_node nd = nodes[i];
+        if (nd.dimension >= 0) continue;
+        for (uint32_t b0 = nd.left; b0 < nd.right; b0 += NBKD_GBLOCK) {
+            const uint32_t c = min((uint32_t)NBKD_GBLOCK, nd.right - b0);
+            // point h of this lane: run position lane + 64 h
+            float p[GPL][3];
+            uint32_t id[GPL], real[GPL], pos[GPL], s[GPL], l[GPL];
+#pragma unroll
+            for (int h = 0; h < GPL; ++h) {
+                const uint32_t j = (uint32_t)(lane + 64 * h);
+                const bool on = j < c;
+                p[h][0] = on ? x[b0 + j] : FLT_MAX;
+                p[h][1] = on ? y[b0 + j] : FLT_MAX;
+                p[h][2] = on ? z[b0 + j] : FLT_MAX;
+                id[h] = on ? idx[b0 + j] : 0xFFFFFFFFu;
+                real[h] = (on && id[h] < n) ? 1u : 0u;
+                pos[h] = j;
+                s[h] = 0;
+                l[h] = on ? c : 0u;
+            }
+            for (;;) {
+                bool more = false;
+#pragma unroll
+                for (int h = 0; h < GPL; ++h) more |= l[h] > (uint32_t)NBKD_GROUP;
+                if (!__any(more)) break;
+#pragma unroll
+                for (int h = 0; h < GPL; ++h) {
+                    P[0][pos[h]] = p[h][0];
+                    P[1][pos[h]] = p[h][1];
+                    P[2][pos[h]] = p[h][2];
+                    R[pos[h]] = real[h];
+                }
+                wave_sync();
+                uint32_t npos[GPL];
+#pragma unroll
+                for (int h = 0; h < GPL; ++h) {
+                    npos[h] = pos[h];
+                    if (l[h] <= (uint32_t)NBKD_GROUP) continue;
+                    float lo[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, hi[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+                    for (uint32_t j = s[h]; j < s[h] + l[h]; ++j) {
+                        if (!R[j]) continue;
+#pragma unroll
+                        for (int a = 0; a < 3; ++a) {
+                            lo[a] = fminf(lo[a], P[a][j]);
+                            hi[a] = fmaxf(hi[a], P[a][j]);
+                        }
+                    }
+                    const float ex = hi[0] - lo[0], ey = hi[1] - lo[1], ez = hi[2] - lo[2];
+                    const int ax = (ey > ex && ey >= ez) ? 1 : (ez > ex && ez > ey ? 2 : 0);
+                    const float key = p[h][ax];
+                    uint32_t rank = 0;
+                    for (uint32_t j = s[h]; j < s[h] + l[h]; ++j) {
+                        const float kj = P[ax][j];
+                        rank += (kj < key || (kj == key && j < pos[h])) ? 1u : 0u;
+                    }
+                    const uint32_t m = (l[h] / 2) / 8 * 8;
+                    npos[h] = s[h] + rank;
+                    if (rank < m) {
+                        l[h] = m;
+                    } else {
+                        s[h] += m;
+                        l[h] -= m;
+                    }
+                }
+                wave_sync();
+#pragma unroll
+                for (int h = 0; h < GPL; ++h) pos[h] = npos[h];
+            }
+#pragma unroll
+            for (int h = 0; h < GPL; ++h) {
+                if ((uint32_t)(lane + 64 * h) < c) {
+                    x[b0 + pos[h]] = p[h][0];
+                    y[b0 + pos[h]] = p[h][1];
+                    z[b0 + pos[h]] = p[h][2];
+                    idx[b0 + pos[h]] = id[h];
+                }
+                P[0][pos[h]] = p[h][0];
+                P[1][pos[h]] = p[h][1];
+                P[2][pos[h]] = p[h][2];
+                R[pos[h]] = real[h];
+            }
+            wave_sync();
+            if ((uint32_t)lane < c / NBKD_GROUP) {
+                float lo[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, hi[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+                for (int j = lane * NBKD_GROUP; j < (lane + 1) * NBKD_GROUP; ++j) {
+                    if (!R[j]) continue;
+#pragma unroll
+                    for (int a = 0; a < 3; ++a) {
+                        lo[a] = fminf(lo[a], P[a][j]);
+                        hi[a] = fmaxf(hi[a], P[a][j]);
+                    }
+                }
+                float *o = ginfo + 6 * ((size_t)(b0 / NBKD_GROUP) + lane);
+                o[0] = lo[0];
+                o[1] = hi[0];
+                o[2] = lo[1];
+                o[3] = hi[1];
+                o[4] = lo[2];
+                o[5] = hi[2];
+            }
+            wave_sync();
+        }
+    }
+}
+
 // Split values in heap (BFS) order for the query bucketing descent: the node
 // reached by turns t_1..t_d (0 left, 1 right) has heap index h, children 2h+1 /
 // 2h+2, so the descent needs neither child ids nor the shape table, and the top
@@ -837,6 +965,14 @@ nbkd_status build_tree(Tree &t, const float *xyz, uint64_t n, int32_t leaf_size,
         heap_splits_kernel<<<(unsigned)std::max<uint64_t>(blocks, 1), TB, 0, s>>>(
             t.nodes, t.nnodes, t.splits, t.shape_c, t.shape_n, t.shape_len, (uint32_t)t.n8,
             (uint32_t)t.leaf, hblk_offset(t.depth), t.hsplit);
+        NBKD_HIP(hipGetLastError());
+    }
+    if (n8 > 0) {
+        TimedScope ts("build_groups", s);
+        NBKD_HIP(hipMalloc(&t.ginfo, (n8 / NBKD_GROUP) * 6 * sizeof(float)));
+        const uint64_t blocks = std::min<uint64_t>((t.nnodes + 3) / 4, 65536);
+        group_kernel<<<(unsigned)std::max<uint64_t>(blocks, 1), TB, 0, s>>>(
+            t.nodes, t.nnodes, t.x, t.y, t.z, t.idx, t.n, t.ginfo);
         NBKD_HIP(hipGetLastError());
     }
     {

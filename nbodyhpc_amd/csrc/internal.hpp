@@ -30,6 +30,8 @@ struct Workspace {
 };
 
 constexpr int NBKD_PAD_LEAVES = 8;
+constexpr int NBKD_GROUP = 8;   // points per sub-leaf group (leaf counts are multiples of 8)
+constexpr int NBKD_GBLOCK = 128; // points ordered together into groups (<= 64 lanes x 2)
 
 // Device-resident tree.  Points are SoA in tree order (the reference layout,
 // kdtree/src/cpp/include/kdtree/position_array.hpp:166-271): x, y, z, original
@@ -53,6 +55,11 @@ struct Tree {
     int shape_len = 0;
     // per node id, leaves only: tight box lo.xyz, hi.xyz, left, right (8 words)
     uint32_t *leafinfo = nullptr;
+    // 8-point groups: the points of each leaf are ordered (per run of 128) by
+    // median splits on the widest axis into groups of NBKD_GROUP consecutive
+    // positions; ginfo[6 g .. 6 g + 6) = the tight box of group g (positions
+    // 8g .. 8g+7, real points only) as lo.x, hi.x, lo.y, hi.y, lo.z, hi.z
+    float *ginfo = nullptr;
     // internal nodes' split values in the 4-level blocked heap order below
     // (hblk_blocks(depth) lines of 16 floats), or nullptr
     float *hsplit = nullptr;
@@ -100,7 +107,7 @@ struct TimedScope {
 };
 bool timing_enabled();
 bool stats_enabled();
-constexpr int NBKD_NSTATS = 10; // see capi.STATS_NAMES (collect kernel) + exact-kernel and retried queries
+constexpr int NBKD_NSTATS = 16; // see capi.STATS_NAMES (collect kernel) + exact-kernel and retried queries
 void stats_store(const uint64_t *v);
 
 // RAII device allocation (plain hipMalloc; freed after the stream drained).

@@ -211,8 +211,22 @@ knn_collect_kernel(DevTree t, const uint32_t *__restrict__ linfo, const float *_
     uint32_t la = 0, pa = 0, ea = 0, lb = 0, pbb = 0, eb = 0;
     bool ha = false, hb = false;
     int b = 0;
+    // phase clocks of the work-counter instance (STATS): shader cycles per wave
+    // in the walk, the staging wait, the leaf test, dense and sparse scanning
+    // and the bound update
+    uint64_t ph[6] = {0, 0, 0, 0, 0, 0};
+    uint64_t tclk = STATS ? clock64() : 0;
+#define NBKD_PH(I)                                                                                 \
+    do {                                                                                           \
+        if constexpr (STATS) {                                                                     \
+            const uint64_t t_ = clock64();                                                         \
+            ph[I] += t_ - tclk;                                                                    \
+            tclk = t_;                                                                             \
+        }                                                                                          \
+    } while (0)
     NBKD_COLLECT_WALK(ha, la, pa, ea);
     if (ha) NBKD_COLLECT_STAGE(0, la, pa, ea);
+    NBKD_PH(0);
     while (ha) {
         if constexpr (PIPE) {
             NBKD_COLLECT_WALK(hb, lb, pbb, eb);
@@ -226,6 +240,7 @@ knn_collect_kernel(DevTree t, const uint32_t *__restrict__ linfo, const float *_
             wait_vm0();
         }
         wave_sync();
+        NBKD_PH(1);
         {
             const uint32_t lpos = pa, lend = ea;
             // first chunk + tight box already staged in buffer b (stage())
@@ -233,6 +248,7 @@ knn_collect_kernel(DevTree t, const uint32_t *__restrict__ linfo, const float *_
             uint32_t cn = min((uint32_t)CHUNK, lend - lpos);
             const float tb[6] = {W.tb[b][0], W.tb[b][3], W.tb[b][1], W.tb[b][4], W.tb[b][2], W.tb[b][5]};
             const uint64_t need = __ballot(box_lb2<PER>(qx, qy, qz, tb, L) <= kth);
+            NBKD_PH(2);
             if (need != 0) {
             const uint32_t nneed = (uint32_t)__popcll(need);
             if constexpr (STATS) ++n_leaves;
@@ -277,6 +293,7 @@ knn_collect_kernel(DevTree t, const uint32_t *__restrict__ linfo, const float *_
                             }
                         }
                     }
+                    NBKD_PH(3);
                 } else {
                     // (needing query, point) pairs compacted onto the 64 lanes:
                     // slot = pair & (c2-1), point = pair >> log2(c2), c2 = pow2 >= nneed
@@ -314,6 +331,7 @@ knn_collect_kernel(DevTree t, const uint32_t *__restrict__ linfo, const float *_
                     }
                     wave_sync();
                     cnt = W.cnt[lane];
+                    NBKD_PH(4);
                 }
                 c0 += cn;
                 if (c0 >= lend) {
@@ -347,6 +365,7 @@ knn_collect_kernel(DevTree t, const uint32_t *__restrict__ linfo, const float *_
                                 kth = fminf(kth, (float)(jstar + 1) * s_over_nb);
                         }
                     }
+                    NBKD_PH(5);
                     break;
                 }
                 cn = min((uint32_t)CHUNK, lend - c0);
@@ -370,7 +389,9 @@ knn_collect_kernel(DevTree t, const uint32_t *__restrict__ linfo, const float *_
             NBKD_COLLECT_WALK(ha, la, pa, ea);
             if (ha) NBKD_COLLECT_STAGE(0, la, pa, ea);
         }
+        NBKD_PH(0);
     }
+#undef NBKD_PH
     if (valid) ccount[gq] = cnt;
     if (STATS && lane == 0) {
         atomicAdd(&stats[0], (unsigned long long)n_nodes); // node visits of the packet walk
@@ -380,6 +401,372 @@ knn_collect_kernel(DevTree t, const uint32_t *__restrict__ linfo, const float *_
         atomicAdd(&stats[4], (unsigned long long)n_scanned);
         atomicAdd(&stats[5], 1ull);
         atomicAdd(&stats[7], (unsigned long long)n_leaves);
+#pragma unroll
+        for (int i = 0; i < 6; ++i) atomicAdd(&stats[10 + i], (unsigned long long)ph[i]);
+    }
+    if (STATS) {
+        uint32_t c = valid ? cnt : 0u;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+        if (lane == 0) atomicAdd(&stats[6], (unsigned long long)c);
+    }
+}
+
+// ---------------------------------------------------------------- group variant
+// The same packet walk over a tree whose leaves are cut into 8-point groups
+// with their own tight boxes (build.hip group_kernel).  At a leaf each lane
+// tests every group of the staged chunk (up to 64 points, 8 groups): the
+// (lane, group) pairs replace the leaf-level need test, so a query evaluates
+// only the points of groups its ball reaches (about half of the leaf-level
+// count at leafsize 32, a third at 64: tests/tools/knn_group_estimate.py).
+// Groups that at least `gdense` lanes need are scanned by every lane (dense);
+// the other pairs are compacted, 8 (pair, point) evaluations per pair, onto
+// the 64 lanes (sparse).
+//
+// Tried and dropped: running packets whose balls clear the box faces with the
+// non-periodic formulas (4 % fewer VALU instructions).  One kernel holding
+// both variants spills VGPRs at the 8-wave budget; two launches leave the
+// wrap packets (~4 %) as a latency-bound tail (+10.9 ms at 1e8), or, on a side
+// stream beside the main launch, still cost +5 ms (r02f/r02g).
+//
+#ifndef NBKD_EXP_NOSTORE
+#define NBKD_EXP_NOSTORE 0
+#endif
+constexpr int GCHUNK = 64; // points staged per step (a multiple of NBKD_GROUP)
+constexpr int GMAX = GCHUNK / NBKD_GROUP;
+
+struct CollectLdsG {
+    float4 sq[64]; // per lane: query xyz + bound
+    float scl[64]; // per lane: bucket factor (d2_bucket)
+    uint32_t cnt[64];
+    uint32_t hist[NB / 4][64];
+    float pb[3][GCHUNK];
+    float gb[6 * GMAX];          // the chunk's group boxes (lo.x, hi.x, lo.y, hi.y, lo.z, hi.z)
+    uint16_t pairs[64 * GMAX];   // sparse (lane, group) pairs: lane | group << 6
+};
+
+#define NBKD_COLLECT_STAGE_G(LPOS, LEND)                                                           \
+    do {                                                                                           \
+        const uint32_t cn_ = min((uint32_t)GCHUNK, (LEND) - (LPOS));                               \
+        glds_f32(t.x + (LPOS), W.pb[0], lane, cn_);                                                \
+        glds_f32(t.y + (LPOS), W.pb[1], lane, cn_);                                                \
+        glds_f32(t.z + (LPOS), W.pb[2], lane, cn_);                                                \
+        glds_f32(ginfo + 6 * (size_t)((LPOS) / NBKD_GROUP), W.gb, lane, 6 * (cn_ / NBKD_GROUP));   \
+    } while (0)
+
+// one internal node (record nd): test both children for every lane, push the
+// far one when both are wanted, step into the near one.  (Tried and dropped:
+// loading both children's records on entry, consumed after the tests, to take
+// the node load off the dependent chain: collect 62.4 -> 66.4 ms, r02h.)
+#define NBKD_GSTEP_ANY                                                                             \
+    {                                                                                              \
+        const int dim = nd.dimension;                                                              \
+        const float split = nd.split;                                                              \
+        const float qd = dim == 0 ? qx : (dim == 1 ? qy : qz);                                     \
+        const float lo = dim == 0 ? bx[0] : (dim == 1 ? bx[2] : bx[4]);                            \
+        const float hi = dim == 0 ? bx[1] : (dim == 1 ? bx[3] : bx[5]);                            \
+        const float tl = box_lb_axis<M>(qd, lo, split, L);                                         \
+        const float tr = box_lb_axis<M>(qd, split, hi, L);                                         \
+        const float dl = ((dim == 0 ? tl : tm[0]) + (dim == 1 ? tl : tm[1])) + (dim == 2 ? tl : tm[2]); \
+        const float dr = ((dim == 0 ? tr : tm[0]) + (dim == 1 ? tr : tm[1])) + (dim == 2 ? tr : tm[2]); \
+        const uint64_t wl = __ballot(dl <= kth), wr = __ballot(dr <= kth);                         \
+        const uint32_t right_votes = (uint32_t)__popcll(wm & __ballot(qd > split));                \
+        const bool right_first = 2 * right_votes > (uint32_t)__popcll(wm);                         \
+        const uint64_t wn = right_first ? wr : wl, wf = right_first ? wl : wr;                     \
+        const int near_slot = right_first ? 2 * dim : 2 * dim + 1;                                 \
+        const int far_slot = right_first ? 2 * dim + 1 : 2 * dim;                                  \
+        const uint32_t sb = __float_as_uint(split);                                                \
+        const bool go_near = wn != 0;                                                              \
+        const bool go_right = go_near == right_first;                                              \
+        if (wn != 0 && wf != 0) {                                                                  \
+            const uint32_t far_node = right_first ? nd.left : nd.right;                            \
+            const bool me = lane == sp;                                                            \
+            sk_node = me ? far_node : sk_node;                                                     \
+            _Pragma("unroll") for (int a = 0; a < 6; ++a) {                                        \
+                const uint32_t fv =                                                                \
+                    __builtin_amdgcn_readfirstlane(a == far_slot ? sb : __float_as_uint(bx[a]));   \
+                sk_b[a] = me ? __uint_as_float(fv) : sk_b[a];                                      \
+            }                                                                                      \
+            ++sp;                                                                                  \
+        }                                                                                          \
+        if (wn == 0 && wf == 0) continue;                                                          \
+        const int slot = go_near ? near_slot : far_slot;                                           \
+        node = go_right ? nd.right : nd.left;                                                      \
+        nd = cnodes[node];                                                                         \
+        const float tnew = go_right ? tr : tl;                                                     \
+        _Pragma("unroll") for (int a = 0; a < 3; ++a) tm[a] = dim == a ? tnew : tm[a];             \
+        _Pragma("unroll") for (int a = 0; a < 6; ++a) bx[a] = __uint_as_float(                     \
+            __builtin_amdgcn_readfirstlane(a == slot ? sb : __float_as_uint(bx[a])));              \
+        wm = go_near ? wn : wf;                                                                    \
+        have = true;                                                                               \
+    }
+
+// advance the packet walk to the next leaf some lane wants (FOUND = false: done)
+#define NBKD_GWALK(FOUND, LPOS, LEND)                                                              \
+    FOUND = false;                                                                                 \
+    for (;;) {                                                                                     \
+        if (!have) {                                                                               \
+            if (sp == 0) break;                                                                    \
+            --sp;                                                                                  \
+            node = (uint32_t)__builtin_amdgcn_readlane((int)sk_node, sp);                          \
+            _Pragma("unroll") for (int a = 0; a < 6; ++a) bx[a] = rdlane(sk_b[a], sp);             \
+            tm[0] = box_lb_axis<M>(qx, bx[0], bx[1], L);                                           \
+            tm[1] = box_lb_axis<M>(qy, bx[2], bx[3], L);                                           \
+            tm[2] = box_lb_axis<M>(qz, bx[4], bx[5], L);                                           \
+            wm = __ballot((tm[0] + tm[1]) + tm[2] <= kth);                                         \
+            if (wm == 0) continue;                                                                 \
+            nd = cnodes[node];                                                                     \
+        }                                                                                          \
+        have = false;                                                                              \
+        if constexpr (STATS) ++st[0];                                                              \
+        if (nd.dimension < 0) {                                                                    \
+            LPOS = nd.left;                                                                        \
+            LEND = nd.right;                                                                       \
+            FOUND = true;                                                                          \
+            break;                                                                                 \
+        }                                                                                          \
+        NBKD_GSTEP_ANY                                                                             \
+    }
+
+// st: node visits, leaves scanned, points staged, dense points, sparse
+// iterations, pair evaluations, then 6 phase clocks (STATS only)
+template <bool PER, bool M, int G, bool STATS>
+__device__ __forceinline__ void grp_packet(const DevTree &t, const float *__restrict__ ginfo,
+                                           CollectLdsG &W, const int lane, const float qx,
+                                           const float qy, const float qz, float kth,
+                                           const float s_over_nb, const float nb_over_s,
+                                           uint2 *__restrict__ col, const uint32_t qpp,
+                                           const uint32_t capg, const int kq, const int gdense,
+                                           uint32_t &cnt, uint64_t (&st)[12]) {
+    const float L = t.box;
+    uint32_t last_cnt = 0;
+    uint32_t sk_node = 0;
+    float sk_b[6] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+    int sp = 0;
+    const cnode_ptr cnodes = (cnode_ptr)t.nodes;
+    uint32_t node = 0;
+    float bx[6];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        bx[2 * a] = PER ? 0.0f : -FLT_MAX;
+        bx[2 * a + 1] = PER ? L : FLT_MAX;
+    }
+    float tm[3] = {box_lb_axis<M>(qx, bx[0], bx[1], L), box_lb_axis<M>(qy, bx[2], bx[3], L),
+                   box_lb_axis<M>(qz, bx[4], bx[5], L)};
+    uint64_t wm = __ballot((tm[0] + tm[1]) + tm[2] <= kth);
+    bool have = wm != 0;
+    nbkd_node nd = cnodes[0]; // record of `node` while `have`
+    uint64_t tclk = STATS ? clock64() : 0;
+#define NBKD_PH(I)                                                                                 \
+    do {                                                                                           \
+        if constexpr (STATS) {                                                                     \
+            const uint64_t t_ = clock64();                                                         \
+            st[6 + (I)] += t_ - tclk;                                                              \
+            tclk = t_;                                                                             \
+        }                                                                                          \
+    } while (0)
+    uint32_t pa = 0, ea = 0;
+    for (;;) {
+        bool ha;
+        NBKD_GWALK(ha, pa, ea);
+        if (!ha) break;
+        NBKD_COLLECT_STAGE_G(pa, ea);
+        NBKD_PH(0);
+        wait_vm0();
+        wave_sync();
+        NBKD_PH(1);
+        const uint32_t lend = ea;
+        uint32_t c0 = pa;
+        uint32_t cn = min((uint32_t)GCHUNK, lend - c0);
+        bool any_leaf = false;
+        for (;;) {
+            const uint32_t ng = cn / NBKD_GROUP;
+            // per lane: the groups of this chunk its ball reaches
+            uint32_t gm = 0;
+#pragma unroll 1
+            for (uint32_t g = 0; g < ng; ++g) {
+                const float tb[6] = {W.gb[6 * g], W.gb[6 * g + 1], W.gb[6 * g + 2],
+                                     W.gb[6 * g + 3], W.gb[6 * g + 4], W.gb[6 * g + 5]};
+                gm |= (box_lb2<M>(qx, qy, qz, tb, L) <= kth ? 1u : 0u) << g;
+            }
+            NBKD_PH(2);
+            if (__any(gm != 0)) {
+                any_leaf = true;
+                if constexpr (STATS) st[2] += cn;
+                // dense groups: every lane scans them for its own query
+                uint32_t sparse_g = 0;
+#pragma unroll 1
+                for (uint32_t g = 0; g < ng; ++g) {
+                    const uint64_t bal = __ballot((gm >> g) & 1u);
+                    if (bal == 0) continue;
+                    if ((int)__popcll(bal) < gdense) {
+                        sparse_g |= 1u << g;
+                        continue;
+                    }
+                    if constexpr (STATS) {
+                        st[3] += NBKD_GROUP;
+                        st[5] += 64 * NBKD_GROUP;
+                    }
+#pragma unroll 1
+                    for (uint32_t u0 = g * NBKD_GROUP; u0 < (g + 1) * NBKD_GROUP; u0 += G) {
+                        float dg[G];
+#pragma unroll
+                        for (int u = 0; u < G; u += 4) {
+                            const float4 xv = *reinterpret_cast<const float4 *>(&W.pb[0][u0 + u]);
+                            const float4 yv = *reinterpret_cast<const float4 *>(&W.pb[1][u0 + u]);
+                            const float4 zv = *reinterpret_cast<const float4 *>(&W.pb[2][u0 + u]);
+                            dg[u] = point_d2_fast<M>(qx, qy, qz, xv.x, yv.x, zv.x, L);
+                            dg[u + 1] = point_d2_fast<M>(qx, qy, qz, xv.y, yv.y, zv.y, L);
+                            dg[u + 2] = point_d2_fast<M>(qx, qy, qz, xv.z, yv.z, zv.z, L);
+                            dg[u + 3] = point_d2_fast<M>(qx, qy, qz, xv.w, yv.w, zv.w, L);
+                        }
+                        uint32_t hm = 0;
+#pragma unroll
+                        for (int u = 0; u < G; ++u) hm |= (dg[u] < kth ? 1u : 0u) << u;
+                        while (__any(hm != 0)) {
+                            if (hm != 0) {
+                                const uint32_t u = (uint32_t)__builtin_ctz(hm);
+                                hm &= hm - 1u;
+                                float d = dg[0];
+#pragma unroll
+                                for (int v = 1; v < G; ++v) d = u == (uint32_t)v ? dg[v] : d;
+                                const uint32_t j = d2_bucket(d, nb_over_s);
+                                atomicAdd(&W.hist[j >> 2][lane], 1u << (8 * (j & 3)));
+                                if (cnt < capg)
+                                    col[((cnt >> 4) * qpp + lane) * 16u + (cnt & 15u)] =
+                                        make_uint2(__float_as_uint(d), c0 + u0 + u);
+                                ++cnt;
+                            }
+                        }
+                    }
+                }
+                NBKD_PH(3);
+                const uint32_t sm = gm & sparse_g;
+                if (__any(sm != 0)) {
+                    // sparse groups: (lane, group) pairs compacted, each pair's 8
+                    // points spread over 8 consecutive lanes
+                    W.cnt[lane] = cnt;
+                    W.sq[lane] = make_float4(qx, qy, qz, kth);
+                    W.scl[lane] = nb_over_s;
+                    uint32_t np = 0;
+#pragma unroll 1
+                    for (uint32_t g = 0; g < ng; ++g) {
+                        if (!((sparse_g >> g) & 1u)) continue;
+                        const uint64_t bal = __ballot((sm >> g) & 1u);
+                        if ((sm >> g) & 1u) W.pairs[np + mbcnt64(bal)] = (uint16_t)(lane | (g << 6));
+                        np += (uint32_t)__popcll(bal);
+                    }
+                    wave_sync();
+                    const uint32_t ntrip = np * NBKD_GROUP;
+                    if constexpr (STATS) st[5] += ntrip;
+#pragma unroll 1
+                    for (uint32_t t0 = 0; t0 < ntrip; t0 += 64) {
+                        if constexpr (STATS) ++st[4];
+                        const uint32_t ti = t0 + lane;
+                        if (ti < ntrip) {
+                            const uint32_t pr = W.pairs[ti / NBKD_GROUP];
+                            const uint32_t owner = pr & 63u;
+                            const uint32_t pi = (pr >> 6) * NBKD_GROUP + (ti % NBKD_GROUP);
+                            const float4 qq = W.sq[owner];
+                            const float d = point_d2_fast<M>(qq.x, qq.y, qq.z, W.pb[0][pi],
+                                                             W.pb[1][pi], W.pb[2][pi], L);
+                            if (d < qq.w) {
+                                const uint32_t j = d2_bucket(d, W.scl[owner]);
+                                atomicAdd(&W.hist[j >> 2][owner], 1u << (8 * (j & 3)));
+                                const uint32_t sl = atomicAdd(&W.cnt[owner], 1u);
+                                if (sl < capg && !NBKD_EXP_NOSTORE)
+                                    col[((sl >> 4) * qpp + owner) * 16u + (sl & 15u)] =
+                                        make_uint2(__float_as_uint(d), c0 + pi);
+                            }
+                        }
+                    }
+                    wave_sync();
+                    cnt = W.cnt[lane];
+                }
+                NBKD_PH(4);
+            }
+            c0 += cn;
+            if (c0 >= lend) {
+                if constexpr (STATS) st[1] += any_leaf ? 1 : 0;
+                // tighten: smallest bucket edge with >= k candidates below it
+                const bool upd = cnt >= (uint32_t)kq && cnt != last_cnt;
+                if (__any(upd)) {
+                    wave_sync();
+                    if (upd) {
+                        last_cnt = cnt;
+                        const uint32_t p0 = W.hist[0][lane] * 0x01010101u;
+                        const uint32_t p1 = W.hist[1][lane] * 0x01010101u;
+                        const uint32_t p2 = W.hist[2][lane] * 0x01010101u;
+                        const uint32_t p3 = W.hist[3][lane] * 0x01010101u;
+                        const uint32_t c0w = p0 >> 24, c1w = c0w + (p1 >> 24), c2w = c1w + (p2 >> 24);
+                        const uint32_t kk = (uint32_t)kq;
+                        const uint32_t w = c0w >= kk ? 0u : c1w >= kk ? 1u : c2w >= kk ? 2u : 3u;
+                        const uint32_t base = w == 0 ? 0u : w == 1 ? c0w : w == 2 ? c1w : c2w;
+                        const uint32_t pw = w == 0 ? p0 : w == 1 ? p1 : w == 2 ? p2 : p3;
+                        const uint32_t need_k = kk - base;
+                        const uint32_t nb = (((pw & 0xFFu) < need_k) ? 1u : 0u) +
+                                            ((((pw >> 8) & 0xFFu) < need_k) ? 1u : 0u) +
+                                            ((((pw >> 16) & 0xFFu) < need_k) ? 1u : 0u) +
+                                            (((pw >> 24) < need_k) ? 1u : 0u);
+                        const uint32_t jstar = 4 * w + nb;
+                        if (jstar < (uint32_t)(NB - 1))
+                            kth = fminf(kth, (float)(jstar + 1) * s_over_nb);
+                    }
+                }
+                NBKD_PH(5);
+                break;
+            }
+            cn = min((uint32_t)GCHUNK, lend - c0);
+            wave_sync();
+            NBKD_COLLECT_STAGE_G(c0, lend);
+            wait_vm0();
+            wave_sync();
+        }
+        wave_sync();
+    }
+    NBKD_PH(0);
+#undef NBKD_PH
+}
+
+template <bool PER, int OCC, int G, bool STATS>
+__global__ void __launch_bounds__(TB, OCC)
+knn_collect_grp_kernel(DevTree t, const float *__restrict__ ginfo, const float *__restrict__ q,
+                       const uint32_t *__restrict__ order, uint32_t m, int kq,
+                       const float *__restrict__ tg, float seed_mul, uint32_t qpp, int gdense,
+                       uint2 *__restrict__ cand, uint32_t capg,
+                       uint32_t *__restrict__ ccount, unsigned long long *__restrict__ stats) {
+    __shared__ CollectLdsG Wl[WPB];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    CollectLdsG &W = Wl[wave];
+    const uint32_t pk = blockIdx.x * WPB + wave;
+    const uint32_t gq = pk * qpp + lane;
+    const bool valid = (uint32_t)lane < qpp && gq < m;
+    const uint32_t qo = valid ? order[gq] : 0u;
+    const float qx = valid ? q[3 * (size_t)qo] : 0.0f;
+    const float qy = valid ? q[3 * (size_t)qo + 1] : 0.0f;
+    const float qz = valid ? q[3 * (size_t)qo + 2] : 0.0f;
+    const float seed = valid ? fminf(tg[qo] * seed_mul, FLT_MAX) : -INFINITY;
+    const bool fin = seed < FLT_MAX && seed >= 1e-30f;
+    const float s_over_nb = fin ? seed * (1.0f / NB) : (seed > 0.0f ? INFINITY : 0.0f);
+    const float nb_over_s = fin ? (float)NB / seed * 1.00000095367431640625f : 0.0f;
+#pragma unroll
+    for (int w = 0; w < NB / 4; ++w) W.hist[w][lane] = 0u;
+    uint2 *const col = cand + (size_t)pk * qpp * capg;
+    uint32_t cnt = 0;
+    uint64_t st[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    grp_packet<PER, PER, G, STATS>(t, ginfo, W, lane, qx, qy, qz, seed, s_over_nb,
+                                               nb_over_s, col, qpp, capg, kq, gdense, cnt, st);
+    if (valid) ccount[gq] = cnt;
+    if (STATS && lane == 0) {
+        atomicAdd(&stats[0], (unsigned long long)st[0]);
+        atomicAdd(&stats[1], (unsigned long long)st[5]);
+        atomicAdd(&stats[2], (unsigned long long)st[3]);
+        atomicAdd(&stats[3], (unsigned long long)st[4]);
+        atomicAdd(&stats[4], (unsigned long long)st[2]);
+        atomicAdd(&stats[5], 1ull);
+        atomicAdd(&stats[7], (unsigned long long)st[1]);
+#pragma unroll
+        for (int i = 0; i < 6; ++i) atomicAdd(&stats[10 + i], (unsigned long long)st[6 + i]);
     }
     if (STATS) {
         uint32_t c = valid ? cnt : 0u;
@@ -552,11 +939,41 @@ int dense_min() {
     return e ? atoi(e) : 33;
 }
 
+bool groups_enabled() {
+    static const bool on = [] { // NBKD_GROUPS=0: leaf-level scan (A/B)
+        const char *e = getenv("NBKD_GROUPS");
+        return !(e && atoi(e) == 0);
+    }();
+    return on;
+}
+
+int group_dense_min() {
+    static const int v = [] { // lanes needing a group before every lane scans it
+        const char *e = getenv("NBKD_GDENSE");
+        return e ? atoi(e) : 65; // > 64: never (all sparse measured fastest, r02i)
+    }();
+    return v;
+}
+
 template <bool PER>
 void launch_collect(const Tree &t, const float *q, const uint32_t *order, uint32_t m, int k,
                     const float *tg, float seed_mul, uint32_t qpp, uint2 *cand, uint32_t capg,
-                    uint32_t *ccount, unsigned long long *stats, hipStream_t s) {
+                    uint32_t *ccount, unsigned long long *stats, bool retry, hipStream_t s) {
+    const char *const name = retry ? "knn_retry" : "knn_collect";
     const unsigned blocks = (unsigned)(((uint64_t)m + qpp - 1) / qpp + WPB - 1) / WPB;
+    if (t.ginfo && groups_enabled()) {
+        const int gd = group_dense_min();
+        TimedScope ts(name, s);
+        if (stats)
+            knn_collect_grp_kernel<PER, 8, 4, true><<<blocks, TB, 0, s>>>(
+                view(t), t.ginfo, q, order, m, k, tg, seed_mul, qpp, gd, cand, capg, ccount, stats);
+        else
+            knn_collect_grp_kernel<PER, 8, 4, false><<<blocks, TB, 0, s>>>(
+                view(t), t.ginfo, q, order, m, k, tg, seed_mul, qpp, gd, cand, capg, ccount,
+                nullptr);
+        return;
+    }
+    TimedScope ts(name, s);
     const int dm = dense_min();
     const char *eo = getenv("NBKD_COLLECT_OCC"); // tuning experiments only
     const int occ = eo ? atoi(eo) : 8;
@@ -643,14 +1060,13 @@ nbkd_status launch_knn_collect(const Tree &t, const float *q, const uint32_t *or
                                bool retry, bool fix_seed, unsigned long long *stats,
                                hipStream_t s) {
     if (m == 0) return NBKD_OK;
-    {
-        TimedScope ts(retry ? "knn_retry" : "knn_collect", s);
-        if (t.periodic)
-            launch_collect<true>(t, q, order, m, k, tg, seed_mul, qpp, cand, capg, ccount, stats, s);
-        else
-            launch_collect<false>(t, q, order, m, k, tg, seed_mul, qpp, cand, capg, ccount, stats, s);
-        NBKD_HIP(hipGetLastError());
-    }
+    if (t.periodic)
+        launch_collect<true>(t, q, order, m, k, tg, seed_mul, qpp, cand, capg, ccount, stats,
+                             retry, s);
+    else
+        launch_collect<false>(t, q, order, m, k, tg, seed_mul, qpp, cand, capg, ccount, stats,
+                              retry, s);
+    NBKD_HIP(hipGetLastError());
     {
         TimedScope ts(retry ? "knn_retry" : "knn_select", s);
         // a retry round follows: failures rewrite their seed for it
