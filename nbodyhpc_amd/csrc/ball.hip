@@ -10,6 +10,13 @@
 // f32 d2 over the box <= r2) counts the leaf's points without evaluating them;
 // the others evaluate the points staged in LDS.
 //
+// Tried and dropped: the kNN collect's 8-point groups here (whole groups
+// counted, partial (lane, group) pairs compacted 8 lanes per pair): the same
+// counts, but 161 ms against 139 ms at leafsize 64 (198 vs 163 at 32, r02n).
+// The per-lane group box tests (lower and upper bound, 8 per chunk) and the
+// compacted pairs cost more than the ~45 % of evaluations they save against
+// the transposed count below.
+//
 // Periodic queries outside [0, L]^3 are excluded here (their minimum-image
 // pruning is not a bound) and answered by ball_brute_kernel below.
 #include "internal.hpp"

@@ -19,6 +19,7 @@ def main():
     ap.add_argument("--r", type=float, default=0.01)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--lognormal", action="store_true")
+    ap.add_argument("--leaf", type=int, default=32)
     a = ap.parse_args()
     hip.preload()
     hip.set_device(0)
@@ -27,7 +28,7 @@ def main():
     s = hip.Stream()
     d = hip.DeviceArray.from_numpy(pts)
     del pts
-    t = capi.Tree(n=n, dev_ptr=d.ptr, leafsize=32, boxsize=1.0, stream=s.handle)
+    t = capi.Tree(n=n, dev_ptr=d.ptr, leafsize=a.leaf, boxsize=1.0, stream=s.handle)
     c = hip.DeviceArray((n,), np.uint32)
     t.ball_count_device(d.ptr, n, a.r, c.ptr, s.handle)
     hip.synchronize()
@@ -37,7 +38,8 @@ def main():
     hip.synchronize()
     ms = (time.perf_counter() - t0) / a.steps * 1e3
     h = c.numpy()
-    print(f"BALL_T={os.environ.get('NBKD_BALL_T', 'default')} n={n:.0e} "
+    knobs = " ".join(f"{k}={v}" for k, v in sorted(os.environ.items()) if k.startswith("NBKD_"))
+    print(f"[{knobs or 'defaults'}] leaf={a.leaf} n={n:.0e} "
           f"lognormal={a.lognormal} ms={ms:.2f} q/s={n / ms * 1e3:.3e} mean={h.mean():.3f} "
           f"sha={hashlib.sha256(h.tobytes()).hexdigest()[:16]}", flush=True)
 
