@@ -454,6 +454,45 @@ struct CollectLdsG {
         glds_f32(ginfo + 6 * (size_t)((LPOS) / NBKD_GROUP), W.gb, lane, 6 * (cn_ / NBKD_GROUP));   \
     } while (0)
 
+// one internal node with split axis D (compile-time): test both children for
+// every lane, push the far one when both are wanted, step into the near one
+// (the walk branches on the node's axis, so no per-lane selects pick the axis)
+#define NBKD_GSTEP(D)                                                                              \
+    {                                                                                              \
+        const float split = nd.split;                                                              \
+        const float qd = (D) == 0 ? qx : ((D) == 1 ? qy : qz);                                     \
+        const float tl = box_lb_axis<M>(qd, bx[2 * (D)], split, L);                                \
+        const float tr = box_lb_axis<M>(qd, split, bx[2 * (D) + 1], L);                            \
+        const float dl = (((D) == 0 ? tl : tm[0]) + ((D) == 1 ? tl : tm[1])) + ((D) == 2 ? tl : tm[2]); \
+        const float dr = (((D) == 0 ? tr : tm[0]) + ((D) == 1 ? tr : tm[1])) + ((D) == 2 ? tr : tm[2]); \
+        const uint64_t wl = __ballot(dl <= kth), wr = __ballot(dr <= kth);                         \
+        const uint32_t right_votes = (uint32_t)__popcll(wm & __ballot(qd > split));                \
+        const bool right_first = 2 * right_votes > (uint32_t)__popcll(wm);                         \
+        const uint64_t wn = right_first ? wr : wl, wf = right_first ? wl : wr;                     \
+        if (wn != 0 && wf != 0) {                                                                  \
+            /* far = left child [lo, split] if right_first, else right child [split, hi] */        \
+            const bool me = lane == sp;                                                            \
+            sk_node = me ? (right_first ? nd.left : nd.right) : sk_node;                           \
+            _Pragma("unroll") for (int a = 0; a < 6; ++a) {                                        \
+                const bool is_split = right_first ? a == 2 * (D) + 1 : a == 2 * (D);               \
+                sk_b[a] = me ? unif(is_split ? split : bx[a]) : sk_b[a];                           \
+            }                                                                                      \
+            ++sp;                                                                                  \
+        }                                                                                          \
+        if (wn == 0 && wf == 0) continue;                                                          \
+        const bool go_near = wn != 0;                                                              \
+        const bool go_right = go_near == right_first;                                              \
+        node = go_right ? nd.right : nd.left;                                                      \
+        nd = cnodes[node];                                                                         \
+        tm[D] = go_right ? tr : tl;                                                                \
+        if (go_right)                                                                              \
+            bx[2 * (D)] = unif(split);                                                             \
+        else                                                                                       \
+            bx[2 * (D) + 1] = unif(split);                                                         \
+        wm = go_near ? wn : wf;                                                                    \
+        have = true;                                                                               \
+    }
+
 // one internal node (record nd): test both children for every lane, push the
 // far one when both are wanted, step into the near one.  (Tried and dropped:
 // loading both children's records on entry, consumed after the tests, to take
@@ -525,7 +564,12 @@ struct CollectLdsG {
             FOUND = true;                                                                          \
             break;                                                                                 \
         }                                                                                          \
-        NBKD_GSTEP_ANY                                                                             \
+        if (nd.dimension == 0)                                                                     \
+            NBKD_GSTEP(0)                                                                          \
+        else if (nd.dimension == 1)                                                                \
+            NBKD_GSTEP(1)                                                                          \
+        else                                                                                       \
+            NBKD_GSTEP(2)                                                                          \
     }
 
 // st: node visits, leaves scanned, points staged, dense points, sparse

@@ -23,18 +23,20 @@ ap.add_argument("--n", type=float, default=1e6)
 ap.add_argument("--queries", type=int, default=2000)
 ap.add_argument("--k", type=int, default=32)
 ap.add_argument("--slack", type=float, default=1.15)
+ap.add_argument("--group", type=int, default=8)
 a = ap.parse_args()
 n, L = int(a.n), 1.0
+GSIZE = a.group
 pts = synth.uniform(n)
 orc = Oracle()
 
 
-def groups_of(q, size=8):
+def groups_of(q, size=GSIZE):
     if len(q) <= size:
         return [q]
     ax = np.argmax(q.max(0) - q.min(0))
     q = q[np.argsort(q[:, ax], kind="stable")]
-    h = (len(q) // 2) // size * size
+    h = (len(q) // 2) // 8 * 8
     return groups_of(q[:h], size) + groups_of(q[h:], size)
 
 
