@@ -653,6 +653,7 @@ def main():
         "traversal_per_packet": {kk: st[kk] / max(st["packets"], 1)
                                  for kk in ("node_visits", "dense_steps", "sparse_iters",
                                             "points_staged", "candidates", "leaves_scanned")},
+        "lanes_per_scanned_chunk": st["chunk_lanes"] / max(st["leaves_scanned"], 1),
         "fallback_queries": st["fallback_queries"], "retry_queries": st["retry_queries"],
         # where a collect wave's cycles go (work-counter pass, s_memtime clocks)
         "collect_phase_frac": _phase_frac(st),

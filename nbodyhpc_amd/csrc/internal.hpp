@@ -107,7 +107,7 @@ struct TimedScope {
 };
 bool timing_enabled();
 bool stats_enabled();
-constexpr int NBKD_NSTATS = 16; // see capi.STATS_NAMES (collect kernel) + exact-kernel and retried queries
+constexpr int NBKD_NSTATS = 17; // see capi.STATS_NAMES (collect kernel) + exact-kernel and retried queries
 void stats_store(const uint64_t *v);
 
 // RAII device allocation (plain hipMalloc; freed after the stream drained).

@@ -414,14 +414,19 @@ knn_collect_kernel(DevTree t, const uint32_t *__restrict__ linfo, const float *_
 
 // ---------------------------------------------------------------- group variant
 // The same packet walk over a tree whose leaves are cut into 8-point groups
-// with their own tight boxes (build.hip group_kernel).  At a leaf each lane
-// tests every group of the staged chunk (up to 64 points, 8 groups): the
-// (lane, group) pairs replace the leaf-level need test, so a query evaluates
-// only the points of groups its ball reaches (about half of the leaf-level
-// count at leafsize 32, a third at 64: tests/tools/knn_group_estimate.py).
-// Groups that at least `gdense` lanes need are scanned by every lane (dense);
-// the other pairs are compacted, 8 (pair, point) evaluations per pair, onto
-// the 64 lanes (sparse).
+// with their own tight boxes (build.hip group_kernel).  At a leaf the lanes
+// whose ball reaches the leaf's tight box (~12 of 64 at 1e8) are compacted;
+// their (lane, group) box tests run 8 lanes per needing lane over the staged
+// chunk (up to 64 points, 8 groups), and the groups reached form a pair list:
+// a query evaluates only the points of groups its ball reaches (about half of
+// the leaf-level count at leafsize 32, a third at 64:
+// tests/tools/knn_group_estimate.py), each pair's 8 (pair, point) evaluations
+// on 8 consecutive lanes.
+//
+// Tried and dropped: scanning groups that >= 20..44 lanes need with every
+// lane (dense) instead (r02i: all-compacted was fastest); the per-lane test
+// of every group before the compaction (r02s: 8 tests per lane where only
+// ~12 lanes need the leaf).
 //
 // Tried and dropped: running packets whose balls clear the box faces with the
 // non-periodic formulas (4 % fewer VALU instructions).  One kernel holding
@@ -429,9 +434,6 @@ knn_collect_kernel(DevTree t, const uint32_t *__restrict__ linfo, const float *_
 // wrap packets (~4 %) as a latency-bound tail (+10.9 ms at 1e8), or, on a side
 // stream beside the main launch, still cost +5 ms (r02f/r02g).
 //
-#ifndef NBKD_EXP_NOSTORE
-#define NBKD_EXP_NOSTORE 0
-#endif
 constexpr int GCHUNK = 64; // points staged per step (a multiple of NBKD_GROUP)
 constexpr int GMAX = GCHUNK / NBKD_GROUP;
 
@@ -442,7 +444,9 @@ struct CollectLdsG {
     uint32_t hist[NB / 4][64];
     float pb[3][GCHUNK];
     float gb[6 * GMAX];          // the chunk's group boxes (lo.x, hi.x, lo.y, hi.y, lo.z, hi.z)
-    uint16_t pairs[64 * GMAX];   // sparse (lane, group) pairs: lane | group << 6
+    float tb[8];                 // the leaf's tight box (leafinfo words 0..5)
+    uint16_t pairs[64 * GMAX];   // (lane, group) pairs: lane | group << 6
+    uint8_t slot[64];            // lanes needing the leaf, compacted
 };
 
 #define NBKD_COLLECT_STAGE_G(LPOS, LEND)                                                           \
@@ -452,6 +456,7 @@ struct CollectLdsG {
         glds_f32(t.y + (LPOS), W.pb[1], lane, cn_);                                                \
         glds_f32(t.z + (LPOS), W.pb[2], lane, cn_);                                                \
         glds_f32(ginfo + 6 * (size_t)((LPOS) / NBKD_GROUP), W.gb, lane, 6 * (cn_ / NBKD_GROUP));   \
+        glds_f32(reinterpret_cast<const float *>(linfo) + 8 * (size_t)node, W.tb, lane, 6);       \
     } while (0)
 
 // one internal node with split axis D (compile-time): test both children for
@@ -573,15 +578,17 @@ struct CollectLdsG {
     }
 
 // st: node visits, leaves scanned, points staged, dense points, sparse
-// iterations, pair evaluations, then 6 phase clocks (STATS only)
-template <bool PER, bool M, int G, bool STATS>
+// iterations, pair evaluations, then 6 phase clocks, then lanes needing a
+// staged chunk summed over chunks (STATS only)
+template <bool PER, bool M, bool STATS>
 __device__ __forceinline__ void grp_packet(const DevTree &t, const float *__restrict__ ginfo,
+                                           const uint32_t *__restrict__ linfo,
                                            CollectLdsG &W, const int lane, const float qx,
                                            const float qy, const float qz, float kth,
                                            const float s_over_nb, const float nb_over_s,
                                            uint2 *__restrict__ col, const uint32_t qpp,
-                                           const uint32_t capg, const int kq, const int gdense,
-                                           uint32_t &cnt, uint64_t (&st)[12]) {
+                                           const uint32_t capg, const int kq, uint32_t &cnt,
+                                           uint64_t (&st)[13]) {
     const float L = t.box;
     uint32_t last_cnt = 0;
     uint32_t sk_node = 0;
@@ -625,108 +632,72 @@ __device__ __forceinline__ void grp_packet(const DevTree &t, const float *__rest
         bool any_leaf = false;
         for (;;) {
             const uint32_t ng = cn / NBKD_GROUP;
-            // per lane: the groups of this chunk its ball reaches
-            uint32_t gm = 0;
-#pragma unroll 1
-            for (uint32_t g = 0; g < ng; ++g) {
-                const float tb[6] = {W.gb[6 * g], W.gb[6 * g + 1], W.gb[6 * g + 2],
-                                     W.gb[6 * g + 3], W.gb[6 * g + 4], W.gb[6 * g + 5]};
-                gm |= (box_lb2<M>(qx, qy, qz, tb, L) <= kth ? 1u : 0u) << g;
-            }
-            NBKD_PH(2);
-            if (__any(gm != 0)) {
+            // the lanes whose ball reaches the leaf's tight box (leafinfo);
+            // ~12 of 64 on average at 1e8, so the group tests run compacted
+            const float tb[6] = {W.tb[0], W.tb[3], W.tb[1], W.tb[4], W.tb[2], W.tb[5]};
+            const bool need = box_lb2<M>(qx, qy, qz, tb, L) <= kth;
+            const uint64_t nm = __ballot(need);
+            if (nm != 0) {
                 any_leaf = true;
-                if constexpr (STATS) st[2] += cn;
-                // dense groups: every lane scans them for its own query
-                uint32_t sparse_g = 0;
+                const uint32_t nneed = (uint32_t)__popcll(nm);
+                if constexpr (STATS) {
+                    st[2] += cn;
+                    st[12] += nneed;
+                }
+                W.cnt[lane] = cnt;
+                W.sq[lane] = make_float4(qx, qy, qz, kth);
+                W.scl[lane] = nb_over_s;
+                if (need) W.slot[mbcnt64(nm)] = (uint8_t)lane;
+                wave_sync();
+                // (needing lane, group) box tests, 8 lanes per needing lane (one
+                // per group); the groups reached become the pair list
+                uint32_t np = 0;
+                const uint32_t ntest = nneed * GMAX;
 #pragma unroll 1
-                for (uint32_t g = 0; g < ng; ++g) {
-                    const uint64_t bal = __ballot((gm >> g) & 1u);
-                    if (bal == 0) continue;
-                    if ((int)__popcll(bal) < gdense) {
-                        sparse_g |= 1u << g;
-                        continue;
+                for (uint32_t t0 = 0; t0 < ntest; t0 += 64) {
+                    const uint32_t ti = t0 + lane;
+                    const uint32_t g = ti % GMAX;
+                    uint32_t owner = 0;
+                    bool hit = false;
+                    if (ti < ntest && g < ng) {
+                        owner = W.slot[ti / GMAX];
+                        const float4 qq = W.sq[owner];
+                        const float gbx[6] = {W.gb[6 * g], W.gb[6 * g + 1], W.gb[6 * g + 2],
+                                              W.gb[6 * g + 3], W.gb[6 * g + 4], W.gb[6 * g + 5]};
+                        hit = box_lb2<M>(qq.x, qq.y, qq.z, gbx, L) <= qq.w;
                     }
-                    if constexpr (STATS) {
-                        st[3] += NBKD_GROUP;
-                        st[5] += 64 * NBKD_GROUP;
-                    }
+                    const uint64_t hm = __ballot(hit);
+                    if (hit) W.pairs[np + mbcnt64(hm)] = (uint16_t)(owner | (g << 6));
+                    np += (uint32_t)__popcll(hm);
+                }
+                NBKD_PH(2);
+                wave_sync();
+                // each pair's 8 points spread over 8 consecutive lanes
+                const uint32_t ntrip = np * NBKD_GROUP;
+                if constexpr (STATS) st[5] += ntrip;
 #pragma unroll 1
-                    for (uint32_t u0 = g * NBKD_GROUP; u0 < (g + 1) * NBKD_GROUP; u0 += G) {
-                        float dg[G];
-#pragma unroll
-                        for (int u = 0; u < G; u += 4) {
-                            const float4 xv = *reinterpret_cast<const float4 *>(&W.pb[0][u0 + u]);
-                            const float4 yv = *reinterpret_cast<const float4 *>(&W.pb[1][u0 + u]);
-                            const float4 zv = *reinterpret_cast<const float4 *>(&W.pb[2][u0 + u]);
-                            dg[u] = point_d2_fast<M>(qx, qy, qz, xv.x, yv.x, zv.x, L);
-                            dg[u + 1] = point_d2_fast<M>(qx, qy, qz, xv.y, yv.y, zv.y, L);
-                            dg[u + 2] = point_d2_fast<M>(qx, qy, qz, xv.z, yv.z, zv.z, L);
-                            dg[u + 3] = point_d2_fast<M>(qx, qy, qz, xv.w, yv.w, zv.w, L);
-                        }
-                        uint32_t hm = 0;
-#pragma unroll
-                        for (int u = 0; u < G; ++u) hm |= (dg[u] < kth ? 1u : 0u) << u;
-                        while (__any(hm != 0)) {
-                            if (hm != 0) {
-                                const uint32_t u = (uint32_t)__builtin_ctz(hm);
-                                hm &= hm - 1u;
-                                float d = dg[0];
-#pragma unroll
-                                for (int v = 1; v < G; ++v) d = u == (uint32_t)v ? dg[v] : d;
-                                const uint32_t j = d2_bucket(d, nb_over_s);
-                                atomicAdd(&W.hist[j >> 2][lane], 1u << (8 * (j & 3)));
-                                if (cnt < capg)
-                                    col[((cnt >> 4) * qpp + lane) * 16u + (cnt & 15u)] =
-                                        make_uint2(__float_as_uint(d), c0 + u0 + u);
-                                ++cnt;
-                            }
+                for (uint32_t t0 = 0; t0 < ntrip; t0 += 64) {
+                    if constexpr (STATS) ++st[4];
+                    const uint32_t ti = t0 + lane;
+                    if (ti < ntrip) {
+                        const uint32_t pr = W.pairs[ti / NBKD_GROUP];
+                        const uint32_t owner = pr & 63u;
+                        const uint32_t pi = (pr >> 6) * NBKD_GROUP + (ti % NBKD_GROUP);
+                        const float4 qq = W.sq[owner];
+                        const float d = point_d2_fast<M>(qq.x, qq.y, qq.z, W.pb[0][pi],
+                                                         W.pb[1][pi], W.pb[2][pi], L);
+                        if (d < qq.w) {
+                            const uint32_t j = d2_bucket(d, W.scl[owner]);
+                            atomicAdd(&W.hist[j >> 2][owner], 1u << (8 * (j & 3)));
+                            const uint32_t sl = atomicAdd(&W.cnt[owner], 1u);
+                            if (sl < capg)
+                                col[((sl >> 4) * qpp + owner) * 16u + (sl & 15u)] =
+                                    make_uint2(__float_as_uint(d), c0 + pi);
                         }
                     }
                 }
-                NBKD_PH(3);
-                const uint32_t sm = gm & sparse_g;
-                if (__any(sm != 0)) {
-                    // sparse groups: (lane, group) pairs compacted, each pair's 8
-                    // points spread over 8 consecutive lanes
-                    W.cnt[lane] = cnt;
-                    W.sq[lane] = make_float4(qx, qy, qz, kth);
-                    W.scl[lane] = nb_over_s;
-                    uint32_t np = 0;
-#pragma unroll 1
-                    for (uint32_t g = 0; g < ng; ++g) {
-                        if (!((sparse_g >> g) & 1u)) continue;
-                        const uint64_t bal = __ballot((sm >> g) & 1u);
-                        if ((sm >> g) & 1u) W.pairs[np + mbcnt64(bal)] = (uint16_t)(lane | (g << 6));
-                        np += (uint32_t)__popcll(bal);
-                    }
-                    wave_sync();
-                    const uint32_t ntrip = np * NBKD_GROUP;
-                    if constexpr (STATS) st[5] += ntrip;
-#pragma unroll 1
-                    for (uint32_t t0 = 0; t0 < ntrip; t0 += 64) {
-                        if constexpr (STATS) ++st[4];
-                        const uint32_t ti = t0 + lane;
-                        if (ti < ntrip) {
-                            const uint32_t pr = W.pairs[ti / NBKD_GROUP];
-                            const uint32_t owner = pr & 63u;
-                            const uint32_t pi = (pr >> 6) * NBKD_GROUP + (ti % NBKD_GROUP);
-                            const float4 qq = W.sq[owner];
-                            const float d = point_d2_fast<M>(qq.x, qq.y, qq.z, W.pb[0][pi],
-                                                             W.pb[1][pi], W.pb[2][pi], L);
-                            if (d < qq.w) {
-                                const uint32_t j = d2_bucket(d, W.scl[owner]);
-                                atomicAdd(&W.hist[j >> 2][owner], 1u << (8 * (j & 3)));
-                                const uint32_t sl = atomicAdd(&W.cnt[owner], 1u);
-                                if (sl < capg && !NBKD_EXP_NOSTORE)
-                                    col[((sl >> 4) * qpp + owner) * 16u + (sl & 15u)] =
-                                        make_uint2(__float_as_uint(d), c0 + pi);
-                            }
-                        }
-                    }
-                    wave_sync();
-                    cnt = W.cnt[lane];
-                }
+                wave_sync();
+                cnt = W.cnt[lane];
                 NBKD_PH(4);
             }
             c0 += cn;
@@ -772,11 +743,12 @@ __device__ __forceinline__ void grp_packet(const DevTree &t, const float *__rest
 #undef NBKD_PH
 }
 
-template <bool PER, int OCC, int G, bool STATS>
+template <bool PER, int OCC, bool STATS>
 __global__ void __launch_bounds__(TB, OCC)
-knn_collect_grp_kernel(DevTree t, const float *__restrict__ ginfo, const float *__restrict__ q,
+knn_collect_grp_kernel(DevTree t, const float *__restrict__ ginfo,
+                       const uint32_t *__restrict__ linfo, const float *__restrict__ q,
                        const uint32_t *__restrict__ order, uint32_t m, int kq,
-                       const float *__restrict__ tg, float seed_mul, uint32_t qpp, int gdense,
+                       const float *__restrict__ tg, float seed_mul, uint32_t qpp,
                        uint2 *__restrict__ cand, uint32_t capg,
                        uint32_t *__restrict__ ccount, unsigned long long *__restrict__ stats) {
     __shared__ CollectLdsG Wl[WPB];
@@ -797,9 +769,9 @@ knn_collect_grp_kernel(DevTree t, const float *__restrict__ ginfo, const float *
     for (int w = 0; w < NB / 4; ++w) W.hist[w][lane] = 0u;
     uint2 *const col = cand + (size_t)pk * qpp * capg;
     uint32_t cnt = 0;
-    uint64_t st[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-    grp_packet<PER, PER, G, STATS>(t, ginfo, W, lane, qx, qy, qz, seed, s_over_nb,
-                                               nb_over_s, col, qpp, capg, kq, gdense, cnt, st);
+    uint64_t st[13] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    grp_packet<PER, PER, STATS>(t, ginfo, linfo, W, lane, qx, qy, qz, seed, s_over_nb, nb_over_s,
+                                col, qpp, capg, kq, cnt, st);
     if (valid) ccount[gq] = cnt;
     if (STATS && lane == 0) {
         atomicAdd(&stats[0], (unsigned long long)st[0]);
@@ -811,6 +783,7 @@ knn_collect_grp_kernel(DevTree t, const float *__restrict__ ginfo, const float *
         atomicAdd(&stats[7], (unsigned long long)st[1]);
 #pragma unroll
         for (int i = 0; i < 6; ++i) atomicAdd(&stats[10 + i], (unsigned long long)st[6 + i]);
+        atomicAdd(&stats[16], (unsigned long long)st[12]);
     }
     if (STATS) {
         uint32_t c = valid ? cnt : 0u;
@@ -991,14 +964,6 @@ bool groups_enabled() {
     return on;
 }
 
-int group_dense_min() {
-    static const int v = [] { // lanes needing a group before every lane scans it
-        const char *e = getenv("NBKD_GDENSE");
-        return e ? atoi(e) : 65; // > 64: never (all sparse measured fastest, r02i)
-    }();
-    return v;
-}
-
 template <bool PER>
 void launch_collect(const Tree &t, const float *q, const uint32_t *order, uint32_t m, int k,
                     const float *tg, float seed_mul, uint32_t qpp, uint2 *cand, uint32_t capg,
@@ -1006,15 +971,15 @@ void launch_collect(const Tree &t, const float *q, const uint32_t *order, uint32
     const char *const name = retry ? "knn_retry" : "knn_collect";
     const unsigned blocks = (unsigned)(((uint64_t)m + qpp - 1) / qpp + WPB - 1) / WPB;
     if (t.ginfo && groups_enabled()) {
-        const int gd = group_dense_min();
         TimedScope ts(name, s);
         if (stats)
-            knn_collect_grp_kernel<PER, 8, 4, true><<<blocks, TB, 0, s>>>(
-                view(t), t.ginfo, q, order, m, k, tg, seed_mul, qpp, gd, cand, capg, ccount, stats);
+            knn_collect_grp_kernel<PER, 8, true><<<blocks, TB, 0, s>>>(
+                view(t), t.ginfo, t.leafinfo, q, order, m, k, tg, seed_mul, qpp, cand, capg,
+                ccount, stats);
         else
-            knn_collect_grp_kernel<PER, 8, 4, false><<<blocks, TB, 0, s>>>(
-                view(t), t.ginfo, q, order, m, k, tg, seed_mul, qpp, gd, cand, capg, ccount,
-                nullptr);
+            knn_collect_grp_kernel<PER, 8, false><<<blocks, TB, 0, s>>>(
+                view(t), t.ginfo, t.leafinfo, q, order, m, k, tg, seed_mul, qpp, cand, capg,
+                ccount, nullptr);
         return;
     }
     TimedScope ts(name, s);
