@@ -459,6 +459,19 @@ struct CollectLdsG {
         glds_f32(reinterpret_cast<const float *>(linfo) + 8 * (size_t)node, W.tb, lane, 6);       \
     } while (0)
 
+// v = lanes in `mask` ? val : old, as one v_cndmask (a select of a uniform
+// value into one lane otherwise compiles to exec-masked branches)
+__device__ __forceinline__ float lane_set(float old, float val, uint64_t mask) {
+    float r;
+    asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(old), "v"(val), "s"(mask));
+    return r;
+}
+__device__ __forceinline__ uint32_t lane_set(uint32_t old, uint32_t val, uint64_t mask) {
+    uint32_t r;
+    asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(old), "v"(val), "s"(mask));
+    return r;
+}
+
 // one internal node with split axis D (compile-time): test both children for
 // every lane, push the far one when both are wanted, step into the near one
 // (the walk branches on the node's axis, so no per-lane selects pick the axis)
@@ -474,15 +487,17 @@ struct CollectLdsG {
         const uint32_t right_votes = (uint32_t)__popcll(wm & __ballot(qd > split));                \
         const bool right_first = 2 * right_votes > (uint32_t)__popcll(wm);                         \
         const uint64_t wn = right_first ? wr : wl, wf = right_first ? wl : wr;                     \
-        if (wn != 0 && wf != 0) {                                                                  \
-            /* far = left child [lo, split] if right_first, else right child [split, hi] */        \
-            const bool me = lane == sp;                                                            \
-            sk_node = me ? (right_first ? nd.left : nd.right) : sk_node;                           \
+        {                                                                                          \
+            /* push the far child when both are wanted: far = left child [lo, split] if          \
+               right_first, else right child [split, hi]; one v_cndmask per word */                \
+            const bool push = wn != 0 && wf != 0;                                                  \
+            const uint64_t pmask = push ? (1ull << sp) : 0ull;                                     \
+            sk_node = lane_set(sk_node, right_first ? nd.left : nd.right, pmask);                  \
             _Pragma("unroll") for (int a = 0; a < 6; ++a) {                                        \
                 const bool is_split = right_first ? a == 2 * (D) + 1 : a == 2 * (D);               \
-                sk_b[a] = me ? unif(is_split ? split : bx[a]) : sk_b[a];                           \
+                sk_b[a] = lane_set(sk_b[a], is_split ? split : bx[a], pmask);                      \
             }                                                                                      \
-            ++sp;                                                                                  \
+            sp += push ? 1 : 0;                                                                    \
         }                                                                                          \
         if (wn == 0 && wf == 0) continue;                                                          \
         const bool go_near = wn != 0;                                                              \
