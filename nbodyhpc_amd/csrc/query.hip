@@ -763,8 +763,12 @@ SeedParams seed_params(const Tree &t, int k) {
     p.on = a > 0.0f;
     const float mu = (float)k + a * sqrtf((float)k) + a;
     p.mu_c = mu / (4.0f / 3.0f * 3.14159265f);
-    const char *ea = getenv("NBKD_KNN_ANCHOR"); // tuning only: anchor subtree in leaves
-    p.anchor = (uint32_t)t.leaf * (ea ? (uint32_t)std::max(1, atoi(ea)) : 4u);
+    // the density comes from the first subtree of <= anchor points on the
+    // descent: 128 points, or the leaf when leaves are larger (at leafsize 64
+    // the former 4-leaf anchor, 256 points, smoothed clustered densities too
+    // much: log-normal 1e8 retried 5.7 M queries)
+    const char *ea = getenv("NBKD_KNN_ANCHOR"); // tuning only: anchor in points
+    p.anchor = std::max<uint32_t>((uint32_t)t.leaf, ea ? (uint32_t)std::max(1, atoi(ea)) : 128u);
     return p;
 }
 

@@ -349,3 +349,48 @@ def test_save_load_and_pickle(gpu, tmp_path, box):
         d, i = t2.query(q, k=8)
         assert np.array_equal(d, d0)
         assert_knn_equal(d, i, d0, i0, pts, q, box)
+
+
+# ---------------------------------------------------------------- sub-leaf groups
+def _lattice(m):
+    g = np.arange(m, dtype=np.float32) / m
+    return np.stack(np.meshgrid(g, g, g, indexing="ij"), -1).reshape(-1, 3)
+
+
+@pytest.mark.parametrize("case", ["lattice64", "dups128", "lognormal64", "uniform64_self",
+                                  "uniform128", "pad64"])
+def test_group_leaves_vs_oracle(gpu, oracle, case):
+    """The collect kernel's 8-point groups (build.hip group_kernel reorders
+    each leaf; knn_collect.hip tests group boxes) at the bench's leafsize 64 and
+    the reference wrapper's 128: exact ties inside a group (lattice, duplicated
+    points), clustered groups, padding rows in the last leaf, and self-queries
+    of every point of a 2e5 set (the bench's workload, smaller)."""
+    from nbodyhpc_amd import synth
+    rng = np.random.Generator(np.random.PCG64(77))
+    if case == "lattice64":
+        pts, leaf, box, k = _lattice(32), 64, 1.0, 16
+        q = pts[::11] + np.float32(0.003)
+    elif case == "dups128":
+        base = uniform(3000, 5)
+        pts, leaf, box, k = np.concatenate([base] * 4), 128, None, 9
+        q = np.concatenate([base[:400], uniform(400, 6)])
+    elif case == "lognormal64":
+        pts, leaf, box, k = synth.lognormal(200_000, grid=64), 64, 1.0, 32
+        q = np.concatenate([pts[::50], rng.uniform(0, 1, (1000, 3)).astype(np.float32)])
+    elif case == "uniform64_self":
+        pts, leaf, box, k = uniform(200_000, 12), 64, 1.0, 32
+        q = pts
+    elif case == "uniform128":
+        pts, leaf, box, k = uniform(150_000, 13), 128, 1.0, 64
+        q = rng.uniform(0, 1, (4000, 3)).astype(np.float32)
+    else:  # n % 8 != 0: FLT_MAX padding rows share the last leaf's groups
+        pts, leaf, box, k = uniform(70_005, 14), 64, None, 24
+        q = np.concatenate([pts[-300:], uniform(300, 15)])
+    t = gpu.Tree(pts, leafsize=leaf, boxsize=box)
+    o = oracle.tree(pts, leaf, box)
+    gn, _, _, _, gi = t.export()
+    on, _, _, _, oi = o.export()
+    assert leaf_sets(gn, gi) == leaf_sets(on, oi)
+    d, i = t.query(q, k)
+    dr, ir = o.query(q, k, workers=8)
+    assert_knn_equal(d, i, dr, ir, pts, q, box)
