@@ -84,6 +84,9 @@ def parse():
     p.add_argument("--input", default=None,
                    help="raw float32 (N, 3) particle file (reference main.cpp -f format) "
                         "instead of the synthetic set; N > 1 streams each rank's slab")
+    p.add_argument("--input-format", choices=("raw", "gadget"), default="raw",
+                   help="gadget: a Gadget-2 snapshot (format 1/2, multi-file); the box is "
+                        "its BoxSize; N > 1 needs --redistribute")
     return p.parse_args()
 
 
@@ -437,12 +440,22 @@ def main():
 
     n = int(args.n)
     k, L = args.k, args.box
+    gadget = None
+    if args.input and args.input_format == "gadget":
+        from nbodyhpc_amd import io as nio
+        gadget, _, gh = nio.read_gadget(args.input, ids=False)
+        L = float(gh["BoxSize"])
+        if world > 1 and not args.redistribute:
+            raise SystemExit("--input-format gadget with --gpus > 1 needs --redistribute")
     stream = hip.Stream()
     t_gen = time.perf_counter()
     ds = None
     halo = None
     if world == 1:
-        if args.input:
+        if gadget is not None:
+            points, gadget = gadget, None
+            n = points.shape[0]
+        elif args.input:
             from nbodyhpc_amd import io as nio
             points = nio.read_positions(args.input, mmap=False)
             n = points.shape[0]
@@ -458,7 +471,7 @@ def main():
         if args.input and args.redistribute:
             # each rank reads its contiguous row chunk; all-to-all-v to the owners
             from nbodyhpc_amd import io as nio
-            rows = nio.read_positions(args.input)
+            rows = gadget if gadget is not None else nio.read_positions(args.input)
             lo_r, hi_r = rank * rows.shape[0] // world, (rank + 1) * rows.shape[0] // world
             own_xyz, own_ids = slab.redistribute(
                 np.array(rows[lo_r:hi_r]), np.arange(lo_r, hi_r, dtype=np.uint32), rank, world,
@@ -616,7 +629,7 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": (f"file: {os.path.basename(args.input)} (raw float32 (N, 3)); self-queries"
+        "data": (f"file: {os.path.basename(args.input)} ({args.input_format}); self-queries"
                  if args.input else
                  "synthetic: numpy PCG64 uniform [0,L)^3, L=1, float32; self-queries"),
         "config": {

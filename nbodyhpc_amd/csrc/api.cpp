@@ -51,7 +51,8 @@ void free_tree(Tree &t) {
     if (t.leafinfo) (void)hipFree(t.leafinfo);
     if (t.hsplit) (void)hipFree(t.hsplit);
     if (t.ginfo) (void)hipFree(t.ginfo);
-    t.ginfo = nullptr;
+    if (t.hinfo) (void)hipFree(t.hinfo);
+    t.ginfo = t.hinfo = nullptr;
     t.leafinfo = nullptr;
     t.hsplit = nullptr;
     t.splits = nullptr;

@@ -576,7 +576,7 @@ constexpr int GPL = NBKD_GBLOCK / 64; // points per lane
 __global__ void __launch_bounds__(TB)
 group_kernel(const nbkd_node *__restrict__ nodes, uint64_t nn, float *__restrict__ x,
              float *__restrict__ y, float *__restrict__ z, uint32_t *__restrict__ idx, uint64_t n,
-             float *__restrict__ ginfo) {
+             float *__restrict__ ginfo, float *__restrict__ hinfo) {
     constexpr int WPB = TB / 64;
     __shared__ float sp[WPB][3][NBKD_GBLOCK];
     __shared__ uint32_t sr[WPB][NBKD_GBLOCK];
@@ -683,6 +683,29 @@ group_kernel(const nbkd_node *__restrict__ nodes, uint64_t nn, float *__restrict
                 o[2] = lo[1];
                 o[3] = hi[1];
                 o[4] = lo[2];
+                o[5] = hi[2];
+            }
+            // a leaf of 65..128 points: the tight boxes of its two halves (the
+            // first cut above, at m), the kNN collect kernel's staging chunks
+            const uint32_t cnt_leaf = nd.right - nd.left;
+            if (hinfo && b0 == nd.left && cnt_leaf > 64 && cnt_leaf <= NBKD_GBLOCK && lane < 2) {
+                const uint32_t m = (c / 2) / 8 * 8;
+                const uint32_t j0 = lane == 0 ? 0u : m, j1 = lane == 0 ? m : c;
+                float lo[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, hi[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+                for (uint32_t j = j0; j < j1; ++j) {
+                    if (!R[j]) continue;
+#pragma unroll
+                    for (int a = 0; a < 3; ++a) {
+                        lo[a] = fminf(lo[a], P[a][j]);
+                        hi[a] = fmaxf(hi[a], P[a][j]);
+                    }
+                }
+                float *o = hinfo + 12 * (size_t)i + 6 * lane; // leafinfo's word order
+                o[0] = lo[0];
+                o[1] = lo[1];
+                o[2] = lo[2];
+                o[3] = hi[0];
+                o[4] = hi[1];
                 o[5] = hi[2];
             }
             wave_sync();
@@ -970,9 +993,10 @@ nbkd_status build_tree(Tree &t, const float *xyz, uint64_t n, int32_t leaf_size,
     if (n8 > 0) {
         TimedScope ts("build_groups", s);
         NBKD_HIP(hipMalloc(&t.ginfo, (n8 / NBKD_GROUP) * 6 * sizeof(float)));
+        if (t.leaf > 64) NBKD_HIP(hipMalloc(&t.hinfo, t.nnodes * 12 * sizeof(float)));
         const uint64_t blocks = std::min<uint64_t>((t.nnodes + 3) / 4, 65536);
         group_kernel<<<(unsigned)std::max<uint64_t>(blocks, 1), TB, 0, s>>>(
-            t.nodes, t.nnodes, t.x, t.y, t.z, t.idx, t.n, t.ginfo);
+            t.nodes, t.nnodes, t.x, t.y, t.z, t.idx, t.n, t.ginfo, t.hinfo);
         NBKD_HIP(hipGetLastError());
     }
     {

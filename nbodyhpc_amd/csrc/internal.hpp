@@ -60,6 +60,10 @@ struct Tree {
     // positions; ginfo[6 g .. 6 g + 6) = the tight box of group g (positions
     // 8g .. 8g+7, real points only) as lo.x, hi.x, lo.y, hi.y, lo.z, hi.z
     float *ginfo = nullptr;
+    // leaves of 65..128 points (leafsize > 64 only): per node id, the tight
+    // boxes of the leaf's two halves (first cut at m = floor(count/2/8)*8), 12
+    // floats: lo.xyz, hi.xyz per half (leafinfo's word order)
+    float *hinfo = nullptr;
     // internal nodes' split values in the 4-level blocked heap order below
     // (hblk_blocks(depth) lines of 16 floats), or nullptr
     float *hsplit = nullptr;

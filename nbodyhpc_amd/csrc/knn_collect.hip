@@ -449,14 +449,15 @@ struct CollectLdsG {
     uint8_t slot[64];            // lanes needing the leaf, compacted
 };
 
-#define NBKD_COLLECT_STAGE_G(LPOS, LEND)                                                           \
+// a chunk of CN points at LPOS, its group boxes and its tight box TBOX (6
+// words: lo.xyz, hi.xyz)
+#define NBKD_COLLECT_STAGE_G(LPOS, CN, TBOX)                                                       \
     do {                                                                                           \
-        const uint32_t cn_ = min((uint32_t)GCHUNK, (LEND) - (LPOS));                               \
-        glds_f32(t.x + (LPOS), W.pb[0], lane, cn_);                                                \
-        glds_f32(t.y + (LPOS), W.pb[1], lane, cn_);                                                \
-        glds_f32(t.z + (LPOS), W.pb[2], lane, cn_);                                                \
-        glds_f32(ginfo + 6 * (size_t)((LPOS) / NBKD_GROUP), W.gb, lane, 6 * (cn_ / NBKD_GROUP));   \
-        glds_f32(reinterpret_cast<const float *>(linfo) + 8 * (size_t)node, W.tb, lane, 6);       \
+        glds_f32(t.x + (LPOS), W.pb[0], lane, (CN));                                               \
+        glds_f32(t.y + (LPOS), W.pb[1], lane, (CN));                                               \
+        glds_f32(t.z + (LPOS), W.pb[2], lane, (CN));                                               \
+        glds_f32(ginfo + 6 * (size_t)((LPOS) / NBKD_GROUP), W.gb, lane, 6 * ((CN) / NBKD_GROUP));  \
+        glds_f32((TBOX), W.tb, lane, 6);                                                           \
     } while (0)
 
 // v = lanes in `mask` ? val : old, as one v_cndmask (a select of a uniform
@@ -598,6 +599,7 @@ __device__ __forceinline__ uint32_t lane_set(uint32_t old, uint32_t val, uint64_
 template <bool PER, bool M, bool STATS>
 __device__ __forceinline__ void grp_packet(const DevTree &t, const float *__restrict__ ginfo,
                                            const uint32_t *__restrict__ linfo,
+                                           const float *__restrict__ hinfo,
                                            CollectLdsG &W, const int lane, const float qx,
                                            const float qy, const float qz, float kth,
                                            const float s_over_nb, const float nb_over_s,
@@ -636,14 +638,22 @@ __device__ __forceinline__ void grp_packet(const DevTree &t, const float *__rest
         bool ha;
         NBKD_GWALK(ha, pa, ea);
         if (!ha) break;
-        NBKD_COLLECT_STAGE_G(pa, ea);
+        // chunks: a leaf of 65..128 points is staged as its two halves, each
+        // with its own tight box (hinfo); other leaves in runs of 64 points
+        // under the leaf's tight box (leafinfo)
+        const uint32_t lend = ea;
+        const uint32_t lc = lend - pa;
+        const bool halves = hinfo != nullptr && lc > (uint32_t)GCHUNK && lc <= 2u * GCHUNK;
+        const uint32_t hm = (lc / 2) / 8 * 8;
+        const float *const lbox = halves ? hinfo + 12 * (size_t)node
+                                         : reinterpret_cast<const float *>(linfo) + 8 * (size_t)node;
+        uint32_t c0 = pa;
+        uint32_t cn = halves ? hm : min((uint32_t)GCHUNK, lc);
+        NBKD_COLLECT_STAGE_G(pa, cn, lbox);
         NBKD_PH(0);
         wait_vm0();
         wave_sync();
         NBKD_PH(1);
-        const uint32_t lend = ea;
-        uint32_t c0 = pa;
-        uint32_t cn = min((uint32_t)GCHUNK, lend - c0);
         bool any_leaf = false;
         for (;;) {
             const uint32_t ng = cn / NBKD_GROUP;
@@ -746,9 +756,9 @@ __device__ __forceinline__ void grp_packet(const DevTree &t, const float *__rest
                 NBKD_PH(5);
                 break;
             }
-            cn = min((uint32_t)GCHUNK, lend - c0);
+            cn = halves ? lc - hm : min((uint32_t)GCHUNK, lend - c0);
             wave_sync();
-            NBKD_COLLECT_STAGE_G(c0, lend);
+            NBKD_COLLECT_STAGE_G(c0, cn, halves ? lbox + 6 : lbox);
             wait_vm0();
             wave_sync();
         }
@@ -761,7 +771,8 @@ __device__ __forceinline__ void grp_packet(const DevTree &t, const float *__rest
 template <bool PER, int OCC, bool STATS>
 __global__ void __launch_bounds__(TB, OCC)
 knn_collect_grp_kernel(DevTree t, const float *__restrict__ ginfo,
-                       const uint32_t *__restrict__ linfo, const float *__restrict__ q,
+                       const uint32_t *__restrict__ linfo, const float *__restrict__ hinfo,
+                       const float *__restrict__ q,
                        const uint32_t *__restrict__ order, uint32_t m, int kq,
                        const float *__restrict__ tg, float seed_mul, uint32_t qpp,
                        uint2 *__restrict__ cand, uint32_t capg,
@@ -785,7 +796,7 @@ knn_collect_grp_kernel(DevTree t, const float *__restrict__ ginfo,
     uint2 *const col = cand + (size_t)pk * qpp * capg;
     uint32_t cnt = 0;
     uint64_t st[13] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-    grp_packet<PER, PER, STATS>(t, ginfo, linfo, W, lane, qx, qy, qz, seed, s_over_nb, nb_over_s,
+    grp_packet<PER, PER, STATS>(t, ginfo, linfo, hinfo, W, lane, qx, qy, qz, seed, s_over_nb, nb_over_s,
                                 col, qpp, capg, kq, cnt, st);
     if (valid) ccount[gq] = cnt;
     if (STATS && lane == 0) {
@@ -989,11 +1000,11 @@ void launch_collect(const Tree &t, const float *q, const uint32_t *order, uint32
         TimedScope ts(name, s);
         if (stats)
             knn_collect_grp_kernel<PER, 8, true><<<blocks, TB, 0, s>>>(
-                view(t), t.ginfo, t.leafinfo, q, order, m, k, tg, seed_mul, qpp, cand, capg,
+                view(t), t.ginfo, t.leafinfo, t.hinfo, q, order, m, k, tg, seed_mul, qpp, cand, capg,
                 ccount, stats);
         else
             knn_collect_grp_kernel<PER, 8, false><<<blocks, TB, 0, s>>>(
-                view(t), t.ginfo, t.leafinfo, q, order, m, k, tg, seed_mul, qpp, cand, capg,
+                view(t), t.ginfo, t.leafinfo, t.hinfo, q, order, m, k, tg, seed_mul, qpp, cand, capg,
                 ccount, nullptr);
         return;
     }

@@ -1,5 +1,6 @@
 """Raw particle files (reference main.cpp:103-114 format) and slab streaming."""
 import numpy as np
+import pytest
 
 from nbodyhpc_amd import io, slab
 
@@ -46,3 +47,29 @@ def test_empty_file(tmp_path):
     assert io.read_positions(p).shape == (0, 3)
     xyz, ids = io.read_slab(p, 0, 2, 1.0)
     assert xyz.shape == (0, 3) and ids.shape == (0,)
+
+
+@pytest.mark.parametrize("fmt,endian,nfiles,idt", [(1, "<", 1, np.uint32), (2, "<", 1, np.uint64),
+                                                   (1, ">", 3, np.uint32), (2, ">", 2, np.uint32)])
+def test_gadget_round_trip(tmp_path, fmt, endian, nfiles, idt):
+    """Gadget-2 snapshots (format 1 and 2, both byte orders, multi-file):
+    positions, ids and BoxSize come back exactly."""
+    from nbodyhpc_amd import io as nio
+    rng = np.random.default_rng(3)
+    xyz = rng.uniform(0, 50.0, (1001, 3)).astype(np.float32)
+    ids = (rng.permutation(1001) + 7).astype(idt)
+    p = str(tmp_path / "snap_010")
+    nio.write_gadget(p, xyz, 50.0, ids=ids, fmt=fmt, endian=endian, num_files=nfiles)
+    got, gid, h = nio.read_gadget(p)
+    assert np.array_equal(got, xyz)
+    assert gid is not None and np.array_equal(gid, ids) and gid.dtype == idt
+    assert h["BoxSize"] == 50.0 and h["num_files"] == nfiles
+    assert int(np.sum(h["npartTotal"])) == 1001
+
+
+def test_gadget_rejects_other_files(tmp_path):
+    from nbodyhpc_amd import io as nio
+    p = tmp_path / "raw.bin"
+    nio.write_positions(str(p), np.ones((10, 3), np.float32))
+    with pytest.raises(ValueError):
+        nio.read_gadget(str(p))
