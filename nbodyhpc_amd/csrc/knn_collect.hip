@@ -441,11 +441,11 @@ struct CollectLdsG {
     float4 sq[64]; // per lane: query xyz + bound
     float scl[64]; // per lane: bucket factor (d2_bucket)
     uint32_t cnt[64];
-    uint32_t hist[NB / 4][64];
+    uint32_t hist[NB / 4][65];  // padded rows: one lane's 4 words sit in 4 banks
     float pb[3][GCHUNK];
     float gb[6 * GMAX];          // the chunk's group boxes (lo.x, hi.x, lo.y, hi.y, lo.z, hi.z)
     float tb[8];                 // the leaf's tight box (leafinfo words 0..5)
-    uint16_t pairs[64 * GMAX];   // (lane, group) pairs: lane | group << 6
+    uint16_t pairs[64 * GMAX];   // (slot, lane, group) pairs: slot | lane << 6 | group << 12
     uint8_t slot[64];            // lanes needing the leaf, compacted
 };
 
@@ -670,29 +670,38 @@ __device__ __forceinline__ void grp_packet(const DevTree &t, const float *__rest
                     st[12] += nneed;
                 }
                 W.cnt[lane] = cnt;
-                W.sq[lane] = make_float4(qx, qy, qz, kth);
-                W.scl[lane] = nb_over_s;
-                if (need) W.slot[mbcnt64(nm)] = (uint8_t)lane;
+                // the needing lanes' queries by compacted slot: 8 consecutive
+                // slots per 64 lanes below read 8 distinct, adjacent LDS words
+                // (indexed by lane, owners 16 apart hit the same banks)
+                if (need) {
+                    const uint32_t r = mbcnt64(nm);
+                    W.slot[r] = (uint8_t)lane;
+                    W.sq[r] = make_float4(qx, qy, qz, kth);
+                    W.scl[r] = nb_over_s;
+                }
                 wave_sync();
                 // (needing lane, group) box tests, 8 lanes per needing lane (one
-                // per group); the groups reached become the pair list
+                // per group); the groups reached become the pair list, entries
+                // slot | owner lane << 6 | group << 12
                 uint32_t np = 0;
                 const uint32_t ntest = nneed * GMAX;
 #pragma unroll 1
                 for (uint32_t t0 = 0; t0 < ntest; t0 += 64) {
                     const uint32_t ti = t0 + lane;
                     const uint32_t g = ti % GMAX;
+                    const uint32_t sl = ti / GMAX;
                     uint32_t owner = 0;
                     bool hit = false;
                     if (ti < ntest && g < ng) {
-                        owner = W.slot[ti / GMAX];
-                        const float4 qq = W.sq[owner];
+                        owner = W.slot[sl];
+                        const float4 qq = W.sq[sl];
                         const float gbx[6] = {W.gb[6 * g], W.gb[6 * g + 1], W.gb[6 * g + 2],
                                               W.gb[6 * g + 3], W.gb[6 * g + 4], W.gb[6 * g + 5]};
                         hit = box_lb2<M>(qq.x, qq.y, qq.z, gbx, L) <= qq.w;
                     }
                     const uint64_t hm = __ballot(hit);
-                    if (hit) W.pairs[np + mbcnt64(hm)] = (uint16_t)(owner | (g << 6));
+                    if (hit)
+                        W.pairs[np + mbcnt64(hm)] = (uint16_t)(sl | (owner << 6) | (g << 12));
                     np += (uint32_t)__popcll(hm);
                 }
                 NBKD_PH(2);
@@ -706,13 +715,13 @@ __device__ __forceinline__ void grp_packet(const DevTree &t, const float *__rest
                     const uint32_t ti = t0 + lane;
                     if (ti < ntrip) {
                         const uint32_t pr = W.pairs[ti / NBKD_GROUP];
-                        const uint32_t owner = pr & 63u;
-                        const uint32_t pi = (pr >> 6) * NBKD_GROUP + (ti % NBKD_GROUP);
-                        const float4 qq = W.sq[owner];
+                        const uint32_t qs = pr & 63u, owner = (pr >> 6) & 63u;
+                        const uint32_t pi = (pr >> 12) * NBKD_GROUP + (ti % NBKD_GROUP);
+                        const float4 qq = W.sq[qs];
                         const float d = point_d2_fast<M>(qq.x, qq.y, qq.z, W.pb[0][pi],
                                                          W.pb[1][pi], W.pb[2][pi], L);
                         if (d < qq.w) {
-                            const uint32_t j = d2_bucket(d, W.scl[owner]);
+                            const uint32_t j = d2_bucket(d, W.scl[qs]);
                             atomicAdd(&W.hist[j >> 2][owner], 1u << (8 * (j & 3)));
                             const uint32_t sl = atomicAdd(&W.cnt[owner], 1u);
                             if (sl < capg)
