@@ -42,6 +42,7 @@ enum {
 /* flags */
 #define NBKD_INPUT_DEVICE 0x1u  /* point / query arrays are device pointers */
 #define NBKD_OUTPUT_DEVICE 0x2u /* output arrays are device pointers        */
+#define NBKD_ACCUMULATE 0x4u    /* nbkd_deposit: add into `out` instead of overwriting it */
 
 typedef struct nbkd_tree nbkd_tree;
 
@@ -190,6 +191,31 @@ nbkd_status nbkd_comm_exchange(nbkd_comm *comm, int32_t npairs, const void *cons
                                void *const *recv, const uint64_t *recv_bytes,
                                const int32_t *recv_peer, void *stream);
 void nbkd_comm_free(nbkd_comm *comm);
+
+/*
+ * Deposit n spheres (centres xyz row-major (n, 3), weight[n], radius[n]) onto a
+ * voxel grid, with the semantics of the reference's point rasteriser:
+ * replaces PointRenderer::render_points_volume / render_points
+ * (rasterization/src/cpp/point_renderer.cpp:606-657,825-950), assemble_vertices
+ * (rasterization/src/cpp/pybind.cpp:25-71), augment_vertices_periodic
+ * (rasterization/src/cpp/vertex_utilities.cpp:15-42) and the vertex / fragment
+ * shaders (rasterization/shaders/triangle.vert, triangle.frag).
+ *   out        gx * gy * nz float32, element (px, py, s) at px + gx * (py + gy * s)
+ *              (the reference's column-major (gx, gy, nz) array); zeroed first
+ *              unless NBKD_ACCUMULATE is set.
+ *   pixels_per_unit  voxels per unit length (> 0).
+ *   period     3 floats (NULL = none); period[d] > 0 wraps axis d with that length.
+ *   subsample  S: each straddled voxel is sampled at S^3 points (1..16).
+ *   mode       0: nz slices [s, s+1) / ppu (render_points_volume);
+ *              1: one plane at z = 0 (render_points; nz must be 1).
+ * A voxel receives weight * (sub-samples inside the ball) / S^3 / (4/3 pi R^3)
+ * (R the radius in voxels); a ball under half a voxel across deposits its whole
+ * weight in the voxel holding its centre.
+ */
+nbkd_status nbkd_deposit(const float *xyz, const float *weight, const float *radius, uint64_t n,
+                         int32_t gx, int32_t gy, int32_t nz, float pixels_per_unit,
+                         const float *period, int32_t subsample, int32_t mode, float *out,
+                         int32_t device, uint32_t flags, void *stream);
 
 #ifdef __cplusplus
 }

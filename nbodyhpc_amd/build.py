@@ -29,7 +29,7 @@ ARCH = os.environ.get("NBKD_ARCH", "gfx950")
 HIP_FLAGS = ["--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
              "-Wall", "-Wno-unused-function", "-Wno-unused-const-variable"]
 SOURCES = ["api.cpp", "build.hip", "query.hip", "knn_packet.hip", "knn_collect.hip", "ball.hip",
-           "slab.hip"]
+           "slab.hip", "deposit.hip"]
 HEADERS = [os.path.join(CSRC, "internal.hpp"), os.path.join(CSRC, "metric.hpp"),
            os.path.join(CSRC, "packet.hpp"),
            os.path.join(ROOT, "include", "nbkd.h")]

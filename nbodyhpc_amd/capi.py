@@ -18,6 +18,7 @@ HEADER = os.path.join(os.path.dirname(PKG), "include", "nbkd.h")
 NBKD_OK, NBKD_EINVAL, NBKD_EBOX, NBKD_ETOOMANY, NBKD_ENOMEM, NBKD_EDEVICE = range(6)
 NBKD_INPUT_DEVICE = 0x1
 NBKD_OUTPUT_DEVICE = 0x2
+NBKD_ACCUMULATE = 0x4
 
 NODE_DTYPE = np.dtype([("dim", "<i4"), ("split", "<f4"), ("left", "<u4"), ("right", "<u4")])
 
@@ -64,6 +65,8 @@ _PROTOS = {
     "nbkd_comm_init": (_i32, [_c_p, _i32, _i32, _i32, ctypes.POINTER(_c_p)]),
     "nbkd_comm_exchange": (_i32, [_c_p, _i32, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p]),
     "nbkd_comm_free": (None, [_c_p]),
+    "nbkd_deposit": (_i32, [_c_p, _c_p, _c_p, _u64, _i32, _i32, _i32, ctypes.c_float, _c_p, _i32,
+                            _i32, _c_p, _i32, _u32, _c_p]),
 }
 COMM_ID_BYTES = 128
 
@@ -207,6 +210,38 @@ class Tree:
                                          idx.ctypes.data if idx.size else None, idx.size, 0,
                                          None))
         return off, idx
+
+
+def deposit(xyz, weight, radius, grid, ppu, period=(-1.0, -1.0, -1.0), subsample=4, mode=0,
+            device=-1, out=None):
+    """Host arrays in, float32 grid (gx, gy, nz) in Fortran order out (nbkd_deposit).
+    `out` (same shape, Fortran-contiguous float32): accumulate into it."""
+    p, w, r = _host_f32(xyz), _host_f32(weight), _host_f32(radius)
+    gx, gy, nz = (int(v) for v in grid)
+    per = np.ascontiguousarray(period, np.float32)
+    flags = 0
+    if out is None:
+        out = np.empty((gx, gy, nz), np.float32, order="F")
+    else:
+        if out.dtype != np.float32 or out.shape != (gx, gy, nz) or not out.flags.f_contiguous:
+            raise ValueError("out must be a Fortran-ordered float32 array of the grid's shape")
+        flags |= NBKD_ACCUMULATE
+    _check(lib().nbkd_deposit(p.ctypes.data, w.ctypes.data, r.ctypes.data, p.shape[0], gx, gy, nz,
+                              float(ppu), per.ctypes.data, int(subsample), int(mode),
+                              out.ctypes.data, int(device), flags, None))
+    return out
+
+
+def deposit_device(xyz_ptr, weight_ptr, radius_ptr, n, grid, ppu, out_ptr,
+                   period=(-1.0, -1.0, -1.0), subsample=4, mode=0, device=-1, accumulate=False,
+                   stream=None):
+    """Device pointers in and out; returns once the deposit is enqueued."""
+    gx, gy, nz = (int(v) for v in grid)
+    per = np.ascontiguousarray(period, np.float32)
+    flags = NBKD_INPUT_DEVICE | NBKD_OUTPUT_DEVICE | (NBKD_ACCUMULATE if accumulate else 0)
+    _check(lib().nbkd_deposit(xyz_ptr, weight_ptr, radius_ptr, int(n), gx, gy, nz, float(ppu),
+                              per.ctypes.data, int(subsample), int(mode), out_ptr, int(device),
+                              flags, stream))
 
 
 def timing_enable(on=True):

@@ -2,6 +2,7 @@
 // build.hip / query.hip.  No exception crosses the boundary.
 #include <hip/hip_runtime.h>
 
+#include <cmath>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -244,6 +245,42 @@ nbkd_status nbkd_query_ball_csr(const nbkd_tree *tree, const float *q, uint64_t 
     DeviceGuard g(tree->t.device);
     return query_ball_csr(tree->t, q, m, r, out_offsets, out_idx, capacity, flags,
                           (hipStream_t)stream);
+    NBKD_GUARD_END
+}
+
+nbkd_status nbkd_deposit(const float *xyz, const float *weight, const float *radius, uint64_t n,
+                         int32_t gx, int32_t gy, int32_t nz, float ppu, const float *period,
+                         int32_t subsample, int32_t mode, float *out, int32_t device,
+                         uint32_t flags, void *stream) {
+    NBKD_GUARD_BEGIN
+    g_err.clear();
+    if (!out || (n > 0 && (!xyz || !weight || !radius))) {
+        set_error("nbkd_deposit: NULL argument");
+        return NBKD_EINVAL;
+    }
+    if (gx < 1 || gy < 1 || nz < 1 || (uint64_t)gx * (uint64_t)gy >= (1ull << 31)) {
+        set_error("nbkd_deposit: grid extents must be >= 1 with gx * gy < 2^31");
+        return NBKD_EINVAL;
+    }
+    if (!(ppu > 0.0f) || !std::isfinite(ppu)) {
+        set_error("nbkd_deposit: pixels_per_unit must be positive and finite");
+        return NBKD_EINVAL;
+    }
+    if (subsample < 1 || subsample > 16) {
+        set_error("nbkd_deposit: subsample must be in [1, 16]");
+        return NBKD_EINVAL;
+    }
+    if (mode != 0 && !(mode == 1 && nz == 1)) {
+        set_error("nbkd_deposit: mode must be 0 (volume) or 1 (one plane, nz = 1)");
+        return NBKD_EINVAL;
+    }
+    DeviceGuard g(device);
+    if (!g.ok) {
+        set_error("nbkd_deposit: cannot select the device");
+        return NBKD_EDEVICE;
+    }
+    return deposit(xyz, weight, radius, n, gx, gy, nz, ppu, period, subsample, mode, out, flags,
+                   (hipStream_t)stream);
     NBKD_GUARD_END
 }
 

@@ -186,6 +186,11 @@ nbkd_status query_ball_count(const Tree &t, const float *q, uint64_t m, float r,
 nbkd_status query_ball_csr(const Tree &t, const float *q, uint64_t m, float r, uint64_t *offsets,
                            uint32_t *out_idx, uint64_t capacity, uint32_t flags, hipStream_t s);
 
+// deposit.hip: spheres onto a voxel grid (render_points_volume / render_points)
+nbkd_status deposit(const float *xyz, const float *weight, const float *radius, uint64_t n, int gx,
+                    int gy, int nz, float ppu, const float *period, int S, int mode, float *out,
+                    uint32_t flags, hipStream_t s);
+
 // order-preserving float -> uint32 key (IEEE-754 total order of non-NaN values)
 __host__ __device__ inline uint32_t fkey(float f) {
     uint32_t u = __builtin_bit_cast(uint32_t, f);

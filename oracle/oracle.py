@@ -160,6 +160,25 @@ class Oracle(_Lib):
         L.orc_point_d2.restype = ctypes.c_float
         L.orc_box_d2.argtypes = [_fp, _fp, ctypes.c_int32, ctypes.c_float]
         L.orc_box_d2.restype = ctypes.c_float
+        L.orc_deposit.argtypes = [_fp, _fp, _fp, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
+                                  ctypes.c_int32, ctypes.c_float, _fp, ctypes.c_int32,
+                                  ctypes.c_int32, ctypes.POINTER(ctypes.c_double)]
+        L.orc_deposit.restype = ctypes.c_int
+
+    def deposit(self, xyz, weight, radius, grid, ppu, period=(-1.0, -1.0, -1.0), subsample=4,
+                mode=0):
+        """Restated rasteriser (deposit_oracle.c): float64 grid of shape (gx, gy, nz),
+        Fortran order, as the reference's render_points_volume returns it."""
+        p, w, r = _f32(xyz), _f32(weight), _f32(radius)
+        gx, gy, nz = (int(v) for v in grid)
+        per = np.asarray(period, np.float32)
+        out = np.zeros(gx * gy * nz, np.float64)
+        st = self.lib.orc_deposit(_ptr(p, _fp), _ptr(w, _fp), _ptr(r, _fp), p.shape[0], gx, gy, nz,
+                                  float(ppu), _ptr(per, _fp), int(subsample), int(mode),
+                                  out.ctypes.data_as(ctypes.POINTER(ctypes.c_double)))
+        if st:
+            raise ValueError("orc_deposit: bad arguments")
+        return out.reshape((gx, gy, nz), order="F")
 
     def tree(self, points, leafsize=128, boxsize=None):
         return Tree(self, points, leafsize, boxsize)

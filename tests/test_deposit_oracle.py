@@ -1,0 +1,180 @@
+"""The deposit oracle (oracle/deposit_oracle.c) and the rasterizer's host logic.
+
+The reference's Vulkan renderer cannot run here (no Vulkan, no GPU), so the
+oracle is pinned by (1) an independent numpy restatement of the shaders written
+from rasterization/shaders/triangle.{vert,frag} and vertex_utilities.cpp, and
+(2) properties the reference's design implies: a ball well inside the grid
+deposits its weight (to the S^3 sampling error), a sub-voxel ball lands whole in
+the voxel holding its centre, periodic images conserve the weight of a ball
+straddling the box edge, and the result is indexed [x, y, slice].
+"""
+import numpy as np
+import pytest
+
+from oracle.oracle import Oracle
+
+f32 = np.float32
+
+
+@pytest.fixture(scope="module")
+def orc():
+    return Oracle()
+
+
+def _np_deposit(xyz, w, r, grid, ppu, period, S, mode):
+    """Straight numpy restatement of the shader pipeline (float32 per step)."""
+    gx, gy, nz = grid
+    out = np.zeros((gx, gy, nz), np.float64)
+    ppu = f32(ppu)
+    off = ((np.arange(S, dtype=f32) + f32(0.5)) / f32(S)).astype(f32)
+    inc = f32(1.0) / f32(S * S * S)
+    tbl = np.zeros(S ** 3 + 1, f32)
+    acc = f32(0)
+    for c in range(1, S ** 3 + 1):
+        acc = f32(acc + inc)
+        tbl[c] = acc
+    for p in range(len(r)):
+        rad, wt = f32(r[p]), f32(w[p])
+        shifts = []
+        for d in range(3):
+            v = f32(xyz[p, d])
+            s = [v]
+            if period[d] > 0:
+                P = f32(period[d])
+                if f32(v + rad) > P:
+                    s.append(f32(v - P))
+                if f32(v - rad) < 0:
+                    s.append(f32(v + P))
+            shifts.append(s)
+        for x in shifts[0]:
+            for y in shifts[1]:
+                for z in shifts[2]:
+                    o = f32(rad * ppu)
+                    r2 = f32(o * o)
+                    vol = f32(f32(f32(f32(f32(f32(4.0) / f32(3.0)) * f32(np.pi)) * o) * o) * o)
+                    slices = [0] if mode == 1 else range(nz)
+                    for s in slices:
+                        if mode == 1:
+                            depth, lo, up = f32(0), f32(-0.5), f32(0.5)
+                        else:
+                            depth = f32((s + 0.5) / float(ppu))
+                            lo, up = f32(s / float(ppu)), f32((s + 1) / float(ppu))
+                        zoff = f32(z - depth)
+                        if f32(f32(ppu * f32(rad - abs(zoff))) + f32(1)) < 0:
+                            continue
+                        if o < f32(0.5):
+                            if z <= lo or z > up:
+                                continue
+                            dens, size = wt, f32(1)
+                        else:
+                            pr = f32(np.sqrt(max(f32(0), f32(f32(rad * rad) - f32(zoff * zoff)))))
+                            size = f32(f32(2) * f32(np.ceil(f32(pr * ppu))) + f32(2))
+                            dens = f32(wt / vol)
+                        xw, yw = f32(x * ppu), f32(y * ppu)
+                        h = f32(f32(0.5) * size)
+                        for py in range(gy):
+                            cy = f32(py + 0.5)
+                            if not (f32(yw - h) <= cy < f32(yw + h)):
+                                continue
+                            for px in range(gx):
+                                cx = f32(px + 0.5)
+                                if not (f32(xw - h) <= cx < f32(xw + h)):
+                                    continue
+                                if r2 < f32(0.25):
+                                    out[px, py, s] += dens
+                                    continue
+                                dx, dy = f32(xw - f32(px)), f32(yw - f32(py))
+                                dz = f32(f32(zoff * ppu) + f32(0.5))
+                                sx = (dx - off).astype(f32)[:, None, None]
+                                sy = (dy - off).astype(f32)[None, :, None]
+                                sz = (dz - off).astype(f32)[None, None, :]
+                                d = ((sx * sx + sy * sy).astype(f32) + sz * sz).astype(f32)
+                                c = int((d < r2).sum())
+                                if c:
+                                    out[px, py, s] += float(f32(dens * tbl[c]))
+    return out
+
+
+@pytest.mark.parametrize("case", ["mixed", "periodic", "slice2d", "s3"])
+def test_oracle_matches_numpy_restatement(orc, case):
+    rng = np.random.default_rng({"mixed": 1, "periodic": 2, "slice2d": 3, "s3": 4}[case])
+    n, grid, ppu, S, mode = 12, (9, 7, 6), 2.0, 4, 0
+    period = (-1.0, -1.0, -1.0)
+    if case == "periodic":
+        period = (grid[0] / ppu, grid[1] / ppu, grid[2] / ppu)
+    if case == "slice2d":
+        grid, mode = (9, 7, 1), 1
+    if case == "s3":
+        S = 3
+    box = np.array([grid[0], grid[1], max(grid[2], 2)]) / ppu
+    xyz = (rng.uniform(0, 1, (n, 3)) * box).astype(f32)
+    if mode == 1:
+        xyz[:, 2] = rng.uniform(-0.6, 0.6, n).astype(f32)
+    r = rng.choice([0.1, 0.3, 0.8, 1.7], n).astype(f32)
+    w = rng.uniform(0.5, 2.0, n).astype(f32)
+    got = orc.deposit(xyz, w, r, grid, ppu, period, S, mode)
+    ref = _np_deposit(xyz, w, r, grid, ppu, period, S, mode)
+    np.testing.assert_allclose(got, ref, rtol=1e-12, atol=0)
+
+
+def test_ball_inside_grid_conserves_weight(orc):
+    # radius 5 voxels at S = 4: the sampled volume is within 1 % of 4/3 pi R^3
+    xyz = np.array([[8.3, 8.1, 7.9]], f32)
+    g = orc.deposit(xyz, np.array([3.0], f32), np.array([5.0], f32), (17, 17, 17), 1.0)
+    assert abs(g.sum() - 3.0) < 0.03
+    # centred on the ball: the voxel holding the centre is fully inside
+    full = 3.0 / (4.0 / 3.0 * np.pi * 125.0)
+    assert abs(g[8, 8, 7] - full) < 1e-6 * full
+
+
+def test_subvoxel_ball_lands_in_its_voxel(orc):
+    xyz = np.array([[2.6, 1.2, 3.9]], f32)
+    g = orc.deposit(xyz, np.array([1.5], f32), np.array([0.2], f32), (5, 4, 6), 1.0)
+    assert g[2, 1, 3] == pytest.approx(1.5)
+    assert g.sum() == pytest.approx(1.5)
+
+
+def test_periodic_images_conserve_weight(orc):
+    # a ball across the corner of a periodic box: its images fill the far faces
+    xyz = np.array([[0.3, 0.2, 15.8]], f32)
+    L = 16.0
+    g = orc.deposit(xyz, np.array([2.0], f32), np.array([4.0], f32), (16, 16, 16), 1.0,
+                    period=(L, L, L))
+    assert abs(g.sum() - 2.0) < 0.03
+    assert g[15, 15, 0] > 0 and g[0, 0, 15] > 0
+    open_ = orc.deposit(xyz, np.array([2.0], f32), np.array([4.0], f32), (16, 16, 16), 1.0)
+    assert open_.sum() < 0.5  # only the octant inside the box
+
+
+def test_layout_is_x_y_slice(orc):
+    xyz = np.array([[3.5, 1.5, 0.5]], f32)
+    g = orc.deposit(xyz, np.array([1.0], f32), np.array([0.1], f32), (6, 4, 3), 1.0)
+    assert g.shape == (6, 4, 3) and g.flags.f_contiguous
+    assert g[3, 1, 0] == pytest.approx(1.0)
+
+
+def test_rasterizer_argument_errors():
+    """assemble_vertices' messages (rasterization/src/cpp/pybind.cpp:28-46); raised
+    before any device call."""
+    from nbodyhpc_amd.rasterizer import (_normalize_period, get_point_renderer,
+                                         render_points_volume)
+
+    pos = np.zeros((4, 3), f32)
+    w = np.ones(4, f32)
+    cases = [
+        ((np.zeros((4, 2), f32), w, w), "positions must be a 2D array of shape (N, 3)"),
+        ((pos, np.ones((4, 1), f32), w), "weight must be a 1D array"),
+        ((pos, w, np.ones((4, 1), f32)), "radii must be a 1D array"),
+        ((pos, w, np.ones(3, f32)), "radii must have the same length as positions"),
+        ((pos, np.ones(3, f32), w), "weights must have the same length as positions"),
+    ]
+    for args, msg in cases:
+        with pytest.raises(RuntimeError, match=msg.replace("(", r"\(").replace(")", r"\)")):
+            render_points_volume(*args, 1.0, 8)
+    # renderer dimensions are stored transposed, as in the reference
+    r = get_point_renderer((10, 6))
+    assert (r.height, r.width) == (10, 6)
+    assert _normalize_period((1.0, 2.0, 3.0), True) == (1.0, 2.0, 3.0)
+    assert _normalize_period((1.0, 2.0, 3.0), False) == (-1.0, -1.0, -1.0)
+    assert _normalize_period((1.0, 2.0, 3.0), 5.0) == (5.0, 5.0, 5.0)
+    assert _normalize_period((1.0, 2.0, 3.0), (4.0, 5.0)) == (4.0, 5.0, -1.0)
