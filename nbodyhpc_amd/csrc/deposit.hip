@@ -8,22 +8,39 @@
 //
 // Layout: particles as given (row-major xyz, weight, radius); grid float32
 // [nz][gy][gx] (index px + gx * (py + gy * s)), i.e. the reference's
-// column-major (gx, gy, nz) result (pybind.cpp:141-145), accumulated with
-// float atomics in L2.
+// column-major (gx, gy, nz) result (pybind.cpp:141-145).
 //
-// Work split: one wave takes 64 consecutive particles (a dynamic counter hands
-// out the groups).  Sub-pixel particles (radius < half a voxel) land in one
-// voxel per image and are deposited by their own lane.  Every other particle
-// is processed by the whole wave: for each slice its sprite rectangle is swept
-// 64 voxels at a time; a voxel whose farthest sub-sample lies inside the ball
-// takes the full weight, one whose nearest sub-sample lies outside takes
-// nothing, and the straddling voxels are compacted into LDS and counted with
-// the wave's lanes over the S^3 sub-samples (one voxel per pass at S = 4), so
-// that the per-sub-sample test is exactly the fragment shader's.
+// Global float atomics execute at the memory side on MI355X (every request
+// leaves L2, ~1.3 TB/s chip-wide; MI355X_MICROARCH.md "Global float atomics"),
+// and a kNN-sized ball touches ~2,500 voxels, so the grid is accumulated in
+// LDS instead, one 32 x 32 x 8 voxel tile per workgroup:
+//   1. pair lists: every periodic image of every ball of at least half a voxel
+//      radius is listed under each tile its sprite box overlaps (count, scan,
+//      fill; a lane enumerates the tiles of a small box, the whole wave those
+//      of a large one);
+//   2. tiles: a workgroup takes a tile from a counter, its 4 waves take the
+//      tile's balls from an LDS counter and sweep each ball's sprite rectangle
+//      (cut to the tile) 64 voxels at a time, slice by slice.  A voxel whose
+//      farthest sub-sample is inside the ball takes the full weight, one whose
+//      nearest sub-sample is outside takes nothing (per-axis min / max
+//      offsets: exact, because float subtraction, squaring and addition are
+//      monotone), and straddling voxels go to a per-wave LDS ring; whenever 64
+//      are queued each lane counts one voxel's S^3 sub-samples with the
+//      fragment shader's own arithmetic.  Contributions are LDS float atomics;
+//      the finished tile is written once with plain coalesced stores (zeros
+//      included, so the grid needs no clearing);
+//   3. sub-voxel balls (the vertex stage's snap, triangle.vert:45-57): one
+//      lane each, one global atomic per image, after the tiles are written.
+// Measured on the 256^3-ball / 1024^3-grid case (scripts/bench_deposit.py):
+// one wave per ball with global atomics took 1775 ms in input order and 574 ms
+// in Morton order (r02_deposit profiles); see DESIGN.md for this version.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
+#include <map>
+#include <mutex>
 #include <vector>
 
 #include "internal.hpp"
@@ -33,41 +50,36 @@ namespace nbkd {
 namespace {
 
 constexpr int DB = 256; // threads per block (4 waves)
+constexpr int TX = 32, TY = 32, TZ = 8;
+constexpr int TVOX = TX * TY * TZ;
+constexpr int QCAP = 128; // straddling voxels queued per wave
 
 struct DepositArgs {
     const float *xyz, *w, *r;
     uint64_t n;
     int gx, gy, nz;
+    int ntx, nty, ntz;
     float ppu;
     float period[3];
-    int S, S3;
-    int mode; // 0: volume; 1: one plane at z = 0 (render_points)
-    const float *tbl;
+    int S; // runtime S (template S == 0)
+    int mode;
+    bool accumulate;
+    const float *planes; // nz x (depth, lower, upper)
+    const float *tbl;    // overlap after c additions of 1 / S^3
     float *grid;
-    uint32_t *work;
+    uint32_t *tile_count; // per tile: pairs (count pass), then fill cursor
+    const uint64_t *tile_off;
+    uint64_t *pairs; // particle | image << 32
+    uint32_t *work;  // tile counter
 };
 
-struct WaveLds {
-    float dx[64], dy[64];
-    uint64_t idx[64];
+struct StraddleRing {
+    float dx[QCAP], dy[QCAP], dz[QCAP], r2[QCAP], dens[QCAP];
+    uint32_t li[QCAP];
 };
 
-__device__ __forceinline__ void grid_add(float *g, uint64_t i, float v) {
-    unsafeAtomicAdd(g + i, v);
-}
-
-// slice plane depth and bounds (point_renderer.cpp:878-880; 2-D: :632-644)
-__device__ __forceinline__ void plane(int mode, int64_t s, float ppu, float &depth, float &lower,
-                                      float &upper) {
-    if (mode == 1) {
-        depth = 0.0f;
-        lower = -0.5f;
-        upper = 0.5f;
-        return;
-    }
-    depth = (float)(((double)s + 0.5) / (double)ppu);
-    lower = (float)((double)s / (double)ppu);
-    upper = (float)((double)(s + 1) / (double)ppu);
+__device__ __forceinline__ void lds_add(float *p, float v) {
+    __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
 // periodic images along one axis (vertex_utilities.cpp:21-40): the value itself,
@@ -82,18 +94,6 @@ __device__ __forceinline__ int images(float p, float r, float P, float sh[3]) {
     return n;
 }
 
-// min / max over the S sub-sample offsets of |d - (i + 0.5) / S|, as the
-// fragment shader rounds them: subtraction is monotone in the offset, so the
-// max sits at an end and the min next to floor(d * S)
-__device__ __forceinline__ void axis_range(float d, int S, float fS, float &mn, float &mx) {
-    mx = fmaxf(fabsf(d - 0.5f / fS), fabsf(d - ((float)(S - 1) + 0.5f) / fS));
-    const float t = floorf(d * fS);
-    const int c = (int)fminf(fmaxf(t, 0.0f), (float)(S - 1));
-    mn = fabsf(d - ((float)c + 0.5f) / fS);
-    if (c > 0) mn = fminf(mn, fabsf(d - ((float)(c - 1) + 0.5f) / fS));
-    if (c < S - 1) mn = fminf(mn, fabsf(d - ((float)(c + 1) + 0.5f) / fS));
-}
-
 // sprite pixel range per axis: centres px + 0.5 in [xw - h, xw + h), cut to [0, g)
 __device__ __forceinline__ void sprite_range(float xw, float h, int g, int &lo, int &hi) {
     const float a = ceilf(xw - h - 0.5f), b = ceilf(xw + h - 0.5f) - 1.0f;
@@ -101,198 +101,430 @@ __device__ __forceinline__ void sprite_range(float xw, float h, int g, int &lo, 
     hi = (int)fmaxf(fminf(b, (float)(g - 1)), -1.0f);
 }
 
-// one particle image deposited by the whole wave (x..r wave-uniform)
-__device__ void wave_image(const DepositArgs &a, WaveLds &L, int lane, float x, float y, float z,
-                           float w, float r, float lxo, float lyo, float lzo, int slot, int sub,
-                           int V) {
+// slices a ball can reach: |zoff| <= r + 1/ppu passes the clip test (with margin)
+__device__ __forceinline__ void slice_range(const DepositArgs &a, float z, float r, int &lo,
+                                            int &hi) {
+    if (a.mode == 1) {
+        lo = hi = 0;
+        return;
+    }
+    const float zl = floorf((z - r) * a.ppu) - 2.0f, zh = ceilf((z + r) * a.ppu) + 2.0f;
+    lo = (int)fminf(fmaxf(zl, 0.0f), (float)a.nz);
+    hi = (int)fmaxf(fminf(zh, (float)(a.nz - 1)), -1.0f);
+}
+
+// tile box of one ball image (sprites of every slice fit the widest one, taken
+// with a voxel of margin); false when it misses the grid
+__device__ __forceinline__ bool tile_box(const DepositArgs &a, float x, float y, float z, float r,
+                                         int &tx0, int &tx1, int &ty0, int &ty1, int &tz0,
+                                         int &tz1) {
+    const float h = ceilf(r * a.ppu) + 2.0f;
+    int px0, px1, py0, py1, s0, s1;
+    sprite_range(x * a.ppu, h, a.gx, px0, px1);
+    sprite_range(y * a.ppu, h, a.gy, py0, py1);
+    slice_range(a, z, r, s0, s1);
+    if (px1 < px0 || py1 < py0 || s1 < s0) return false;
+    tx0 = px0 / TX;
+    tx1 = px1 / TX;
+    ty0 = py0 / TY;
+    ty1 = py1 / TY;
+    tz0 = s0 / TZ;
+    tz1 = s1 / TZ;
+    return true;
+}
+
+// sub-sample offset (i + 0.5) / S (triangle.frag:25-33); with S a template
+// constant and i unrolled this folds to the same correctly rounded constant
+template <int S> __device__ __forceinline__ float off(int i, int Srt) {
+    return ((float)i + 0.5f) / (float)(S ? S : Srt);
+}
+
+// min / max over the sub-sample offsets of |d - off_i|
+template <int S>
+__device__ __forceinline__ void axis_range(float d, int Srt, float &mn, float &mx) {
+    const int n = S ? S : Srt;
+    mx = fmaxf(fabsf(d - off<S>(0, Srt)), fabsf(d - off<S>(n - 1, Srt)));
+    mn = fabsf(d - off<S>(0, Srt));
+    if constexpr (S > 0) {
+#pragma unroll
+        for (int i = 1; i < S; ++i) mn = fminf(mn, fabsf(d - off<S>(i, Srt)));
+    } else {
+        for (int i = 1; i < n; ++i) mn = fminf(mn, fabsf(d - off<S>(i, Srt)));
+    }
+}
+
+// number of the S^3 sub-samples inside the ball, d = (sx^2 + sy^2) + sz^2 < r2
+template <int S>
+__device__ __forceinline__ int subsample_count(float dx, float dy, float dz, float r2, int Srt) {
+    int c = 0;
+    if constexpr (S > 0) {
+        float x2[S], y2[S], z2[S];
+#pragma unroll
+        for (int i = 0; i < S; ++i) {
+            const float sx = dx - off<S>(i, Srt), sy = dy - off<S>(i, Srt),
+                        sz = dz - off<S>(i, Srt);
+            x2[i] = sx * sx;
+            y2[i] = sy * sy;
+            z2[i] = sz * sz;
+        }
+#pragma unroll
+        for (int i = 0; i < S; ++i)
+#pragma unroll
+            for (int j = 0; j < S; ++j) {
+                const float t = x2[i] + y2[j];
+#pragma unroll
+                for (int k = 0; k < S; ++k) c += (t + z2[k] < r2) ? 1 : 0;
+            }
+    } else {
+        for (int i = 0; i < Srt; ++i) {
+            const float sx = dx - off<S>(i, Srt);
+            for (int j = 0; j < Srt; ++j) {
+                const float sy = dy - off<S>(j, Srt);
+                const float t = sx * sx + sy * sy;
+                for (int k = 0; k < Srt; ++k) {
+                    const float sz = dz - off<S>(k, Srt);
+                    c += (t + sz * sz < r2) ? 1 : 0;
+                }
+            }
+        }
+    }
+    return c;
+}
+
+// lanes < cnt count and deposit ring entries head + lane
+template <int S>
+__device__ __forceinline__ void drain(const DepositArgs &a, StraddleRing &Q, float *acc,
+                                      uint32_t head, uint32_t cnt, int lane) {
+    if ((uint32_t)lane < cnt) {
+        const uint32_t e = (head + lane) % QCAP;
+        const int c = subsample_count<S>(Q.dx[e], Q.dy[e], Q.dz[e], Q.r2[e], a.S);
+        if (c) lds_add(acc + Q.li[e], Q.dens[e] * a.tbl[c]);
+    }
+}
+
+// one ball image (radius >= half a voxel) cut to the tile [X0, X0+TX) x
+// [Y0, Y0+TY) x [Z0, Z0+TZ), deposited by the whole wave into acc
+template <int S>
+__device__ void tile_image(const DepositArgs &a, StraddleRing &Q, float *acc, uint32_t &head,
+                           uint32_t &tail, int lane, float x, float y, float z, float w, float r,
+                           float full, int X0, int Y0, int Z0) {
     const float ppu = a.ppu;
     const float o = r * ppu;
     const float r2 = o * o;
     const float vol = 4.0f / 3.0f * 3.14159265358979f * o * o * o;
+    const float dens = w / vol;
+    const float vfull = dens * full;
     const float xw = x * ppu, yw = y * ppu;
-    const float fS = (float)a.S;
-    const float full = a.tbl[a.S3];
-    int64_t s_lo = 0, s_hi = 0;
-    if (a.mode == 0) {
-        const float zl = floorf((z - r) * ppu) - 2.0f, zh = ceilf((z + r) * ppu) + 2.0f;
-        s_lo = (int64_t)fminf(fmaxf(zl, 0.0f), (float)a.nz);
-        s_hi = (int64_t)fmaxf(fminf(zh, (float)(a.nz - 1)), -1.0f);
-    }
-    for (int64_t s = s_lo; s <= s_hi; ++s) {
-        float depth, lower, upper;
-        plane(a.mode, s, ppu, depth, lower, upper);
+    int s_lo, s_hi;
+    slice_range(a, z, r, s_lo, s_hi);
+    s_lo = max(s_lo, Z0);
+    s_hi = min(s_hi, min(Z0 + TZ, a.nz) - 1);
+    const int gxe = min(X0 + TX, a.gx), gye = min(Y0 + TY, a.gy);
+    for (int s = s_lo; s <= s_hi; ++s) {
+        const float depth = a.planes[3 * s];
         const float zoff = z - depth;
         if (ppu * (r - fabsf(zoff)) + 1.0f < 0.0f) continue; // gl_ClipDistance
-        float dens, psize;
-        if (o < 0.5f) {
-            if (z <= lower || z > upper) continue;
-            dens = w;
-            psize = 1.0f;
-        } else {
-            const float pr = sqrtf(fmaxf(0.0f, r * r - zoff * zoff));
-            psize = 2.0f * ceilf(pr * ppu) + 2.0f;
-            dens = w / vol;
-        }
+        const float pr = sqrtf(fmaxf(0.0f, r * r - zoff * zoff));
+        const float psize = 2.0f * ceilf(pr * ppu) + 2.0f;
         int px0, px1, py0, py1;
-        sprite_range(xw, 0.5f * psize, a.gx, px0, px1);
-        sprite_range(yw, 0.5f * psize, a.gy, py0, py1);
+        sprite_range(xw, 0.5f * psize, gxe, px0, px1);
+        sprite_range(yw, 0.5f * psize, gye, py0, py1);
+        px0 = max(px0, X0);
+        py0 = max(py0, Y0);
         if (px1 < px0 || py1 < py0) continue;
         const int rw = px1 - px0 + 1;
-        const int nvox = rw * (py1 - py0 + 1);
+        const int nvox = rw * (py1 - py0 + 1); // <= TX * TY
+        const float rcp = 1.0f / (float)rw;
         const float dz = zoff * ppu + 0.5f;
         float zmn, zmx;
-        axis_range(dz, a.S, fS, zmn, zmx);
-        const uint64_t sbase = (uint64_t)a.gy * (uint64_t)s;
+        axis_range<S>(dz, a.S, zmn, zmx);
+        const float zmx2 = zmx * zmx, zmn2 = zmn * zmn;
+        const int lbase = (px0 - X0) + TX * ((py0 - Y0) + TY * (s - Z0));
         for (int c0 = 0; c0 < nvox; c0 += 64) {
             const int c = c0 + lane;
             const bool act = c < nvox;
-            const int ry = c / rw;
-            const int px = px0 + (c - ry * rw), py = py0 + ry;
-            const uint64_t gi = (uint64_t)px + (uint64_t)a.gx * ((uint64_t)py + sbase);
-            if (r2 < 0.25f) {
-                if (act) grid_add(a.grid, gi, dens);
-                continue;
-            }
-            const float dx = xw - (float)px, dy = yw - (float)py;
+            // row of voxel c: (c + 0.5) / rw is at least 0.5 / rw from an integer
+            const int ry = (int)(((float)c + 0.5f) * rcp);
+            const int cx = c - ry * rw;
+            const float dx = xw - (float)(px0 + cx), dy = yw - (float)(py0 + ry);
+            const int li = lbase + cx + TX * ry;
             float xmn, xmx, ymn, ymx;
-            axis_range(dx, a.S, fS, xmn, xmx);
-            axis_range(dy, a.S, fS, ymn, ymx);
-            const float dmax = xmx * xmx + ymx * ymx + zmx * zmx;
-            const float dmin = xmn * xmn + ymn * ymn + zmn * zmn;
-            if (act && dmax < r2) grid_add(a.grid, gi, dens * full);
-            const bool str = act && !(dmax < r2) && dmin < r2;
+            axis_range<S>(dx, a.S, xmn, xmx);
+            axis_range<S>(dy, a.S, ymn, ymx);
+            const bool inside = xmx * xmx + ymx * ymx + zmx2 < r2;
+            const bool reach = xmn * xmn + ymn * ymn + zmn2 < r2;
+            if (act && inside) lds_add(acc + li, vfull);
+            const bool str = act && reach && !inside;
             const uint64_t m = __ballot(str);
             if (!m) continue;
-            const int nstr = __popcll(m);
             if (str) {
-                const int p = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-                L.dx[p] = dx;
-                L.dy[p] = dy;
-                L.idx[p] = gi;
+                const uint32_t e =
+                    (tail + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))) %
+                    QCAP;
+                Q.dx[e] = dx;
+                Q.dy[e] = dy;
+                Q.dz[e] = dz;
+                Q.r2[e] = r2;
+                Q.dens[e] = dens;
+                Q.li[e] = (uint32_t)li;
             }
-            dev::wave_sync();
-            if (a.S3 <= 64) {
-                // V voxels per pass, S^3 lanes each
-                const uint64_t seg = a.S3 == 64 ? ~0ull : ((1ull << a.S3) - 1ull);
-                for (int e0 = 0; e0 < nstr; e0 += V) {
-                    const int e = e0 + slot;
-                    const bool ok = slot < V && e < nstr;
-                    bool in = false;
-                    if (ok) {
-                        const float sx = L.dx[e] - lxo, sy = L.dy[e] - lyo, sz = dz - lzo;
-                        in = sx * sx + sy * sy + sz * sz < r2;
-                    }
-                    const uint64_t b = __ballot(in);
-                    if (ok && sub == 0) {
-                        const int cnt = __popcll((b >> (slot * a.S3)) & seg);
-                        if (cnt) grid_add(a.grid, L.idx[e], dens * a.tbl[cnt]);
-                    }
-                }
-            } else {
-                for (int e = 0; e < nstr; ++e) {
-                    const float ex = L.dx[e], ey = L.dy[e];
-                    int cnt = 0;
-                    for (int t0 = 0; t0 < a.S3; t0 += 64) {
-                        const int t = t0 + lane;
-                        bool in = false;
-                        if (t < a.S3) {
-                            const int i = t / (a.S * a.S), j = (t / a.S) % a.S, k = t % a.S;
-                            const float sx = ex - ((float)i + 0.5f) / fS;
-                            const float sy = ey - ((float)j + 0.5f) / fS;
-                            const float sz = dz - ((float)k + 0.5f) / fS;
-                            in = sx * sx + sy * sy + sz * sz < r2;
-                        }
-                        cnt += __popcll(__ballot(in));
-                    }
-                    if (lane == 0 && cnt) grid_add(a.grid, L.idx[e], dens * a.tbl[cnt]);
-                }
+            tail += (uint32_t)__popcll(m);
+            if (tail - head >= 64) {
+                dev::wave_sync();
+                drain<S>(a, Q, acc, head, 64, lane);
+                head += 64;
+                dev::wave_sync();
             }
-            dev::wave_sync();
         }
     }
 }
 
-// a sub-pixel particle image: one voxel (the vertex stage's snap, triangle.vert:45-57)
-__device__ __forceinline__ void lane_image(const DepositArgs &a, float x, float y, float z, float w,
-                                           float r) {
-    const float ppu = a.ppu;
-    int64_t s = 0;
-    if (a.mode == 0) {
-        s = (int64_t)fminf(fmaxf(floorf(z * ppu), -2.0f), (float)a.nz) - 1;
-        float d, lo, up;
-        int t = 0;
-        for (; t < 3; ++t, ++s) {
-            if (s < 0 || s >= a.nz) continue;
-            plane(0, s, ppu, d, lo, up);
-            if (z > lo && z <= up) break;
-        }
-        if (t == 3) return;
-    }
-    float depth, lower, upper;
-    plane(a.mode, s, ppu, depth, lower, upper);
-    if (ppu * (r - fabsf(z - depth)) + 1.0f < 0.0f) return;
-    if (z <= lower || z > upper) return;
-    int px0, px1, py0, py1;
-    sprite_range(x * ppu, 0.5f, a.gx, px0, px1);
-    sprite_range(y * ppu, 0.5f, a.gy, py0, py1);
-    if (px1 < px0 || py1 < py0) return;
-    grid_add(a.grid, (uint64_t)px0 + (uint64_t)a.gx * ((uint64_t)py0 + (uint64_t)a.gy * s), w);
+// the image `im` (ia * 9 + ib * 3 + ic over the per-axis image lists) of ball p
+__device__ __forceinline__ void image_of(const DepositArgs &a, uint32_t p, uint32_t im, float &x,
+                                         float &y, float &z, float &w, float &r) {
+    r = a.r[p];
+    w = a.w[p];
+    float sx[3], sy[3], sz[3];
+    images(a.xyz[3 * (uint64_t)p], r, a.period[0], sx);
+    images(a.xyz[3 * (uint64_t)p + 1], r, a.period[1], sy);
+    images(a.xyz[3 * (uint64_t)p + 2], r, a.period[2], sz);
+    const uint32_t ia = im / 9, ib = (im / 3) % 3, ic = im % 3;
+    x = ia == 0 ? sx[0] : ia == 1 ? sx[1] : sx[2];
+    y = ib == 0 ? sy[0] : ib == 1 ? sy[1] : sy[2];
+    z = ic == 0 ? sz[0] : ic == 1 ? sz[1] : sz[2];
 }
 
-__global__ void __launch_bounds__(DB) deposit_kernel(DepositArgs a) {
-    __shared__ WaveLds lds[DB / 64];
+// pair lists.  COUNT: tile_count[t] += 1 per (ball image, tile); FILL: place
+// the pair at tile_off[t] + (--tile_count[t])
+template <bool FILL>
+__device__ __forceinline__ void emit(const DepositArgs &a, uint32_t t, uint64_t pair) {
+    if constexpr (FILL) {
+        const uint32_t pos = atomicSub(a.tile_count + t, 1u) - 1u;
+        a.pairs[a.tile_off[t] + pos] = pair;
+    } else {
+        atomicAdd(a.tile_count + t, 1u);
+    }
+}
+
+template <bool FILL> __global__ void __launch_bounds__(DB) deposit_pairs_kernel(DepositArgs a) {
+    const uint64_t i = (uint64_t)blockIdx.x * DB + threadIdx.x;
+    const bool valid = i < a.n;
+    const uint32_t p = (uint32_t)i;
+    float r = 0.0f, x = 0.0f, y = 0.0f, z = 0.0f;
+    if (valid) {
+        r = a.r[p];
+        x = a.xyz[3 * i];
+        y = a.xyz[3 * i + 1];
+        z = a.xyz[3 * i + 2];
+    }
+    const bool ball = valid && !(r * a.ppu < 0.5f); // sub-voxel balls: deposit_tiny_kernel
+    float sx[3], sy[3], sz[3];
+    int nx = 0, ny = 0, nzi = 0;
+    if (ball) {
+        nx = images(x, r, a.period[0], sx);
+        ny = images(y, r, a.period[1], sy);
+        nzi = images(z, r, a.period[2], sz);
+    }
+    uint32_t big = 0; // images with more than 64 tiles: enumerated by the whole wave
+    for (int ia = 0; ia < nx; ++ia)
+        for (int ib = 0; ib < ny; ++ib)
+            for (int ic = 0; ic < nzi; ++ic) {
+                int tx0, tx1, ty0, ty1, tz0, tz1;
+                if (!tile_box(a, sx[ia], sy[ib], sz[ic], r, tx0, tx1, ty0, ty1, tz0, tz1))
+                    continue;
+                const uint32_t im = ia * 9 + ib * 3 + ic;
+                const int nt = (tx1 - tx0 + 1) * (ty1 - ty0 + 1) * (tz1 - tz0 + 1);
+                if (nt > 64) {
+                    big |= 1u << im;
+                    continue;
+                }
+                const uint64_t pair = (uint64_t)p | ((uint64_t)im << 32);
+                for (int tz = tz0; tz <= tz1; ++tz)
+                    for (int ty = ty0; ty <= ty1; ++ty)
+                        for (int tx = tx0; tx <= tx1; ++tx)
+                            emit<FILL>(a, (uint32_t)(tx + a.ntx * (ty + a.nty * tz)), pair);
+            }
     const int lane = threadIdx.x & 63;
-    WaveLds &L = lds[threadIdx.x >> 6];
-    // this lane's sub-sample for the S^3 <= 64 path: voxel slot `slot`, sample `sub`
-    const int S = a.S, S3 = a.S3;
-    const int V = S3 <= 64 ? 64 / S3 : 1;
-    const int slot = S3 <= 64 ? lane / S3 : 0, sub = S3 <= 64 ? lane % S3 : 0;
-    const float fS = (float)S;
-    const float lxo = ((float)(sub / (S * S)) + 0.5f) / fS;
-    const float lyo = ((float)((sub / S) % S) + 0.5f) / fS;
-    const float lzo = ((float)(sub % S) + 0.5f) / fS;
-    for (;;) {
-        uint32_t g = 0;
-        if (lane == 0) g = atomicAdd(a.work, 1u);
-        g = __builtin_amdgcn_readfirstlane(__shfl(g, 0));
-        const uint64_t base = (uint64_t)g * 64u;
-        if (base >= a.n) break;
-        const uint64_t i = base + lane;
-        const bool valid = i < a.n;
-        float x = 0.0f, y = 0.0f, z = 0.0f, w = 0.0f, r = 0.0f;
-        if (valid) {
-            x = a.xyz[3 * i];
-            y = a.xyz[3 * i + 1];
-            z = a.xyz[3 * i + 2];
-            w = a.w[i];
-            r = a.r[i];
-        }
-        const bool tiny = valid && r * a.ppu < 0.5f;
-        if (tiny) {
-            float sx[3], sy[3], sz[3];
-            const int nx = images(x, r, a.period[0], sx), ny = images(y, r, a.period[1], sy),
-                      nzi = images(z, r, a.period[2], sz);
-            for (int ia = 0; ia < nx; ++ia)
-                for (int ib = 0; ib < ny; ++ib)
-                    for (int ic = 0; ic < nzi; ++ic) lane_image(a, sx[ia], sy[ib], sz[ic], w, r);
-        }
-        uint64_t big = __ballot(valid && !tiny);
-        while (big) {
-            const int l = __builtin_ctzll(big);
-            big &= big - 1;
-            const float bx = __shfl(x, l), by = __shfl(y, l), bz = __shfl(z, l);
-            const float bw = __shfl(w, l), br = __shfl(r, l);
-            float sx[3], sy[3], sz[3];
-            const int nx = images(bx, br, a.period[0], sx), ny = images(by, br, a.period[1], sy),
-                      nzi = images(bz, br, a.period[2], sz);
-            for (int ia = 0; ia < nx; ++ia)
-                for (int ib = 0; ib < ny; ++ib)
-                    for (int ic = 0; ic < nzi; ++ic)
-                        wave_image(a, L, lane, sx[ia], sy[ib], sz[ic], bw, br, lxo, lyo, lzo, slot,
-                                   sub, V);
+    uint64_t todo = __ballot(big != 0);
+    while (todo) {
+        const int l = __builtin_ctzll(todo);
+        const uint32_t bl = (uint32_t)__shfl((int)big, l);
+        const uint32_t im = (uint32_t)__builtin_ctz(bl);
+        if (lane == l) big &= big - 1;
+        if (!__shfl((int)(big != 0), l)) todo &= todo - 1;
+        const uint32_t bp = (uint32_t)__shfl((int)p, l);
+        float bx, by, bz, bw, br;
+        image_of(a, bp, im, bx, by, bz, bw, br);
+        int tx0, tx1, ty0, ty1, tz0, tz1;
+        tile_box(a, bx, by, bz, br, tx0, tx1, ty0, ty1, tz0, tz1);
+        const int wx = tx1 - tx0 + 1, wy = ty1 - ty0 + 1;
+        const int nt = wx * wy * (tz1 - tz0 + 1);
+        const uint64_t pair = (uint64_t)bp | ((uint64_t)im << 32);
+        for (int j = lane; j < nt; j += 64) {
+            const int tz = tz0 + j / (wx * wy), rem = j % (wx * wy);
+            const int ty = ty0 + rem / wx, tx = tx0 + rem % wx;
+            emit<FILL>(a, (uint32_t)(tx + a.ntx * (ty + a.nty * tz)), pair);
         }
     }
+}
+
+template <int S> __global__ void __launch_bounds__(DB) deposit_tile_kernel(DepositArgs a) {
+    __shared__ float acc[TVOX];
+    __shared__ StraddleRing rings[DB / 64];
+    __shared__ uint32_t sh_tile, sh_next;
+    const int lane = threadIdx.x & 63;
+    StraddleRing &Q = rings[threadIdx.x >> 6];
+    const int S3 = S ? S * S * S : a.S * a.S * a.S;
+    const float full = a.tbl[S3];
+    const uint32_t ntiles = (uint32_t)(a.ntx * a.nty * a.ntz);
+    for (;;) {
+        if (threadIdx.x == 0) {
+            sh_tile = atomicAdd(a.work, 1u);
+            sh_next = 0;
+        }
+        for (int v = threadIdx.x; v < TVOX; v += DB) acc[v] = 0.0f;
+        __syncthreads();
+        const uint32_t t = sh_tile;
+        if (t >= ntiles) break;
+        const int tx = (int)(t % a.ntx), ty = (int)((t / a.ntx) % a.nty), tz = (int)(t / (a.ntx * a.nty));
+        const int X0 = tx * TX, Y0 = ty * TY, Z0 = tz * TZ;
+        const uint64_t beg = a.tile_off[t], cnt = a.tile_off[t + 1] - beg;
+        uint32_t head = 0, tail = 0;
+        for (;;) {
+            uint32_t j = 0;
+            if (lane == 0) j = atomicAdd(&sh_next, 1u);
+            j = __builtin_amdgcn_readfirstlane(__shfl(j, 0));
+            if (j >= cnt) break;
+            const uint64_t pair = a.pairs[beg + j];
+            float x, y, z, w, r;
+            image_of(a, (uint32_t)pair, (uint32_t)(pair >> 32), x, y, z, w, r);
+            tile_image<S>(a, Q, acc, head, tail, lane, x, y, z, w, r, full, X0, Y0, Z0);
+        }
+        dev::wave_sync();
+        drain<S>(a, Q, acc, head, tail - head, lane);
+        __syncthreads();
+        // the finished tile: one plain store per voxel (rows of 32 floats)
+        for (int v = threadIdx.x; v < TVOX; v += DB) {
+            const int lx = v % TX, ly = (v / TX) % TY, lz = v / (TX * TY);
+            const int px = X0 + lx, py = Y0 + ly, s = Z0 + lz;
+            if (px < a.gx && py < a.gy && s < a.nz) {
+                const uint64_t gi = (uint64_t)px + (uint64_t)a.gx * ((uint64_t)py + (uint64_t)a.gy * s);
+                a.grid[gi] = a.accumulate ? a.grid[gi] + acc[v] : acc[v];
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// sub-voxel balls: one lane each, one voxel per image (global atomics, after the tiles)
+__global__ void __launch_bounds__(DB) deposit_tiny_kernel(DepositArgs a) {
+    const uint64_t p = (uint64_t)blockIdx.x * DB + threadIdx.x;
+    if (p >= a.n) return;
+    const float r = a.r[p], ppu = a.ppu;
+    if (!(r * ppu < 0.5f)) return;
+    const float x = a.xyz[3 * p], y = a.xyz[3 * p + 1], z = a.xyz[3 * p + 2], w = a.w[p];
+    float sx[3], sy[3], sz[3];
+    const int nx = images(x, r, a.period[0], sx), ny = images(y, r, a.period[1], sy),
+              nzi = images(z, r, a.period[2], sz);
+    for (int ic = 0; ic < nzi; ++ic) {
+        const float zz = sz[ic];
+        // the slice with lower < z <= upper (only those pass the snap test)
+        int s = 0;
+        if (a.mode == 0) {
+            int c = (int)fminf(fmaxf(floorf(zz * ppu), -2.0f), (float)a.nz) - 1;
+            int t3 = 0;
+            for (; t3 < 3; ++t3, ++c)
+                if (c >= 0 && c < a.nz && zz > a.planes[3 * c + 1] && zz <= a.planes[3 * c + 2])
+                    break;
+            if (t3 == 3) continue;
+            s = c;
+        }
+        const float depth = a.planes[3 * s], lower = a.planes[3 * s + 1],
+                    upper = a.planes[3 * s + 2];
+        if (ppu * (r - fabsf(zz - depth)) + 1.0f < 0.0f) continue;
+        if (zz <= lower || zz > upper) continue;
+        for (int ia = 0; ia < nx; ++ia)
+            for (int ib = 0; ib < ny; ++ib) {
+                int px0, px1, py0, py1;
+                sprite_range(sx[ia] * ppu, 0.5f, a.gx, px0, px1);
+                sprite_range(sy[ib] * ppu, 0.5f, a.gy, py0, py1);
+                if (px1 < px0 || py1 < py0) continue;
+                unsafeAtomicAdd(a.grid + (uint64_t)px0 +
+                                    (uint64_t)a.gx * ((uint64_t)py0 + (uint64_t)a.gy * s),
+                                w);
+            }
+    }
+}
+
+// exclusive scan of n uint32 counts into uint64 offsets (out[n] = total):
+// 1024-element blocks, then the block sums by one block, then the carry-in
+constexpr int SB = 1024;
+__device__ __forceinline__ uint64_t block_incl_scan(uint64_t v, uint64_t *wsum) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint64_t u = __shfl_up(v, o, 64);
+        if (lane >= o) v += u;
+    }
+    if (lane == 63) wsum[wv] = v;
+    __syncthreads();
+    if (threadIdx.x < 64) {
+        uint64_t s = threadIdx.x < SB / 64 ? wsum[threadIdx.x] : 0;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint64_t u = __shfl_up(s, o, 64);
+            if ((int)threadIdx.x >= o) s += u;
+        }
+        if (threadIdx.x < SB / 64) wsum[threadIdx.x] = s;
+    }
+    __syncthreads();
+    const uint64_t r = v + (wv ? wsum[wv - 1] : 0);
+    __syncthreads();
+    return r;
+}
+
+__global__ void __launch_bounds__(SB) scan_blocks_kernel(const uint32_t *in, uint64_t n,
+                                                         uint64_t *out, uint64_t *bsum) {
+    __shared__ uint64_t wsum[SB / 64];
+    const uint64_t i = (uint64_t)blockIdx.x * SB + threadIdx.x;
+    const uint64_t v = i < n ? in[i] : 0;
+    const uint64_t inc = block_incl_scan(v, wsum);
+    if (i <= n) out[i] = inc - v;
+    if (threadIdx.x == SB - 1) bsum[blockIdx.x] = inc;
+}
+
+__global__ void __launch_bounds__(SB) scan_sums_kernel(uint64_t *bsum, uint32_t nb) {
+    __shared__ uint64_t wsum[SB / 64];
+    uint64_t carry = 0;
+    for (uint32_t b0 = 0; b0 < nb; b0 += SB) {
+        const uint32_t b = b0 + threadIdx.x;
+        const uint64_t v = b < nb ? bsum[b] : 0;
+        const uint64_t inc = block_incl_scan(v, wsum);
+        if (b < nb) bsum[b] = carry + inc - v;
+        carry += wsum[SB / 64 - 1]; // the chunk's total
+        __syncthreads();
+    }
+}
+
+__global__ void __launch_bounds__(SB) scan_add_kernel(uint64_t *out, uint64_t n,
+                                                      const uint64_t *bsum) {
+    const uint64_t i = (uint64_t)blockIdx.x * SB + threadIdx.x;
+    if (i <= n) out[i] += bsum[blockIdx.x];
+}
+
+// one workspace per device for the deposit's scratch (held for the whole call)
+Workspace &deposit_ws(int dev, std::unique_lock<std::mutex> &lk) {
+    static std::mutex mu;
+    static std::map<int, Workspace *> ws;
+    lk = std::unique_lock<std::mutex>(mu);
+    Workspace *&w = ws[dev];
+    if (!w) w = new Workspace();
+    return *w;
+}
+
+template <int S> void launch_tiles(const DepositArgs &a, uint64_t blocks, hipStream_t s) {
+    deposit_tile_kernel<S><<<(unsigned)blocks, DB, 0, s>>>(a);
 }
 
 } // namespace
@@ -303,67 +535,128 @@ nbkd_status deposit(const float *xyz, const float *weight, const float *radius, 
     const uint64_t cells = (uint64_t)gx * (uint64_t)gy * (uint64_t)nz;
     const bool in_dev = flags & NBKD_INPUT_DEVICE, out_dev = flags & NBKD_OUTPUT_DEVICE;
     const bool accumulate = flags & NBKD_ACCUMULATE;
-    if ((n + 63) / 64 >= (1ull << 32)) {
-        set_error("nbkd_deposit: too many particles per call");
+    if (n >= (1ull << 32)) {
+        set_error("nbkd_deposit: at most 2^32 - 1 particles per call");
         return NBKD_EINVAL;
     }
-    DevBuf bx, bw, br, bg, bt, bc;
+    const int ntx = (gx + TX - 1) / TX, nty = (gy + TY - 1) / TY, ntz = (nz + TZ - 1) / TZ;
+    const uint64_t ntiles = (uint64_t)ntx * nty * ntz;
+    if (ntiles >= (1ull << 31)) {
+        set_error("nbkd_deposit: grid too large");
+        return NBKD_EINVAL;
+    }
+    int dev = 0, cus = 256;
+    NBKD_HIP(hipGetDevice(&dev));
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    std::unique_lock<std::mutex> lk;
+    Workspace &ws = deposit_ws(dev, lk);
     const float *dx = xyz, *dw = weight, *dr = radius;
     if (!in_dev && n) {
-        NBKD_HIP(bx.alloc(n * 12, s));
-        NBKD_HIP(bw.alloc(n * 4, s));
-        NBKD_HIP(br.alloc(n * 4, s));
-        NBKD_HIP(hipMemcpyAsync(bx.p, xyz, n * 12, hipMemcpyHostToDevice, s));
-        NBKD_HIP(hipMemcpyAsync(bw.p, weight, n * 4, hipMemcpyHostToDevice, s));
-        NBKD_HIP(hipMemcpyAsync(br.p, radius, n * 4, hipMemcpyHostToDevice, s));
-        dx = bx.as<float>();
-        dw = bw.as<float>();
-        dr = br.as<float>();
+        float *b = (float *)ws.get(WS_Q, n * 20, s);
+        if (!b) return NBKD_ENOMEM;
+        NBKD_HIP(hipMemcpyAsync(b, xyz, n * 12, hipMemcpyHostToDevice, s));
+        NBKD_HIP(hipMemcpyAsync(b + 3 * n, weight, n * 4, hipMemcpyHostToDevice, s));
+        NBKD_HIP(hipMemcpyAsync(b + 4 * n, radius, n * 4, hipMemcpyHostToDevice, s));
+        dx = b;
+        dw = b + 3 * n;
+        dr = b + 4 * n;
     }
     float *dg = out;
     if (!out_dev) {
-        NBKD_HIP(bg.alloc(cells * 4, s));
-        dg = bg.as<float>();
+        dg = (float *)ws.get(WS_OUTD, cells * 4, s);
+        if (!dg) return NBKD_ENOMEM;
         if (accumulate) NBKD_HIP(hipMemcpyAsync(dg, out, cells * 4, hipMemcpyHostToDevice, s));
     }
-    if (!accumulate) NBKD_HIP(hipMemsetAsync(dg, 0, cells * 4, s));
-    // overlap after c float additions of 1 / S^3 (triangle.frag:16,39)
+    // small tables: overlap after c float additions of 1 / S^3 (triangle.frag:16,39),
+    // slice planes (point_renderer.cpp:878-880; 2-D: depth 0, bounds +-0.5), counter
     const int S3 = S * S * S;
-    std::vector<float> tbl(S3 + 1);
+    std::vector<float> host((size_t)S3 + 1 + 3 * (size_t)nz + 1);
     {
         const float inc = 1.0f / (float)S3;
         float acc = 0.0f;
-        tbl[0] = 0.0f;
-        for (int c = 1; c <= S3; ++c) tbl[c] = (acc += inc);
+        host[0] = 0.0f;
+        for (int c = 1; c <= S3; ++c) host[c] = (acc += inc);
+        float *pl = host.data() + S3 + 1;
+        for (int i = 0; i < nz; ++i) {
+            if (mode == 1) {
+                pl[3 * i] = 0.0f;
+                pl[3 * i + 1] = -0.5f;
+                pl[3 * i + 2] = 0.5f;
+            } else {
+                pl[3 * i] = (float)(((double)i + 0.5) / (double)ppu);
+                pl[3 * i + 1] = (float)((double)i / (double)ppu);
+                pl[3 * i + 2] = (float)((double)(i + 1) / (double)ppu);
+            }
+        }
+        host.back() = 0.0f; // tile counter
     }
-    NBKD_HIP(bt.alloc(tbl.size() * 4, s));
-    NBKD_HIP(hipMemcpyAsync(bt.p, tbl.data(), tbl.size() * 4, hipMemcpyHostToDevice, s));
-    NBKD_HIP(bc.alloc(4, s));
-    NBKD_HIP(hipMemsetAsync(bc.p, 0, 4, s));
-    if (n) {
-        DepositArgs a;
-        a.xyz = dx;
-        a.w = dw;
-        a.r = dr;
-        a.n = n;
-        a.gx = gx;
-        a.gy = gy;
-        a.nz = nz;
-        a.ppu = ppu;
-        for (int d = 0; d < 3; ++d) a.period[d] = period ? period[d] : -1.0f;
-        a.S = S;
-        a.S3 = S3;
-        a.mode = mode;
-        a.tbl = bt.as<float>();
-        a.grid = dg;
-        a.work = bc.as<uint32_t>();
-        int dev = 0, cus = 256;
-        NBKD_HIP(hipGetDevice(&dev));
-        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        const uint64_t groups = (n + 63) / 64;
-        const uint64_t blocks = std::min<uint64_t>((groups + 3) / 4, (uint64_t)cus * 8);
+    float *dtab = (float *)ws.get(WS_TMP, host.size() * 4, s);
+    uint32_t *tcount = (uint32_t *)ws.get(WS_COUNT, ntiles * 4, s);
+    uint64_t *toff = (uint64_t *)ws.get(WS_OFF, (ntiles + 1) * 8, s);
+    const uint32_t nsb = (uint32_t)((ntiles + 1 + SB - 1) / SB);
+    uint64_t *bsum = (uint64_t *)ws.get(WS_SUMS, (size_t)nsb * 8, s);
+    if (!dtab || !tcount || !toff || !bsum) return NBKD_ENOMEM;
+    NBKD_HIP(hipMemcpyAsync(dtab, host.data(), host.size() * 4, hipMemcpyHostToDevice, s));
+    NBKD_HIP(hipMemsetAsync(tcount, 0, ntiles * 4, s));
+    DepositArgs a;
+    a.xyz = dx;
+    a.w = dw;
+    a.r = dr;
+    a.n = n;
+    a.gx = gx;
+    a.gy = gy;
+    a.nz = nz;
+    a.ntx = ntx;
+    a.nty = nty;
+    a.ntz = ntz;
+    a.ppu = ppu;
+    for (int d = 0; d < 3; ++d) a.period[d] = period ? period[d] : -1.0f;
+    a.S = S;
+    a.mode = mode;
+    a.accumulate = accumulate;
+    a.tbl = dtab;
+    a.planes = dtab + S3 + 1;
+    a.grid = dg;
+    a.tile_count = tcount;
+    a.tile_off = toff;
+    a.pairs = nullptr;
+    a.work = (uint32_t *)(dtab + host.size() - 1);
+    const unsigned nb = (unsigned)std::max<uint64_t>((n + DB - 1) / DB, 1);
+    {
+        TimedScope ts("deposit_pairs", s);
+        if (n) deposit_pairs_kernel<false><<<nb, DB, 0, s>>>(a);
+        scan_blocks_kernel<<<nsb, SB, 0, s>>>(tcount, ntiles, toff, bsum);
+        scan_sums_kernel<<<1, SB, 0, s>>>(bsum, nsb);
+        scan_add_kernel<<<nsb, SB, 0, s>>>(toff, ntiles, bsum);
+        NBKD_HIP(hipGetLastError());
+    }
+    uint64_t npairs = 0;
+    NBKD_HIP(hipMemcpyAsync(&npairs, toff + ntiles, 8, hipMemcpyDeviceToHost, s));
+    NBKD_HIP(hipStreamSynchronize(s));
+    a.pairs = (uint64_t *)ws.get(WS_CAND, std::max<uint64_t>(npairs, 1) * 8, s);
+    if (!a.pairs) return NBKD_ENOMEM;
+    {
+        TimedScope ts("deposit_fill", s);
+        if (npairs) deposit_pairs_kernel<true><<<nb, DB, 0, s>>>(a);
+        NBKD_HIP(hipGetLastError());
+    }
+    {
+        // persistent blocks over the tiles: 44 KB of LDS each, 3 per CU
+        const uint64_t blocks = std::min<uint64_t>(ntiles, (uint64_t)cus * 3);
         TimedScope ts("deposit", s);
-        deposit_kernel<<<(unsigned)blocks, DB, 0, s>>>(a);
+        switch (S) {
+        case 1: launch_tiles<1>(a, blocks, s); break;
+        case 2: launch_tiles<2>(a, blocks, s); break;
+        case 3: launch_tiles<3>(a, blocks, s); break;
+        case 4: launch_tiles<4>(a, blocks, s); break;
+        case 5: launch_tiles<5>(a, blocks, s); break;
+        default: launch_tiles<0>(a, blocks, s); break;
+        }
+        NBKD_HIP(hipGetLastError());
+    }
+    if (n) {
+        TimedScope ts("deposit_tiny", s);
+        deposit_tiny_kernel<<<nb, DB, 0, s>>>(a);
         NBKD_HIP(hipGetLastError());
     }
     if (!out_dev) {

@@ -186,6 +186,11 @@ nbkd_status query_ball_count(const Tree &t, const float *q, uint64_t m, float r,
 nbkd_status query_ball_csr(const Tree &t, const float *q, uint64_t m, float r, uint64_t *offsets,
                            uint32_t *out_idx, uint64_t capacity, uint32_t flags, hipStream_t s);
 
+// query.hip: LSD radix sort of (key, value) pairs by the low nbits of the keys,
+// ping-ponging (k0, v0) <-> (k1, v1); *vout = the buffer holding the sorted values
+nbkd_status sort_pairs(Workspace &ws, uint32_t *k0, uint32_t *v0, uint32_t *k1, uint32_t *v1,
+                       uint32_t n, int nbits, hipStream_t s, uint32_t **vout);
+
 // deposit.hip: spheres onto a voxel grid (render_points_volume / render_points)
 nbkd_status deposit(const float *xyz, const float *weight, const float *radius, uint64_t n, int gx,
                     int gy, int nz, float ppu, const float *period, int S, int mode, float *out,

@@ -830,6 +830,12 @@ nbkd_status stage_queries(const Tree &t, const float *q, uint64_t m, uint32_t fl
 
 } // namespace
 
+// LSD radix sort of (key, value) pairs for other translation units (deposit.hip)
+nbkd_status sort_pairs(Workspace &ws, uint32_t *k0, uint32_t *v0, uint32_t *k1, uint32_t *v1,
+                       uint32_t n, int nbits, hipStream_t s, uint32_t **vout) {
+    return radix_sort(ws, k0, v0, k1, v1, n, nbits, s, vout);
+}
+
 namespace {
 
 bool collect_disabled() {
