@@ -49,7 +49,7 @@
 namespace nbkd {
 namespace {
 
-constexpr int DB = 256; // threads per block (4 waves)
+constexpr int DB = 512; // threads per block (8 waves; two blocks per CU share the LDS)
 constexpr int TX = 32, TY = 32, TZ = 8;
 constexpr int TVOX = TX * TY * TZ;
 constexpr int QCAP = 128; // straddling voxels queued per wave
@@ -194,20 +194,24 @@ __device__ __forceinline__ int subsample_count(float dx, float dy, float dz, flo
 // lanes < cnt count and deposit ring entries head + lane
 template <int S>
 __device__ __forceinline__ void drain(const DepositArgs &a, StraddleRing &Q, float *acc,
-                                      uint32_t head, uint32_t cnt, int lane) {
+                                      const float *tbl, uint32_t head, uint32_t cnt, int lane) {
     if ((uint32_t)lane < cnt) {
         const uint32_t e = (head + lane) % QCAP;
         const int c = subsample_count<S>(Q.dx[e], Q.dy[e], Q.dz[e], Q.r2[e], a.S);
-        if (c) lds_add(acc + Q.li[e], Q.dens[e] * a.tbl[c]);
+        if (c) lds_add(acc + Q.li[e], Q.dens[e] * tbl[c]);
     }
 }
 
 // one ball image (radius >= half a voxel) cut to the tile [X0, X0+TX) x
-// [Y0, Y0+TY) x [Z0, Z0+TZ), deposited by the whole wave into acc
+// [Y0, Y0+TY) x [Z0, Z0+TZ), deposited by the whole wave into acc.  Lane k
+// first takes slice s_lo + k (clip test, sprite rectangle, z terms); the wave
+// then sweeps the union of those rectangles 64 (x, y) columns at a time, each
+// lane computing its column's x / y terms once and walking the slices.
 template <int S>
-__device__ void tile_image(const DepositArgs &a, StraddleRing &Q, float *acc, uint32_t &head,
-                           uint32_t &tail, int lane, float x, float y, float z, float w, float r,
-                           float full, int X0, int Y0, int Z0) {
+__device__ void tile_image(const DepositArgs &a, StraddleRing &Q, float *acc, const float *tbl,
+                           const float *depth, uint32_t &head, uint32_t &tail, int lane, float x,
+                           float y, float z, float w, float r, float full, int X0, int Y0,
+                           int Z0) {
     const float ppu = a.ppu;
     const float o = r * ppu;
     const float r2 = o * o;
@@ -219,42 +223,70 @@ __device__ void tile_image(const DepositArgs &a, StraddleRing &Q, float *acc, ui
     slice_range(a, z, r, s_lo, s_hi);
     s_lo = max(s_lo, Z0);
     s_hi = min(s_hi, min(Z0 + TZ, a.nz) - 1);
+    const int ns = s_hi - s_lo + 1;
+    if (ns <= 0) return;
     const int gxe = min(X0 + TX, a.gx), gye = min(Y0 + TY, a.gy);
-    for (int s = s_lo; s <= s_hi; ++s) {
-        const float depth = a.planes[3 * s];
-        const float zoff = z - depth;
-        if (ppu * (r - fabsf(zoff)) + 1.0f < 0.0f) continue; // gl_ClipDistance
-        const float pr = sqrtf(fmaxf(0.0f, r * r - zoff * zoff));
-        const float psize = 2.0f * ceilf(pr * ppu) + 2.0f;
-        int px0, px1, py0, py1;
-        sprite_range(xw, 0.5f * psize, gxe, px0, px1);
-        sprite_range(yw, 0.5f * psize, gye, py0, py1);
-        px0 = max(px0, X0);
-        py0 = max(py0, Y0);
-        if (px1 < px0 || py1 < py0) continue;
-        const int rw = px1 - px0 + 1;
-        const int nvox = rw * (py1 - py0 + 1); // <= TX * TY
-        const float rcp = 1.0f / (float)rw;
-        const float dz = zoff * ppu + 0.5f;
-        float zmn, zmx;
-        axis_range<S>(dz, a.S, zmn, zmx);
-        const float zmx2 = zmx * zmx, zmn2 = zmn * zmn;
-        const int lbase = (px0 - X0) + TX * ((py0 - Y0) + TY * (s - Z0));
-        for (int c0 = 0; c0 < nvox; c0 += 64) {
-            const int c = c0 + lane;
-            const bool act = c < nvox;
-            // row of voxel c: (c + 0.5) / rw is at least 0.5 / rw from an integer
-            const int ry = (int)(((float)c + 0.5f) * rcp);
-            const int cx = c - ry * rw;
-            const float dx = xw - (float)(px0 + cx), dy = yw - (float)(py0 + ry);
-            const int li = lbase + cx + TX * ry;
-            float xmn, xmx, ymn, ymx;
-            axis_range<S>(dx, a.S, xmn, xmx);
-            axis_range<S>(dy, a.S, ymn, ymx);
-            const bool inside = xmx * xmx + ymx * ymx + zmx2 < r2;
-            const bool reach = xmn * xmn + ymn * ymn + zmn2 < r2;
-            if (act && inside) lds_add(acc + li, vfull);
-            const bool str = act && reach && !inside;
+    // this lane's slice (lanes >= ns hold a copy of the last one, never used)
+    const int ks = s_lo + min(lane, ns - 1);
+    const float zoff = z - depth[ks - Z0];
+    const float pr = sqrtf(fmaxf(0.0f, r * r - zoff * zoff));
+    const float psize = 2.0f * ceilf(pr * ppu) + 2.0f;
+    int sx0, sx1, sy0, sy1;
+    sprite_range(xw, 0.5f * psize, gxe, sx0, sx1);
+    sprite_range(yw, 0.5f * psize, gye, sy0, sy1);
+    sx0 = max(sx0, X0);
+    sy0 = max(sy0, Y0);
+    const bool pass = lane < ns && !(ppu * (r - fabsf(zoff)) + 1.0f < 0.0f) && sx1 >= sx0 &&
+                      sy1 >= sy0; // gl_ClipDistance, sprite inside the tile
+    const uint64_t pm = __ballot(pass);
+    if (!pm) return;
+    const float dz = zoff * ppu + 0.5f;
+    float zmn, zmx;
+    axis_range<S>(dz, a.S, zmn, zmx);
+    const float zmn2 = zmn * zmn, zmx2 = zmx * zmx;
+    // union rectangle of the passing slices (lanes < TZ)
+    int ux0 = pass ? sx0 : 0x7FFFFFFF, uy0 = pass ? sy0 : 0x7FFFFFFF;
+    int ux1 = pass ? sx1 : -1, uy1 = pass ? sy1 : -1;
+#pragma unroll
+    for (int m = 1; m < TZ; m <<= 1) {
+        ux0 = min(ux0, __shfl_xor(ux0, m, 64));
+        uy0 = min(uy0, __shfl_xor(uy0, m, 64));
+        ux1 = max(ux1, __shfl_xor(ux1, m, 64));
+        uy1 = max(uy1, __shfl_xor(uy1, m, 64));
+    }
+    ux0 = __builtin_amdgcn_readfirstlane(ux0);
+    uy0 = __builtin_amdgcn_readfirstlane(uy0);
+    ux1 = __builtin_amdgcn_readfirstlane(ux1);
+    uy1 = __builtin_amdgcn_readfirstlane(uy1);
+    const int rw = ux1 - ux0 + 1;
+    const int ncol = rw * (uy1 - uy0 + 1); // <= TX * TY
+    const float rcp = 1.0f / (float)rw;
+    for (int c0 = 0; c0 < ncol; c0 += 64) {
+        const int c = c0 + lane;
+        const bool act = c < ncol;
+        // row of column c: (c + 0.5) / rw is at least 0.5 / rw from an integer
+        const int ry = (int)(((float)c + 0.5f) * rcp);
+        const int px = ux0 + (c - ry * rw), py = uy0 + ry;
+        const float dx = xw - (float)px, dy = yw - (float)py;
+        float xmn, xmx, ymn, ymx;
+        axis_range<S>(dx, a.S, xmn, xmx);
+        axis_range<S>(dy, a.S, ymn, ymx);
+        const float xy_mx = xmx * xmx + ymx * ymx, xy_mn = xmn * xmn + ymn * ymn;
+        const int li0 = (px - X0) + TX * (py - Y0);
+        uint64_t sl = pm;
+        while (sl) {
+            const int k = __builtin_ctzll(sl);
+            sl &= sl - 1;
+            const int kx0 = __builtin_amdgcn_readlane(sx0, k), kx1 = __builtin_amdgcn_readlane(sx1, k);
+            const int ky0 = __builtin_amdgcn_readlane(sy0, k), ky1 = __builtin_amdgcn_readlane(sy1, k);
+            const float kmx2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(zmx2), k));
+            const float kmn2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(zmn2), k));
+            const bool in = act && px >= kx0 && px <= kx1 && py >= ky0 && py <= ky1;
+            const bool inside = xy_mx + kmx2 < r2;
+            const bool reach = xy_mn + kmn2 < r2;
+            const int li = li0 + TX * TY * (s_lo + k - Z0);
+            if (in && inside) lds_add(acc + li, vfull);
+            const bool str = in && reach && !inside;
             const uint64_t m = __ballot(str);
             if (!m) continue;
             if (str) {
@@ -264,7 +296,7 @@ __device__ void tile_image(const DepositArgs &a, StraddleRing &Q, float *acc, ui
                     QCAP;
                 Q.dx[e] = dx;
                 Q.dy[e] = dy;
-                Q.dz[e] = dz;
+                Q.dz[e] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dz), k));
                 Q.r2[e] = r2;
                 Q.dens[e] = dens;
                 Q.li[e] = (uint32_t)li;
@@ -272,7 +304,7 @@ __device__ void tile_image(const DepositArgs &a, StraddleRing &Q, float *acc, ui
             tail += (uint32_t)__popcll(m);
             if (tail - head >= 64) {
                 dev::wave_sync();
-                drain<S>(a, Q, acc, head, 64, lane);
+                drain<S>(a, Q, acc, tbl, head, 64, lane);
                 head += 64;
                 dev::wave_sync();
             }
@@ -373,10 +405,15 @@ template <int S> __global__ void __launch_bounds__(DB) deposit_tile_kernel(Depos
     __shared__ float acc[TVOX];
     __shared__ StraddleRing rings[DB / 64];
     __shared__ uint32_t sh_tile, sh_next;
+    __shared__ float sh_depth[TZ];                   // the tile's slice depths
+    __shared__ float sh_tbl[S ? S * S * S + 1 : 1]; // overlap table (template S)
     const int lane = threadIdx.x & 63;
     StraddleRing &Q = rings[threadIdx.x >> 6];
     const int S3 = S ? S * S * S : a.S * a.S * a.S;
     const float full = a.tbl[S3];
+    if constexpr (S > 0)
+        for (int i = threadIdx.x; i <= S3; i += DB) sh_tbl[i] = a.tbl[i];
+    const float *tbl = S ? sh_tbl : a.tbl;
     const uint32_t ntiles = (uint32_t)(a.ntx * a.nty * a.ntz);
     for (;;) {
         if (threadIdx.x == 0) {
@@ -389,20 +426,40 @@ template <int S> __global__ void __launch_bounds__(DB) deposit_tile_kernel(Depos
         if (t >= ntiles) break;
         const int tx = (int)(t % a.ntx), ty = (int)((t / a.ntx) % a.nty), tz = (int)(t / (a.ntx * a.nty));
         const int X0 = tx * TX, Y0 = ty * TY, Z0 = tz * TZ;
+        if (threadIdx.x < TZ) sh_depth[threadIdx.x] = a.planes[3 * min(Z0 + (int)threadIdx.x, a.nz - 1)];
+        __syncthreads();
         const uint64_t beg = a.tile_off[t], cnt = a.tile_off[t + 1] - beg;
         uint32_t head = 0, tail = 0;
-        for (;;) {
+        // the next ball's record and coordinates are loaded while this one is swept
+        auto take = [&]() {
             uint32_t j = 0;
             if (lane == 0) j = atomicAdd(&sh_next, 1u);
-            j = __builtin_amdgcn_readfirstlane(__shfl(j, 0));
-            if (j >= cnt) break;
+            return __builtin_amdgcn_readfirstlane(__shfl(j, 0));
+        };
+        uint32_t j = take();
+        float x = 0.0f, y = 0.0f, z = 0.0f, w = 0.0f, r = 0.0f;
+        if (j < cnt) {
             const uint64_t pair = a.pairs[beg + j];
-            float x, y, z, w, r;
             image_of(a, (uint32_t)pair, (uint32_t)(pair >> 32), x, y, z, w, r);
-            tile_image<S>(a, Q, acc, head, tail, lane, x, y, z, w, r, full, X0, Y0, Z0);
+        }
+        while (j < cnt) {
+            const uint32_t jn = take();
+            float nx = 0.0f, ny = 0.0f, nz = 0.0f, nw = 0.0f, nr = 0.0f;
+            if (jn < cnt) {
+                const uint64_t pair = a.pairs[beg + jn];
+                image_of(a, (uint32_t)pair, (uint32_t)(pair >> 32), nx, ny, nz, nw, nr);
+            }
+            tile_image<S>(a, Q, acc, tbl, sh_depth, head, tail, lane, x, y, z, w, r, full, X0, Y0,
+                          Z0);
+            j = jn;
+            x = nx;
+            y = ny;
+            z = nz;
+            w = nw;
+            r = nr;
         }
         dev::wave_sync();
-        drain<S>(a, Q, acc, head, tail - head, lane);
+        drain<S>(a, Q, acc, tbl, head, tail - head, lane);
         __syncthreads();
         // the finished tile: one plain store per voxel (rows of 32 floats)
         for (int v = threadIdx.x; v < TVOX; v += DB) {
@@ -641,8 +698,8 @@ nbkd_status deposit(const float *xyz, const float *weight, const float *radius, 
         NBKD_HIP(hipGetLastError());
     }
     {
-        // persistent blocks over the tiles: 44 KB of LDS each, 3 per CU
-        const uint64_t blocks = std::min<uint64_t>(ntiles, (uint64_t)cus * 3);
+        // persistent blocks over the tiles: 56 KB of LDS each, 2 per CU
+        const uint64_t blocks = std::min<uint64_t>(ntiles, (uint64_t)cus * 2);
         TimedScope ts("deposit", s);
         switch (S) {
         case 1: launch_tiles<1>(a, blocks, s); break;

@@ -49,9 +49,9 @@ def test_volume_mixed_radii(gpu, oracle, periodic):
     _close(got, oracle.deposit(xyz, w, r, grid, ppu, period, 4, 0))
 
 
-@pytest.mark.parametrize("S", [1, 2, 3, 5])
+@pytest.mark.parametrize("S", [1, 2, 3, 5, 6])
 def test_subsample_factors(gpu, oracle, S):
-    """S^3 <= 64 packs 64 // S^3 voxels per pass; S = 5 takes the multi-pass path."""
+    """Templated S = 1..5 and the generic runtime-S kernel (S = 6)."""
     rng = np.random.default_rng(20 + S)
     grid, ppu = (24, 24, 24), 3.0
     box = np.array(grid) / ppu
@@ -91,6 +91,20 @@ def test_edges_outside_and_boundaries(gpu, oracle):
         got = _ras().render_points_volume(xyz, w, r, ppu, grid, periodic=periodic)
         period = tuple(box) if periodic else (-1.0, -1.0, -1.0)
         _close(got, oracle.deposit(xyz, w, r, grid, ppu, period, 4, 0))
+
+
+@pytest.mark.parametrize("periodic", [False, True])
+def test_balls_spanning_many_tiles(gpu, oracle, periodic):
+    """Balls whose sprite box covers more than 64 of the 32 x 32 x 8 tiles are
+    listed by the whole wave (deposit_pairs_kernel's cooperative path)."""
+    grid, ppu = (96, 80, 48), 1.0
+    box = np.array(grid, np.float64)
+    xyz = np.array([[40.0, 30.0, 20.0], [90.0, 5.0, 45.0], [10.5, 70.2, 3.3]], f32)
+    r = np.array([45.0, 30.0, 6.0], f32)
+    w = np.array([1.0, 2.0, 0.5], f32)
+    got = _ras().render_points_volume(xyz, w, r, ppu, grid, periodic=periodic)
+    period = tuple(box) if periodic else (-1.0, -1.0, -1.0)
+    _close(got, oracle.deposit(xyz, w, r, grid, ppu, period, 4, 0))
 
 
 def test_empty_and_accumulate(gpu, oracle):
