@@ -70,6 +70,8 @@ def parse():
                    help="also measure SURVEY §8(d)'s secondary runs (independent uniform "
                         "queries, C3 radius count + CSR batch, log-normal kNN) into 'suite'")
     p.add_argument("--radius", type=float, default=0.01, help="C3 radius, units of L")
+    p.add_argument("--deposit-grid", type=int, default=1024,
+                   help="--suite: grid side of the smoothing-radius deposit (0: skip)")
     p.add_argument("--csr-batch", type=int, default=1_000_000)
     p.add_argument("--lognormal-grid", type=int, default=512)
     p.add_argument("--redistribute", action="store_true",
@@ -167,6 +169,34 @@ def suite(args, capi, hip, tree, dev_pts, n, k, L, stream, od, oi):
     out["knn_kth_distance_only"] = {"queries_per_s": n / sec, "ms": sec * 1e3, "k": k,
                                     "queries": n}
     log(f"suite: k-th distance only {n / sec:.3e} q/s")
+    # those k-th distances as smoothing radii, deposited
+    # onto a G^3 periodic grid (render_points_volume semantics, S = 4)
+    if args.deposit_grid > 0:
+        G = args.deposit_grid
+        wd = hip.DeviceArray.from_numpy(np.full(n, 1.0 / n, np.float32))
+        gd = hip.DeviceArray((G, G, G), np.float32)
+
+        def dep():
+            capi.deposit_device(dev_pts.ptr, wd.ptr, rk.ptr, n, (G, G, G), G / L, gd.ptr,
+                                period=(L, L, L), stream=stream.handle)
+        dep()
+        capi.timing_reset()
+        capi.timing_enable(True)
+        sec = timed(dep, 1, hip)
+        parts = {nm: capi.timing_read(nm)[0] for nm in
+                 ("deposit_pairs", "deposit_fill", "deposit", "deposit_tiny")}
+        capi.timing_enable(False)
+        mass, plane = 0.0, G * G
+        for s0 in range(0, G, 64):
+            blk = np.empty(plane * min(64, G - s0), np.float32)
+            hip.memcpy(blk.ctypes.data, gd.ptr + s0 * plane * 4, blk.nbytes, hip.D2H)
+            mass += float(blk.sum(dtype=np.float64))
+        out["deposit"] = {"balls_per_s": n / sec, "ms": sec * 1e3, "breakdown_ms": parts,
+                          "grid": G, "subsample": 4, "radius": f"k={k} neighbour distance",
+                          "mass_on_grid": mass, "mass_expected": 1.0}
+        log(f"suite: deposit {n / sec:.3e} balls/s on {G}^3, mass {mass:.6f}")
+        gd.free()
+        wd.free()
     rk.free()
     # C3: radius count of every particle (self-queries), r = 0.01 L
     r = args.radius * L
