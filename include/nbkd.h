@@ -208,14 +208,18 @@ void nbkd_comm_free(nbkd_comm *comm);
  *   subsample  S: each straddled voxel is sampled at S^3 points (1..16).
  *   mode       0: nz slices [s, s+1) / ppu (render_points_volume);
  *              1: one plane at z = 0 (render_points; nz must be 1).
+ *   x0, wx     `out` holds only the columns [x0, x0 + wx) of the gx-wide grid,
+ *              element (px, py, s) at (px - x0) + wx * (py + gy * s); sprites,
+ *              periodic images and clipping are those of the whole grid
+ *              (0, gx: the whole grid).  One rank's x-slab (nbodyhpc_amd/slab.py).
  * A voxel receives weight * (sub-samples inside the ball) / S^3 / (4/3 pi R^3)
  * (R the radius in voxels); a ball under half a voxel across deposits its whole
  * weight in the voxel holding its centre.
  */
 nbkd_status nbkd_deposit(const float *xyz, const float *weight, const float *radius, uint64_t n,
                          int32_t gx, int32_t gy, int32_t nz, float pixels_per_unit,
-                         const float *period, int32_t subsample, int32_t mode, float *out,
-                         int32_t device, uint32_t flags, void *stream);
+                         const float *period, int32_t subsample, int32_t mode, int32_t x0,
+                         int32_t wx, float *out, int32_t device, uint32_t flags, void *stream);
 
 #ifdef __cplusplus
 }

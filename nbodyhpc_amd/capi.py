@@ -66,7 +66,7 @@ _PROTOS = {
     "nbkd_comm_exchange": (_i32, [_c_p, _i32, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p]),
     "nbkd_comm_free": (None, [_c_p]),
     "nbkd_deposit": (_i32, [_c_p, _c_p, _c_p, _u64, _i32, _i32, _i32, ctypes.c_float, _c_p, _i32,
-                            _i32, _c_p, _i32, _u32, _c_p]),
+                            _i32, _i32, _i32, _c_p, _i32, _u32, _c_p]),
 }
 COMM_ID_BYTES = 128
 
@@ -213,35 +213,38 @@ class Tree:
 
 
 def deposit(xyz, weight, radius, grid, ppu, period=(-1.0, -1.0, -1.0), subsample=4, mode=0,
-            device=-1, out=None):
+            device=-1, out=None, window=None):
     """Host arrays in, float32 grid (gx, gy, nz) in Fortran order out (nbkd_deposit).
-    `out` (same shape, Fortran-contiguous float32): accumulate into it."""
+    `window` = (x0, wx): only columns [x0, x0 + wx) of the gx-wide grid, shape
+    (wx, gy, nz).  `out` (that shape, Fortran-contiguous float32): accumulate into it."""
     p, w, r = _host_f32(xyz), _host_f32(weight), _host_f32(radius)
     gx, gy, nz = (int(v) for v in grid)
+    x0, wx = (0, gx) if window is None else (int(window[0]), int(window[1]))
     per = np.ascontiguousarray(period, np.float32)
     flags = 0
     if out is None:
-        out = np.empty((gx, gy, nz), np.float32, order="F")
+        out = np.empty((wx, gy, nz), np.float32, order="F")
     else:
-        if out.dtype != np.float32 or out.shape != (gx, gy, nz) or not out.flags.f_contiguous:
+        if out.dtype != np.float32 or out.shape != (wx, gy, nz) or not out.flags.f_contiguous:
             raise ValueError("out must be a Fortran-ordered float32 array of the grid's shape")
         flags |= NBKD_ACCUMULATE
     _check(lib().nbkd_deposit(p.ctypes.data, w.ctypes.data, r.ctypes.data, p.shape[0], gx, gy, nz,
-                              float(ppu), per.ctypes.data, int(subsample), int(mode),
+                              float(ppu), per.ctypes.data, int(subsample), int(mode), x0, wx,
                               out.ctypes.data, int(device), flags, None))
     return out
 
 
 def deposit_device(xyz_ptr, weight_ptr, radius_ptr, n, grid, ppu, out_ptr,
                    period=(-1.0, -1.0, -1.0), subsample=4, mode=0, device=-1, accumulate=False,
-                   stream=None):
+                   stream=None, window=None):
     """Device pointers in and out; returns once the deposit is enqueued."""
     gx, gy, nz = (int(v) for v in grid)
+    x0, wx = (0, gx) if window is None else (int(window[0]), int(window[1]))
     per = np.ascontiguousarray(period, np.float32)
     flags = NBKD_INPUT_DEVICE | NBKD_OUTPUT_DEVICE | (NBKD_ACCUMULATE if accumulate else 0)
     _check(lib().nbkd_deposit(xyz_ptr, weight_ptr, radius_ptr, int(n), gx, gy, nz, float(ppu),
-                              per.ctypes.data, int(subsample), int(mode), out_ptr, int(device),
-                              flags, stream))
+                              per.ctypes.data, int(subsample), int(mode), x0, wx, out_ptr,
+                              int(device), flags, stream))
 
 
 def timing_enable(on=True):

@@ -250,8 +250,8 @@ nbkd_status nbkd_query_ball_csr(const nbkd_tree *tree, const float *q, uint64_t 
 
 nbkd_status nbkd_deposit(const float *xyz, const float *weight, const float *radius, uint64_t n,
                          int32_t gx, int32_t gy, int32_t nz, float ppu, const float *period,
-                         int32_t subsample, int32_t mode, float *out, int32_t device,
-                         uint32_t flags, void *stream) {
+                         int32_t subsample, int32_t mode, int32_t x0, int32_t wx, float *out,
+                         int32_t device, uint32_t flags, void *stream) {
     NBKD_GUARD_BEGIN
     g_err.clear();
     if (!out || (n > 0 && (!xyz || !weight || !radius))) {
@@ -270,6 +270,10 @@ nbkd_status nbkd_deposit(const float *xyz, const float *weight, const float *rad
         set_error("nbkd_deposit: subsample must be in [1, 16]");
         return NBKD_EINVAL;
     }
+    if (x0 < 0 || wx < 1 || (int64_t)x0 + wx > gx) {
+        set_error("nbkd_deposit: the column window [x0, x0 + wx) must lie inside [0, gx)");
+        return NBKD_EINVAL;
+    }
     if (mode != 0 && !(mode == 1 && nz == 1)) {
         set_error("nbkd_deposit: mode must be 0 (volume) or 1 (one plane, nz = 1)");
         return NBKD_EINVAL;
@@ -279,8 +283,8 @@ nbkd_status nbkd_deposit(const float *xyz, const float *weight, const float *rad
         set_error("nbkd_deposit: cannot select the device");
         return NBKD_EDEVICE;
     }
-    return deposit(xyz, weight, radius, n, gx, gy, nz, ppu, period, subsample, mode, out, flags,
-                   (hipStream_t)stream);
+    return deposit(xyz, weight, radius, n, gx, gy, nz, ppu, period, subsample, mode, x0, wx, out,
+                   flags, (hipStream_t)stream);
     NBKD_GUARD_END
 }
 

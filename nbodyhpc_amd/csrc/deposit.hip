@@ -8,7 +8,9 @@
 //
 // Layout: particles as given (row-major xyz, weight, radius); grid float32
 // [nz][gy][gx] (index px + gx * (py + gy * s)), i.e. the reference's
-// column-major (gx, gy, nz) result (pybind.cpp:141-145).
+// column-major (gx, gy, nz) result (pybind.cpp:141-145).  A caller may hold
+// only the columns [x0, x0 + wx) (index px - x0 + wx * (py + gy * s)): the
+// x-slab of one rank (nbodyhpc_amd/slab.py deposit_slab).
 //
 // Global float atomics execute at the memory side on MI355X (every request
 // leaves L2, ~1.3 TB/s chip-wide; MI355X_MICROARCH.md "Global float atomics"),
@@ -58,6 +60,7 @@ struct DepositArgs {
     const float *xyz, *w, *r;
     uint64_t n;
     int gx, gy, nz;
+    int x0, wx; // the columns [x0, x0 + wx) held in `grid` (a slab of a gx-wide grid)
     int ntx, nty, ntz;
     float ppu;
     float period[3];
@@ -122,10 +125,12 @@ __device__ __forceinline__ bool tile_box(const DepositArgs &a, float x, float y,
     int px0, px1, py0, py1, s0, s1;
     sprite_range(x * a.ppu, h, a.gx, px0, px1);
     sprite_range(y * a.ppu, h, a.gy, py0, py1);
+    px0 = max(px0, a.x0);
+    px1 = min(px1, a.x0 + a.wx - 1);
     slice_range(a, z, r, s0, s1);
     if (px1 < px0 || py1 < py0 || s1 < s0) return false;
-    tx0 = px0 / TX;
-    tx1 = px1 / TX;
+    tx0 = (px0 - a.x0) / TX;
+    tx1 = (px1 - a.x0) / TX;
     ty0 = py0 / TY;
     ty1 = py1 / TY;
     tz0 = s0 / TZ;
@@ -225,7 +230,7 @@ __device__ void tile_image(const DepositArgs &a, StraddleRing &Q, float *acc, co
     s_hi = min(s_hi, min(Z0 + TZ, a.nz) - 1);
     const int ns = s_hi - s_lo + 1;
     if (ns <= 0) return;
-    const int gxe = min(X0 + TX, a.gx), gye = min(Y0 + TY, a.gy);
+    const int gxe = min(X0 + TX, a.x0 + a.wx), gye = min(Y0 + TY, a.gy);
     // this lane's slice (lanes >= ns hold a copy of the last one, never used)
     const int ks = s_lo + min(lane, ns - 1);
     const float zoff = z - depth[ks - Z0];
@@ -425,7 +430,7 @@ template <int S> __global__ void __launch_bounds__(DB) deposit_tile_kernel(Depos
         const uint32_t t = sh_tile;
         if (t >= ntiles) break;
         const int tx = (int)(t % a.ntx), ty = (int)((t / a.ntx) % a.nty), tz = (int)(t / (a.ntx * a.nty));
-        const int X0 = tx * TX, Y0 = ty * TY, Z0 = tz * TZ;
+        const int X0 = a.x0 + tx * TX, Y0 = ty * TY, Z0 = tz * TZ;
         if (threadIdx.x < TZ) sh_depth[threadIdx.x] = a.planes[3 * min(Z0 + (int)threadIdx.x, a.nz - 1)];
         __syncthreads();
         const uint64_t beg = a.tile_off[t], cnt = a.tile_off[t + 1] - beg;
@@ -465,8 +470,9 @@ template <int S> __global__ void __launch_bounds__(DB) deposit_tile_kernel(Depos
         for (int v = threadIdx.x; v < TVOX; v += DB) {
             const int lx = v % TX, ly = (v / TX) % TY, lz = v / (TX * TY);
             const int px = X0 + lx, py = Y0 + ly, s = Z0 + lz;
-            if (px < a.gx && py < a.gy && s < a.nz) {
-                const uint64_t gi = (uint64_t)px + (uint64_t)a.gx * ((uint64_t)py + (uint64_t)a.gy * s);
+            if (px < a.x0 + a.wx && py < a.gy && s < a.nz) {
+                const uint64_t gi =
+                    (uint64_t)(px - a.x0) + (uint64_t)a.wx * ((uint64_t)py + (uint64_t)a.gy * s);
                 a.grid[gi] = a.accumulate ? a.grid[gi] + acc[v] : acc[v];
             }
         }
@@ -506,9 +512,9 @@ __global__ void __launch_bounds__(DB) deposit_tiny_kernel(DepositArgs a) {
                 int px0, px1, py0, py1;
                 sprite_range(sx[ia] * ppu, 0.5f, a.gx, px0, px1);
                 sprite_range(sy[ib] * ppu, 0.5f, a.gy, py0, py1);
-                if (px1 < px0 || py1 < py0) continue;
-                unsafeAtomicAdd(a.grid + (uint64_t)px0 +
-                                    (uint64_t)a.gx * ((uint64_t)py0 + (uint64_t)a.gy * s),
+                if (px1 < px0 || py1 < py0 || px0 < a.x0 || px0 >= a.x0 + a.wx) continue;
+                unsafeAtomicAdd(a.grid + (uint64_t)(px0 - a.x0) +
+                                    (uint64_t)a.wx * ((uint64_t)py0 + (uint64_t)a.gy * s),
                                 w);
             }
     }
@@ -587,16 +593,16 @@ template <int S> void launch_tiles(const DepositArgs &a, uint64_t blocks, hipStr
 } // namespace
 
 nbkd_status deposit(const float *xyz, const float *weight, const float *radius, uint64_t n, int gx,
-                    int gy, int nz, float ppu, const float *period, int S, int mode, float *out,
-                    uint32_t flags, hipStream_t s) {
-    const uint64_t cells = (uint64_t)gx * (uint64_t)gy * (uint64_t)nz;
+                    int gy, int nz, float ppu, const float *period, int S, int mode, int x0, int wx,
+                    float *out, uint32_t flags, hipStream_t s) {
+    const uint64_t cells = (uint64_t)wx * (uint64_t)gy * (uint64_t)nz;
     const bool in_dev = flags & NBKD_INPUT_DEVICE, out_dev = flags & NBKD_OUTPUT_DEVICE;
     const bool accumulate = flags & NBKD_ACCUMULATE;
     if (n >= (1ull << 32)) {
         set_error("nbkd_deposit: at most 2^32 - 1 particles per call");
         return NBKD_EINVAL;
     }
-    const int ntx = (gx + TX - 1) / TX, nty = (gy + TY - 1) / TY, ntz = (nz + TZ - 1) / TZ;
+    const int ntx = (wx + TX - 1) / TX, nty = (gy + TY - 1) / TY, ntz = (nz + TZ - 1) / TZ;
     const uint64_t ntiles = (uint64_t)ntx * nty * ntz;
     if (ntiles >= (1ull << 31)) {
         set_error("nbkd_deposit: grid too large");
@@ -661,6 +667,8 @@ nbkd_status deposit(const float *xyz, const float *weight, const float *radius, 
     a.r = dr;
     a.n = n;
     a.gx = gx;
+    a.x0 = x0;
+    a.wx = wx;
     a.gy = gy;
     a.nz = nz;
     a.ntx = ntx;

@@ -193,8 +193,8 @@ nbkd_status sort_pairs(Workspace &ws, uint32_t *k0, uint32_t *v0, uint32_t *k1, 
 
 // deposit.hip: spheres onto a voxel grid (render_points_volume / render_points)
 nbkd_status deposit(const float *xyz, const float *weight, const float *radius, uint64_t n, int gx,
-                    int gy, int nz, float ppu, const float *period, int S, int mode, float *out,
-                    uint32_t flags, hipStream_t s);
+                    int gy, int nz, float ppu, const float *period, int S, int mode, int x0, int wx,
+                    float *out, uint32_t flags, hipStream_t s);
 
 // order-preserving float -> uint32 key (IEEE-754 total order of non-NaN values)
 __host__ __device__ inline uint32_t fkey(float f) {

@@ -461,3 +461,78 @@ def init_comm(dist, rank, world, device, log=None):
 
 def log_stderr(*a):
     print("[slab]", *a, file=sys.stderr, flush=True)
+
+
+# ------------------------------------------------------- density deposit per slab
+def grid_columns(world: int, gx: int, ppu: float, bounds):
+    """The W + 1 grid column cuts: rank r holds columns [c_r, c_r+1), c_r the
+    column nearest its slab's lower bound (c_0 = 0, c_W = gx)."""
+    c = [min(max(int(round(float(b) * ppu)), 0), gx) for b in bounds]
+    c[0], c[-1] = 0, gx
+    for i in range(1, world + 1):
+        c[i] = max(c[i], c[i - 1])
+    return c
+
+
+def deposit_halo(r_max: float, ppu: float) -> float:
+    """Halo width for the deposit: a ball's sprite reaches ceil(r ppu) + 1
+    voxels past its centre and a column cut sits within half a voxel of the
+    slab bound, so r_max + 3 voxels covers every ball touching a rank's columns."""
+    return float(r_max) + 3.0 / float(ppu)
+
+
+def exchange_payload(payload, rank, world, box, h, dist, bounds=None):
+    """exchange_host for (n, c) float32 rows whose column 0 is x: own rows,
+    then the left neighbour's strip, then the right neighbour's."""
+    import torch
+
+    if world == 1:
+        return payload
+    bounds = bounds_list(world, box) if bounds is None else bounds
+    check_halo(h, bounds)
+    lo, hi = float(bounds[rank]), float(bounds[rank + 1])
+    x = payload[:, 0]
+    mr = x >= np.float32(hi - h)
+    ml = x < np.float32(lo + h)
+    n_fl, n_fr = _strip_counts(dist, rank, world, int(mr.sum()), int(ml.sum()))
+    fl, fr = _host_sendrecv(dist, rank, world, payload[mr], payload[ml], n_fl, n_fr,
+                            torch.float32, payload.shape[1])
+    return np.concatenate([payload, fl.reshape(-1, payload.shape[1]),
+                           fr.reshape(-1, payload.shape[1])])
+
+
+def deposit_slab(own_xyz, own_w, own_r, rank, world, box, grid, ppu, dist, bounds=None,
+                 subsample=4, device=-1, engine=None):
+    """This rank's x-slab of the periodic sphere deposit over all ranks' balls
+    (SURVEY.md 8(f) rank 3 on the 8(e) decomposition): the own balls plus a
+    halo of the neighbours' balls within deposit_halo(max radius) are deposited
+    into the rank's grid columns only (nbkd_deposit's column window).  No grid
+    reduction is needed: the slabs of all ranks tile the grid.
+
+    Returns (c0, slab): the first column and the (wx, gy, nz) float32 slab.
+    `engine(xyz, w, r, grid, ppu, period, subsample, window)` defaults to the
+    HIP deposit (capi.deposit)."""
+    import torch
+
+    gx = int(grid[0])
+    bounds = bounds_list(world, box) if bounds is None else [float(b) for b in bounds]
+    if engine is None:
+        from . import capi
+
+        def engine(xyz, w, r, grid, ppu, period, subsample, window):
+            return capi.deposit(xyz, w, r, grid, ppu, period=period, subsample=subsample,
+                                device=device, window=window)
+    payload = np.column_stack([np.asarray(own_xyz, np.float32), np.asarray(own_w, np.float32),
+                               np.asarray(own_r, np.float32)]).astype(np.float32)
+    if world > 1:
+        rmax = torch.tensor([float(np.max(own_r)) if len(own_r) else 0.0], dtype=torch.float64)
+        dist.all_reduce(rmax, op=dist.ReduceOp.MAX)
+        h = deposit_halo(float(rmax[0]), ppu)
+        payload = exchange_payload(payload, rank, world, box, h, dist, bounds)
+    cuts = grid_columns(world, gx, ppu, bounds)
+    c0, wx = cuts[rank], cuts[rank + 1] - cuts[rank]
+    if wx == 0:
+        return c0, np.zeros((0, int(grid[1]), int(grid[2])), np.float32, order="F")
+    slab_grid = engine(payload[:, :3], payload[:, 3], payload[:, 4], tuple(int(g) for g in grid),
+                       float(ppu), (box, box, box), subsample, (c0, wx))
+    return c0, slab_grid

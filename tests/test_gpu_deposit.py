@@ -107,6 +107,21 @@ def test_balls_spanning_many_tiles(gpu, oracle, periodic):
     _close(got, oracle.deposit(xyz, w, r, grid, ppu, period, 4, 0))
 
 
+def test_column_windows(gpu, oracle):
+    """nbkd_deposit's column window (one rank's x-slab): each window equals those
+    columns of the whole periodic grid, balls wrapping across x = 0 included."""
+    from nbodyhpc_amd import capi
+    rng = np.random.default_rng(51)
+    grid, ppu = (40, 24, 16), 4.0
+    box = np.array(grid) / ppu
+    xyz, w, r = _particles(rng, 300, box, [0.1, 0.6, 1.8])
+    ref = oracle.deposit(xyz, w, r, grid, ppu, tuple(box), 4, 0)
+    for x0, wx in ((0, 40), (0, 13), (13, 14), (27, 13), (39, 1)):
+        got = capi.deposit(xyz, w, r, grid, ppu, period=tuple(box), window=(x0, wx))
+        assert got.shape == (wx, 24, 16)
+        _close(got, ref[x0:x0 + wx])
+
+
 def test_empty_and_accumulate(gpu, oracle):
     from nbodyhpc_amd import capi
     e = np.zeros((0, 3), f32)

@@ -203,3 +203,60 @@ def test_bench_c5_line_small(gpu, oracle, monkeypatch, capsys):
     dens = k / (4.0 / 3.0 * np.pi * d[:, -1].astype(np.float64) ** 3) / n
     got = line["kth_density"]["mean_density_over_mean"]
     assert abs(got - dens.mean()) < 1e-6 * dens.mean()
+
+
+def _deposit_worker(rank, world, port, n_per, grid, outdir):
+    from nbodyhpc_amd import hip
+
+    hip.preload()
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        hip.set_device(0)
+        xyz, w, r = _deposit_balls(n_per, rank, world)
+        c0, part = slab.deposit_slab(xyz, w, r, rank, world, 1.0, grid, float(grid[0]), dist,
+                                     device=0)
+        np.savez(os.path.join(outdir, f"d{rank}.npz"), c0=c0, g=part)
+    finally:
+        dist.destroy_process_group()
+
+
+def _deposit_balls(n_per, rank, world):
+    xyz, _ = _rank_points(n_per, rank, world)
+    rng = np.random.default_rng(200 + rank)
+    r = rng.choice(np.array([0.003, 0.02, 0.06], np.float32), n_per)
+    w = rng.uniform(0.5, 1.5, n_per).astype(np.float32)
+    return xyz, w, r
+
+
+def test_two_rank_slab_deposit_on_one_gpu(gpu, oracle, tmp_path):
+    """SURVEY.md 8(f) rank 3 on the 8(e) slabs: two ranks (sharing the box's one
+    GPU) deposit their balls plus the halo into their own grid columns with the
+    HIP kernel; the two slabs tile the oracle's single deposit of all balls."""
+    import multiprocessing as mp
+
+    world, n_per, grid = 2, 3000, (64, 64, 64)
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    procs = [ctx.Process(target=_deposit_worker, args=(r, world, port, n_per, grid, str(tmp_path)))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=300)
+    for p in procs:
+        if p.exitcode is None:
+            p.kill()
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    parts = [np.load(os.path.join(tmp_path, f"d{r}.npz")) for r in range(world)]
+    assert [int(p["c0"]) for p in parts] == [0, 32]
+    got = np.concatenate([p["g"] for p in parts], axis=0)
+    balls = [_deposit_balls(n_per, r, world) for r in range(world)]
+    xyz = np.concatenate([b[0] for b in balls])
+    w = np.concatenate([b[1] for b in balls])
+    r = np.concatenate([b[2] for b in balls])
+    ref = oracle.deposit(xyz, w, r, grid, float(grid[0]), (1.0, 1.0, 1.0), 4)
+    np.testing.assert_allclose(got, ref, rtol=2e-5, atol=1e-6 * float(ref.max()))

@@ -289,3 +289,61 @@ def test_violations_absolute_slack_for_thin_halos():
     assert slab.violations_host(q, np.array([near], np.float32), rank, world, box, h) == 1
     ok = np.float32(face) * np.float32(0.5)
     assert slab.violations_host(q, np.array([ok], np.float32), rank, world, box, h) == 0
+
+
+# ------------------------------------------------------------ deposit per slab
+def _deposit_worker(rank, world, port, n_per, grid, outdir):
+    """deposit_slab's decomposition (payload halo + column windows) with the
+    oracle as the deposit (full grid, then this rank's columns): the checker
+    stands in for nbkd_deposit here; tests/test_gpu_slab.py runs the HIP one."""
+    import torch.distributed as dist
+
+    from oracle.oracle import Oracle
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        xyz, w, r = _deposit_balls(n_per, rank, world)
+        orc = Oracle()
+
+        def engine(bx, bw, br, g, ppu, period, S, window):
+            full = orc.deposit(bx, bw, br, g, ppu, period, S)
+            return full[window[0]:window[0] + window[1]]
+        c0, part = slab.deposit_slab(xyz, w, r, rank, world, 1.0, grid, float(grid[0]), dist,
+                                     engine=engine)
+        np.savez(os.path.join(outdir, f"d{rank}.npz"), c0=c0, g=part)
+    finally:
+        dist.destroy_process_group()
+
+
+def _deposit_balls(n_per, rank, world):
+    xyz, _ = _slab_points(n_per, 31, rank, world)
+    rng = np.random.default_rng(100 + rank)
+    r = rng.choice(np.array([0.01, 0.04, 0.09], np.float32), n_per)
+    w = rng.uniform(0.5, 1.5, n_per).astype(np.float32)
+    return xyz, w, r
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_deposit_slabs_tile_the_single_deposit(world, tmp_path, oracle):
+    """Each rank's column window, deposited from its own balls plus the halo,
+    equals those columns of the single deposit of all balls; the windows tile
+    the grid, so their concatenation is the whole grid."""
+    import torch.multiprocessing as mp
+
+    n_per, grid = 150, (24, 24, 24)
+    port = _free_port()
+    mp.start_processes(_deposit_worker, args=(world, port, n_per, grid, str(tmp_path)),
+                       nprocs=world, join=True, start_method="spawn")
+    parts = [np.load(os.path.join(tmp_path, f"d{r}.npz")) for r in range(world)]
+    got = np.concatenate([p["g"] for p in parts], axis=0)
+    assert [int(p["c0"]) for p in parts] == slab.grid_columns(world, grid[0], grid[0],
+                                                              slab.bounds_list(world, 1.0))[:-1]
+    balls = [_deposit_balls(n_per, r, world) for r in range(world)]
+    xyz = np.concatenate([b[0] for b in balls])
+    w = np.concatenate([b[1] for b in balls])
+    r = np.concatenate([b[2] for b in balls])
+    ref = oracle.deposit(xyz, w, r, grid, float(grid[0]), (1.0, 1.0, 1.0), 4)
+    np.testing.assert_allclose(got, ref, rtol=1e-9, atol=1e-12)
+    assert abs(got.sum() - w.sum()) < 0.01 * w.sum()
