@@ -785,11 +785,13 @@ knn_collect_grp_kernel(DevTree t, const float *__restrict__ ginfo,
                        const uint32_t *__restrict__ order, uint32_t m, int kq,
                        const float *__restrict__ tg, float seed_mul, uint32_t qpp,
                        uint2 *__restrict__ cand, uint32_t capg,
-                       uint32_t *__restrict__ ccount, unsigned long long *__restrict__ stats) {
+                       uint32_t *__restrict__ ccount, unsigned long long *__restrict__ stats,
+                       bool xcd) {
     __shared__ CollectLdsG Wl[WPB];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     CollectLdsG &W = Wl[wave];
-    const uint32_t pk = blockIdx.x * WPB + wave;
+    const uint32_t bid = xcd ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
+    const uint32_t pk = bid * WPB + wave;
     const uint32_t gq = pk * qpp + lane;
     const bool valid = (uint32_t)lane < qpp && gq < m;
     const uint32_t qo = valid ? order[gq] : 0u;
@@ -1006,15 +1008,20 @@ void launch_collect(const Tree &t, const float *q, const uint32_t *order, uint32
     const char *const name = retry ? "knn_retry" : "knn_collect";
     const unsigned blocks = (unsigned)(((uint64_t)m + qpp - 1) / qpp + WPB - 1) / WPB;
     if (t.ginfo && groups_enabled()) {
+        // NBKD_XCD_MAP=0: hardware block order (A/B of the XCD-contiguous packet ranges)
+        static const bool xcd = [] {
+            const char *e = getenv("NBKD_XCD_MAP");
+            return !(e && atoi(e) == 0);
+        }();
         TimedScope ts(name, s);
         if (stats)
             knn_collect_grp_kernel<PER, 8, true><<<blocks, TB, 0, s>>>(
                 view(t), t.ginfo, t.leafinfo, t.hinfo, q, order, m, k, tg, seed_mul, qpp, cand, capg,
-                ccount, stats);
+                ccount, stats, xcd);
         else
             knn_collect_grp_kernel<PER, 8, false><<<blocks, TB, 0, s>>>(
                 view(t), t.ginfo, t.leafinfo, t.hinfo, q, order, m, k, tg, seed_mul, qpp, cand, capg,
-                ccount, nullptr);
+                ccount, nullptr, xcd);
         return;
     }
     TimedScope ts(name, s);

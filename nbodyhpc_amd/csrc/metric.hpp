@@ -14,6 +14,16 @@ __device__ __forceinline__ uint32_t mbcnt64(uint64_t mask) {
 }
 
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+
+// Workgroups are dealt round-robin over the 8 XCDs (observed, not promised:
+// MI355X_MICROARCH.md "Workgroup dispatch, XCD placement").  This bijection of
+// [0, nb) gives each XCD a contiguous range of logical blocks instead, so
+// neighbouring packets (which stage the same leaves) share one XCD's L2.  Speed
+// only: every placement computes the same result.
+__device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t nb) {
+    const uint32_t q = nb >> 3, r = nb & 7u, x = b & 7u, j = b >> 3;
+    return x * q + (x < r ? x : r) + j;
+}
 __device__ __forceinline__ float unif(float v) {
     return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(uint32_t, v)));
 }

@@ -61,3 +61,28 @@ def test_timing_api_roundtrip():
     capi.timing_reset()
     assert capi.timing_read("knn") == (0.0, 0)
     capi.timing_enable(False)
+
+
+def test_deposit_arguments_rejected_before_any_device_call():
+    """nbkd_deposit validates its arguments first (EINVAL with a message), so
+    these fail the same way with or without a GPU."""
+    xyz = np.zeros((4, 3), np.float32)
+    w = np.ones(4, np.float32)
+    cases = [
+        (dict(grid=(0, 8, 8), ppu=1.0), "grid extents"),
+        (dict(grid=(8, 8, 8), ppu=0.0), "pixels_per_unit"),
+        (dict(grid=(8, 8, 8), ppu=float("nan")), "pixels_per_unit"),
+        (dict(grid=(8, 8, 8), ppu=1.0, subsample=0), "subsample"),
+        (dict(grid=(8, 8, 8), ppu=1.0, subsample=17), "subsample"),
+        (dict(grid=(8, 8, 2), ppu=1.0, mode=1), "mode"),
+        (dict(grid=(8, 8, 8), ppu=1.0, window=(6, 3)), "column window"),
+        (dict(grid=(8, 8, 8), ppu=1.0, window=(0, 0)), "column window"),
+    ]
+    for kw, msg in cases:
+        with pytest.raises(capi.NbkdError, match=msg) as e:
+            capi.deposit(xyz, w, w, **kw)
+        assert e.value.status == capi.NBKD_EINVAL
+    L = capi.lib()
+    assert L.nbkd_deposit(None, None, None, 4, 8, 8, 8, 1.0, None, 4, 0, 0, 8, None, -1, 0,
+                          None) == capi.NBKD_EINVAL
+    assert b"NULL" in L.nbkd_last_error()
