@@ -87,8 +87,8 @@ def parse():
                    help="raw float32 (N, 3) particle file (reference main.cpp -f format) "
                         "instead of the synthetic set; N > 1 streams each rank's slab")
     p.add_argument("--input-format", choices=("raw", "gadget"), default="raw",
-                   help="gadget: a Gadget-2 snapshot (format 1/2, multi-file); the box is "
-                        "its BoxSize; N > 1 needs --redistribute")
+                   help="gadget: a Gadget-2 snapshot (format 1/2, multi-file; N > 1 streams each "
+                        "rank's slab unless --redistribute); the box is its BoxSize")
     return p.parse_args()
 
 
@@ -473,10 +473,11 @@ def main():
     gadget = None
     if args.input and args.input_format == "gadget":
         from nbodyhpc_amd import io as nio
-        gadget, _, gh = nio.read_gadget(args.input, ids=False)
+        if world == 1 or args.redistribute:
+            gadget, _, gh = nio.read_gadget(args.input, ids=False)
+        else:  # each rank streams its own slab (read_gadget_slab below)
+            gh = nio._gadget_pos_blocks(args.input)[1]
         L = float(gh["BoxSize"])
-        if world > 1 and not args.redistribute:
-            raise SystemExit("--input-format gadget with --gpus > 1 needs --redistribute")
     stream = hip.Stream()
     t_gen = time.perf_counter()
     ds = None
@@ -507,6 +508,9 @@ def main():
                 np.array(rows[lo_r:hi_r]), np.arange(lo_r, hi_r, dtype=np.uint32), rank, world,
                 L, dist, comm=comm, device=local_rank, log=log)
             del rows
+        elif args.input and args.input_format == "gadget":
+            from nbodyhpc_amd import io as nio
+            own_xyz, own_ids, _ = nio.read_gadget_slab(args.input, rank, world, L)
         elif args.input:
             from nbodyhpc_amd import io as nio
             own_xyz, own_ids = nio.read_slab(args.input, rank, world, L)

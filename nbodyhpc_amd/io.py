@@ -187,6 +187,67 @@ def read_gadget(path, ids=True):
     return xyz, idall, header
 
 
+def _gadget_pos_blocks(path):
+    """Per file: (path, endian, payload offset of POS, particle count), and
+    the first file's header as a dict."""
+    out, header = [], None
+    for fp in _gadget_files(path):
+        r = _Records(fp)
+        blocks = r.blocks()
+        if not blocks or blocks[0][2] != 256:
+            raise ValueError(f"{fp}: first block is not a 256-byte header")
+        with open(fp, "rb") as f:
+            f.seek(blocks[0][1])
+            h = np.frombuffer(f.read(256), GADGET_HEADER.newbyteorder(r.endian)
+                              if r.endian == ">" else GADGET_HEADER)[0]
+        n = int(np.asarray(h["npart"], np.uint64).sum())
+        if header is None:
+            header = {k: (h[k].tolist() if hasattr(h[k], "tolist") else h[k])
+                      for k in GADGET_HEADER.names if k != "fill"}
+        if r.format == 2:
+            p_blk = {lab.strip(): (o, nb) for lab, o, nb in blocks[1:]}.get("POS")
+        else:
+            p_blk = blocks[1][1:] if len(blocks) > 1 else None
+        if p_blk is None or p_blk[1] != 12 * n:
+            raise ValueError(f"{fp}: no float32 POS block of {n} particles")
+        out.append((fp, r.endian, p_blk[0], n))
+    return out, header
+
+
+def read_gadget_slab(path, rank, world, box=None, chunk_rows=1 << 24, bounds=None):
+    """Rank `rank`'s x-slab of a Gadget-2 snapshot, streamed: each file's POS
+    block is memory-mapped and scanned in chunks, so no rank holds the whole
+    snapshot ("streams to slabs directly").  Returns
+    (xyz float32 (m, 3), row numbers uint32 in read_gadget's order, header).
+    `box`: the periodic box (default: the header's BoxSize); `bounds`: the
+    W + 1 slab cuts (default: equal widths).  The last slab also owns x == box."""
+    from .slab import bounds_list
+    files, header = _gadget_pos_blocks(path)
+    box = float(header["BoxSize"]) if box is None else float(box)
+    cuts = bounds_list(world, box) if bounds is None else bounds
+    lo32, hi32 = np.float32(cuts[rank]), np.float32(cuts[rank + 1])
+    last = rank == world - 1
+    if sum(f[3] for f in files) > 0xFFFFFFFF:
+        raise ValueError("More than uint32_t points are not supported.")
+    xs, ids, base = [], [], 0
+    for fp, endian, off, n in files:
+        if n == 0:
+            continue
+        a = np.memmap(fp, dtype=np.dtype(endian + "f4"), mode="r", offset=off, shape=(n, 3))
+        for s in range(0, n, chunk_rows):
+            c = a[s:s + chunk_rows]
+            x = c[:, 0]
+            keep = (x >= lo32) & ((x <= hi32) if last else (x < hi32))
+            sel = np.nonzero(keep)[0]
+            xs.append(np.asarray(c[sel], dtype=np.float32))
+            ids.append((sel + base + s).astype(np.uint32))
+        base += n
+        del a
+    if not xs:
+        return np.empty((0, 3), np.float32), np.empty(0, np.uint32), header
+    return np.concatenate(xs), np.concatenate(ids), header
+
+
 def write_gadget(path, xyz, box, ids=None, fmt=1, endian="<", num_files=1):
     """A minimal Gadget-2 snapshot (all particles type 1, unit mass): the
     test-fixture writer for read_gadget.  num_files > 1 writes <path>.0 ...

@@ -73,3 +73,31 @@ def test_gadget_rejects_other_files(tmp_path):
     nio.write_positions(str(p), np.ones((10, 3), np.float32))
     with pytest.raises(ValueError):
         nio.read_gadget(str(p))
+
+
+@pytest.mark.parametrize("fmt,endian,nfiles,world", [(1, "<", 1, 2), (2, ">", 3, 3),
+                                                     (1, ">", 2, 4)])
+def test_gadget_slab_streaming_partitions_rows(tmp_path, fmt, endian, nfiles, world):
+    """read_gadget_slab: the ranks' slabs partition the snapshot's rows (in
+    read_gadget's order), each row in its x-slab, x == BoxSize on the last
+    rank; small chunks exercise the chunked scan across file boundaries."""
+    from nbodyhpc_amd import io as nio
+    rng = np.random.default_rng(4)
+    box = 20.0
+    xyz = rng.uniform(0, box, (2003, 3)).astype(np.float32)
+    xyz[:3, 0] = box
+    xyz[3:6, 0] = 0.0
+    p = str(tmp_path / "snap")
+    nio.write_gadget(p, xyz, box, fmt=fmt, endian=endian, num_files=nfiles)
+    cuts = slab.bounds_list(world, box)
+    seen = []
+    for r in range(world):
+        part, rows, h = nio.read_gadget_slab(p, r, world, chunk_rows=97)
+        assert h["BoxSize"] == box and rows.dtype == np.uint32
+        assert np.array_equal(part, xyz[rows])
+        x = part[:, 0]
+        assert np.all(x >= np.float32(cuts[r]))
+        assert np.all(x <= np.float32(box)) if r == world - 1 else np.all(x < np.float32(cuts[r + 1]))
+        seen.append(rows)
+    allr = np.sort(np.concatenate(seen))
+    assert np.array_equal(allr, np.arange(2003, dtype=np.uint32))
