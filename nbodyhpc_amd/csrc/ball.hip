@@ -61,7 +61,7 @@ ball_packet_kernel(DevTree t, const uint32_t *__restrict__ linfo, const float *_
     __shared__ BallLds Wl[WPB];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     BallLds &W = Wl[wave];
-    const uint32_t gq = (blockIdx.x * WPB + wave) * 64u + lane;
+    const uint32_t gq = (xcd_block(blockIdx.x, gridDim.x) * WPB + wave) * 64u + lane;
     const bool valid = gq < m;
     const uint32_t qo = valid ? order[gq] : 0u;
     const float qx = valid ? q[3 * (size_t)qo] : 0.0f;
