@@ -573,10 +573,16 @@ leafinfo_kernel(const nbkd_node *__restrict__ nodes, uint64_t nn, const float *_
 // and padding rows (FLT_MAX) sort last and are left out of the boxes.
 constexpr int GPL = NBKD_GBLOCK / 64; // points per lane
 
+//
+// The same pass writes leafinfo (8 words per leaf: its tight box, the union of
+// its group boxes, and its point range), lists the leaves holding padding and
+// reduces the data bounding box (bbox as in leafinfo_kernel, which it replaces
+// whenever there are points: one lane per leaf there read 64 scattered points).
 __global__ void __launch_bounds__(TB)
 group_kernel(const nbkd_node *__restrict__ nodes, uint64_t nn, float *__restrict__ x,
              float *__restrict__ y, float *__restrict__ z, uint32_t *__restrict__ idx, uint64_t n,
-             float *__restrict__ ginfo, float *__restrict__ hinfo) {
+             float *__restrict__ ginfo, float *__restrict__ hinfo, uint32_t *__restrict__ info,
+             uint32_t *__restrict__ bbox) {
     constexpr int WPB = TB / 64;
     __shared__ float sp[WPB][3][NBKD_GBLOCK];
     __shared__ uint32_t sr[WPB][NBKD_GBLOCK];
@@ -584,9 +590,13 @@ group_kernel(const nbkd_node *__restrict__ nodes, uint64_t nn, float *__restrict
     float (*const P)[NBKD_GBLOCK] = sp[wave];
     uint32_t *const R = sr[wave];
     const uint64_t nw = (uint64_t)gridDim.x * WPB;
+    float dlo[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, dhi[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
     for (uint64_t i = (uint64_t)blockIdx.x * WPB + wave; i < nn; i += nw) {
         const nbkd_node nd = nodes[i];
         if (nd.dimension >= 0) continue;
+        // this lane's running union of its group boxes, and padding seen
+        float llo[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, lhi[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+        bool pad = false;
         for (uint32_t b0 = nd.left; b0 < nd.right; b0 += NBKD_GBLOCK) {
             const uint32_t c = min((uint32_t)NBKD_GBLOCK, nd.right - b0);
             // point h of this lane: run position lane + 64 h
@@ -601,6 +611,7 @@ group_kernel(const nbkd_node *__restrict__ nodes, uint64_t nn, float *__restrict
                 p[h][2] = on ? z[b0 + j] : FLT_MAX;
                 id[h] = on ? idx[b0 + j] : 0xFFFFFFFFu;
                 real[h] = (on && id[h] < n) ? 1u : 0u;
+                pad |= on && id[h] >= n;
                 pos[h] = j;
                 s[h] = 0;
                 l[h] = on ? c : 0u;
@@ -623,22 +634,33 @@ group_kernel(const nbkd_node *__restrict__ nodes, uint64_t nn, float *__restrict
                 for (int h = 0; h < GPL; ++h) {
                     npos[h] = pos[h];
                     if (l[h] <= (uint32_t)NBKD_GROUP) continue;
+                    // pieces hold multiples of 8 points: both scans unrolled by 8,
+                    // branch-free, so the LDS reads of an 8-run issue together
                     float lo[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, hi[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
-                    for (uint32_t j = s[h]; j < s[h] + l[h]; ++j) {
-                        if (!R[j]) continue;
+                    for (uint32_t j0 = s[h]; j0 < s[h] + l[h]; j0 += 8) {
 #pragma unroll
-                        for (int a = 0; a < 3; ++a) {
-                            lo[a] = fminf(lo[a], P[a][j]);
-                            hi[a] = fmaxf(hi[a], P[a][j]);
+                        for (uint32_t u = 0; u < 8; ++u) {
+                            const uint32_t j = j0 + u;
+                            const bool rj = R[j] != 0u;
+#pragma unroll
+                            for (int a = 0; a < 3; ++a) {
+                                const float v = P[a][j];
+                                lo[a] = rj ? fminf(lo[a], v) : lo[a];
+                                hi[a] = rj ? fmaxf(hi[a], v) : hi[a];
+                            }
                         }
                     }
                     const float ex = hi[0] - lo[0], ey = hi[1] - lo[1], ez = hi[2] - lo[2];
                     const int ax = (ey > ex && ey >= ez) ? 1 : (ez > ex && ez > ey ? 2 : 0);
                     const float key = p[h][ax];
                     uint32_t rank = 0;
-                    for (uint32_t j = s[h]; j < s[h] + l[h]; ++j) {
-                        const float kj = P[ax][j];
-                        rank += (kj < key || (kj == key && j < pos[h])) ? 1u : 0u;
+                    for (uint32_t j0 = s[h]; j0 < s[h] + l[h]; j0 += 8) {
+#pragma unroll
+                        for (uint32_t u = 0; u < 8; ++u) {
+                            const uint32_t j = j0 + u;
+                            const float kj = P[ax][j];
+                            rank += (kj < key || (kj == key && j < pos[h])) ? 1u : 0u;
+                        }
                     }
                     const uint32_t m = (l[h] / 2) / 8 * 8;
                     npos[h] = s[h] + rank;
@@ -684,6 +706,11 @@ group_kernel(const nbkd_node *__restrict__ nodes, uint64_t nn, float *__restrict
                 o[3] = hi[1];
                 o[4] = lo[2];
                 o[5] = hi[2];
+#pragma unroll
+                for (int a = 0; a < 3; ++a) {
+                    llo[a] = fminf(llo[a], lo[a]);
+                    lhi[a] = fmaxf(lhi[a], hi[a]);
+                }
             }
             // a leaf of 65..128 points: the tight boxes of its two halves (the
             // first cut above, at m), the kNN collect kernel's staging chunks
@@ -709,6 +736,55 @@ group_kernel(const nbkd_node *__restrict__ nodes, uint64_t nn, float *__restrict
                 o[5] = hi[2];
             }
             wave_sync();
+        }
+        // leafinfo of leaf i: the union of the lanes' group-box unions
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+                llo[a] = fminf(llo[a], __shfl_xor(llo[a], o, 64));
+                lhi[a] = fmaxf(lhi[a], __shfl_xor(lhi[a], o, 64));
+            }
+        }
+        const bool any_pad = __any(pad);
+        if (lane == 0) {
+            float4 *o = reinterpret_cast<float4 *>(info + 8 * i);
+            o[0] = make_float4(llo[0], llo[1], llo[2], lhi[0]);
+            o[1] = make_float4(lhi[1], lhi[2], __uint_as_float(nd.left), __uint_as_float(nd.right));
+            if (any_pad) {
+                const uint32_t slot = atomicAdd(&bbox[6], 1u);
+                if (slot < (uint32_t)NBKD_PAD_LEAVES) bbox[7 + slot] = (uint32_t)i;
+            }
+        }
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            dlo[a] = fminf(dlo[a], llo[a]);
+            dhi[a] = fmaxf(dhi[a], lhi[a]);
+        }
+    }
+    // data bounding box (wave-uniform already): reduced over the block, then one
+    // lane per block issues the atomics (all blocks hit the same six words)
+    __shared__ float sbox[WPB][6];
+    if (lane == 0) {
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            sbox[wave][a] = dlo[a];
+            sbox[wave][3 + a] = dhi[a];
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            float lo = sbox[0][a], hi = sbox[0][3 + a];
+            for (int w = 1; w < WPB; ++w) {
+                lo = fminf(lo, sbox[w][a]);
+                hi = fmaxf(hi, sbox[w][3 + a]);
+            }
+            if (lo <= hi) {
+                atomicMin(&bbox[a], fkey(lo));
+                atomicMax(&bbox[3 + a], fkey(hi));
+            }
         }
     }
 }
@@ -990,26 +1066,33 @@ nbkd_status build_tree(Tree &t, const float *xyz, uint64_t n, int32_t leaf_size,
             (uint32_t)t.leaf, hblk_offset(t.depth), t.hsplit);
         NBKD_HIP(hipGetLastError());
     }
-    if (n8 > 0) {
-        TimedScope ts("build_groups", s);
-        NBKD_HIP(hipMalloc(&t.ginfo, (n8 / NBKD_GROUP) * 6 * sizeof(float)));
-        if (t.leaf > 64) NBKD_HIP(hipMalloc(&t.hinfo, t.nnodes * 12 * sizeof(float)));
-        const uint64_t blocks = std::min<uint64_t>((t.nnodes + 3) / 4, 65536);
-        group_kernel<<<(unsigned)std::max<uint64_t>(blocks, 1), TB, 0, s>>>(
-            t.nodes, t.nnodes, t.x, t.y, t.z, t.idx, t.n, t.ginfo, t.hinfo);
-        NBKD_HIP(hipGetLastError());
-    }
     {
-        TimedScope ts("build_leafinfo", s);
+        // groups (ginfo, hinfo) and leafinfo + padding leaves + data box in one pass
+        // (leafinfo_kernel only for a tree without points)
+        TimedScope ts("build_groups", s);
         NBKD_HIP(hipMalloc(&t.leafinfo, std::max<uint64_t>(t.nnodes, 1) * 32));
-        uint64_t blocks = std::min<uint64_t>((t.nnodes + TB - 1) / TB, 16384);
         DevBuf d_bbox;
         constexpr int NW = 7 + NBKD_PAD_LEAVES;
         NBKD_HIP(d_bbox.alloc(NW * 4, s));
         uint32_t init[NW] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u, 0u, 0u};
         NBKD_HIP(hipMemcpyAsync(d_bbox.p, init, sizeof(init), hipMemcpyHostToDevice, s));
-        leafinfo_kernel<<<(unsigned)std::max<uint64_t>(blocks, 1), TB, 0, s>>>(
-            t.nodes, t.nnodes, t.x, t.y, t.z, t.idx, t.n, t.leafinfo, d_bbox.as<uint32_t>());
+        if (n8 > 0) {
+            NBKD_HIP(hipMalloc(&t.ginfo, (n8 / NBKD_GROUP) * 6 * sizeof(float)));
+            if (t.leaf > 64) NBKD_HIP(hipMalloc(&t.hinfo, t.nnodes * 12 * sizeof(float)));
+            int dev = 0, cus = 256;
+            NBKD_HIP(hipGetDevice(&dev));
+            (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+            const char *eg = getenv("NBKD_GROUP_BLOCKS_PER_CU"); // A/B only
+            const uint64_t per_cu = eg ? (uint64_t)std::max(1, atoi(eg)) : 128u;
+            const uint64_t blocks = std::min<uint64_t>((t.nnodes + 3) / 4, (uint64_t)cus * per_cu);
+            group_kernel<<<(unsigned)std::max<uint64_t>(blocks, 1), TB, 0, s>>>(
+                t.nodes, t.nnodes, t.x, t.y, t.z, t.idx, t.n, t.ginfo, t.hinfo,
+                reinterpret_cast<uint32_t *>(t.leafinfo), d_bbox.as<uint32_t>());
+        } else {
+            uint64_t blocks = std::min<uint64_t>((t.nnodes + TB - 1) / TB, 16384);
+            leafinfo_kernel<<<(unsigned)std::max<uint64_t>(blocks, 1), TB, 0, s>>>(
+                t.nodes, t.nnodes, t.x, t.y, t.z, t.idx, t.n, t.leafinfo, d_bbox.as<uint32_t>());
+        }
         NBKD_HIP(hipGetLastError());
         uint32_t hb[NW];
         NBKD_HIP(hipMemcpyAsync(hb, d_bbox.p, sizeof(hb), hipMemcpyDeviceToHost, s));
