@@ -428,6 +428,10 @@ knn_collect_kernel(DevTree t, const uint32_t *__restrict__ linfo, const float *_
 // of every group before the compaction (r02s: 8 tests per lane where only
 // ~12 lanes need the leaf).
 //
+// Tried and dropped: testing each chunk's tight box (scalar loads of leafinfo /
+// hinfo) before staging it, so chunks no lane reaches skip the staging and its
+// wait: collect 54.0 -> 54.2 ms (r02as; few staged chunks are unreached).
+//
 // Tried and dropped: running packets whose balls clear the box faces with the
 // non-periodic formulas (4 % fewer VALU instructions).  One kernel holding
 // both variants spills VGPRs at the 8-wave budget; two launches leave the
