@@ -137,6 +137,13 @@ def cpu_baseline(points, k, leafsize, box, sample, gpu_d, gpu_i):
             "build_s": build_s}, parity
 
 
+def gloo_halo() -> bool:
+    """NBKD_HALO_TRANSPORT=gloo: stage the (setup-time) halo exchange over gloo
+    instead of RCCL, e.g. where RCCL cannot run; the timed step has no collective
+    either way."""
+    return os.environ.get("NBKD_HALO_TRANSPORT", "rccl").lower() == "gloo"
+
+
 def timed(fn, steps, hip):
     """fn() `steps` times between device synchronisations; seconds per call."""
     hip.synchronize()
@@ -300,7 +307,7 @@ def run_c5(args, rank, world, local_rank, dist, same_dev, barrier, allmax):
     if world == 1:
         dev_pts, n_local = hip.DeviceArray.from_numpy(own_xyz), own
     else:
-        comm = None if same_dev else slab.init_comm(dist, rank, world, local_rank, log)
+        comm = None if (same_dev or gloo_halo()) else slab.init_comm(dist, rank, world, local_rank, log)
         ds = slab.DeviceSlab(own_xyz, own_ids, rank, world, L, local_rank, dist, comm, log,
                              bounds=bounds)
         ds.exchange(h, stream.handle)
@@ -498,7 +505,7 @@ def main():
     else:
         from nbodyhpc_amd import slab
         points = None
-        comm = None if same_dev else slab.init_comm(dist, rank, world, local_rank, log)
+        comm = None if (same_dev or gloo_halo()) else slab.init_comm(dist, rank, world, local_rank, log)
         if args.input and args.redistribute:
             # each rank reads its contiguous row chunk; all-to-all-v to the owners
             from nbodyhpc_amd import io as nio
