@@ -647,7 +647,8 @@ def main():
             pm = json.load(open(pmcs[-1]))
             if (pm.get("n_particles") == own and pm.get("k") == k
                     and str(pm.get("kernel", "")).startswith("knn_collect")
-                    and pm.get("queries_per_launch") == q_per_launch):
+                    and abs(float(pm.get("queries_per_launch") or 0) - q_per_launch)
+                    <= 1e-9 * q_per_launch):
                 traffic = pm.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
@@ -681,7 +682,8 @@ def main():
                          f"particles per GPU (L={L}), leafsize {args.leafsize}"),
             "n_particles_per_gpu": own, "k": k, "leafsize": args.leafsize,
             "queries_per_step": own_total,
-            "parallelism": "single" if world == 1 else f"x-slab x{world} + RCCL halo",
+            "parallelism": ("single" if world == 1 else
+                            f"x-slab x{world} + halo over {(halo or {}).get('transport', 'rccl')}"),
         },
         "halo": halo,
         "build_ms": build_ms,
