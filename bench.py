@@ -640,18 +640,24 @@ def main():
     traffic = None
     # HBM bytes per knn launch from the newest committed rocprofv3 PMC summary
     # (profiles/rNN_pmc_knn.json: FETCH_SIZE x2 (gfx950) + WRITE_SIZE passes)
+    # (tags run r01, r01b, ..., r02z, r02aa, ...: newest = longest suffix, then last)
     import glob
-    pmcs = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_knn.json")))
-    if pmcs:
+
+    def tag_key(path):
+        tag = os.path.basename(path).split("_pmc")[0]
+        return tag[:3], len(tag) - 3, tag[3:]
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_knn.json")), key=tag_key,
+                       reverse=True):
         try:
-            pm = json.load(open(pmcs[-1]))
-            if (pm.get("n_particles") == own and pm.get("k") == k
-                    and str(pm.get("kernel", "")).startswith("knn_collect")
-                    and abs(float(pm.get("queries_per_launch") or 0) - q_per_launch)
-                    <= 1e-9 * q_per_launch):
-                traffic = pm.get("hbm_bytes_per_launch")
+            pm = json.load(open(path))
         except Exception:
-            traffic = None
+            continue
+        if (pm.get("n_particles") == own and pm.get("k") == k
+                and str(pm.get("kernel", "")).startswith("knn_collect")
+                and abs(float(pm.get("queries_per_launch") or 0) - q_per_launch)
+                <= 1e-9 * q_per_launch):
+            traffic = pm.get("hbm_bytes_per_launch")
+            break
     extra = None
     if world == 1 and args.suite:
         extra = suite(args, capi, hip, tree, dev_pts, n, k, L, stream, od, oi)
