@@ -981,7 +981,10 @@ knn_select_kernel(DevTree t, const float *__restrict__ q, const uint32_t *__rest
     // tree positions -> original ids: KC independent gathers in flight per lane
     // (inside store_rows' loop they would be issued one after another)
 #pragma unroll
-    for (int j = 0; j < KC; ++j) ti[j] = ti[j] == 0xFFFFFFFFu ? ti[j] : t.idx[ti[j]];
+    for (int j = 0; j < KC; ++j) { // branch-free: no-neighbour slots gather idx[0] and keep the sentinel
+        const uint32_t v = t.idx[ti[j] == 0xFFFFFFFFu ? 0u : ti[j]];
+        ti[j] = ti[j] == 0xFFFFFFFFu ? ti[j] : v;
+    }
 #pragma unroll
     for (int j0 = 0; j0 < KC; j0 += CC) {
         wave_sync();

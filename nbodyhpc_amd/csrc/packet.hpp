@@ -49,6 +49,25 @@ __device__ __forceinline__ void store_rows(const uint32_t *stage, const uint32_t
     const int jlo = c0 < 0 ? -c0 : 0;           // first staged register in [0, k)
     const int nc = min(CC, k - c0) - jlo;       // staged registers in [0, k)
     if (nc <= 0) return;
+    if (nc == CC) {
+        // every staged register is an output column (jlo == 0): the row and
+        // column of element e = it*64 + lane are shifts of a constant, and the
+        // unrolled iterations keep their LDS reads in flight together (the
+        // generic loop below divides by a runtime nc and waits on each read)
+        constexpr int RPI = 64 / CC; // rows per store instruction
+        const int j = lane % CC, r0 = lane / CC;
+#pragma unroll 8
+        for (int it = 0; it < CC; ++it) {
+            const int row = it * RPI + r0;
+            const uint32_t qr = rowq[row];
+            uint32_t v = stage[j * 64 + (row ^ j)];
+            if (qr != 0xFFFFFFFFu) {
+                if (remap && v != 0xFFFFFFFFu) v = remap[v];
+                dst[(size_t)qr * k + c0 + j] = v;
+            }
+        }
+        return;
+    }
     for (int e = lane; e < 64 * nc; e += 64) {
         const int row = e / nc, j = jlo + (e - row * nc);
         const uint32_t qr = rowq[row];
