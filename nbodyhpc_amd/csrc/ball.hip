@@ -29,7 +29,7 @@ using namespace dev;
 
 constexpr int TB = 256;
 constexpr int WPB = TB / 64;
-constexpr int CHUNK = 32;
+constexpr int CHUNK = 64; // one staged chunk per leaf up to leafsize 64
 
 struct PadLeaves {
     uint32_t id[NBKD_PAD_LEAVES];
@@ -91,73 +91,17 @@ ball_packet_kernel(DevTree t, const uint32_t *__restrict__ linfo, const float *_
                    box_lb_axis<PER>(qz, bx[4], bx[5], L)};
     uint64_t wm = __ballot((tm[0] + tm[1]) + tm[2] <= thr);
     bool have = wm != 0;
+    nbkd_node nd = cnodes[0]; // record of `node` while `have`
+    // the shared packet walk (packet.hpp: per-axis steps, branch-free pushes)
+    constexpr bool M = PER, STATS = false;
+    const float kth = thr;
+    uint64_t st[1] = {0};
+    (void)st;
 
     for (;;) {
-        bool found = false;
+        bool found;
         uint32_t lpos = 0, lend = 0;
-        for (;;) {
-            if (!have) {
-                if (sp == 0) break;
-                --sp;
-                node = __builtin_amdgcn_readlane(sk_node, sp);
-#pragma unroll
-                for (int a = 0; a < 6; ++a) bx[a] = rdlane(sk_b[a], sp);
-                tm[0] = box_lb_axis<PER>(qx, bx[0], bx[1], L);
-                tm[1] = box_lb_axis<PER>(qy, bx[2], bx[3], L);
-                tm[2] = box_lb_axis<PER>(qz, bx[4], bx[5], L);
-                wm = __ballot((tm[0] + tm[1]) + tm[2] <= thr);
-                if (wm == 0) continue;
-            }
-            have = false;
-            const nbkd_node nd = cnodes[node];
-            const int dim = nd.dimension;
-            if (dim < 0) {
-                lpos = nd.left;
-                lend = nd.right;
-                found = true;
-                break;
-            }
-            const float split = nd.split;
-            const float qd = dim == 0 ? qx : (dim == 1 ? qy : qz);
-            const float lo = dim == 0 ? bx[0] : (dim == 1 ? bx[2] : bx[4]);
-            const float hi = dim == 0 ? bx[1] : (dim == 1 ? bx[3] : bx[5]);
-            const float tl = box_lb_axis<PER>(qd, lo, split, L);
-            const float tr = box_lb_axis<PER>(qd, split, hi, L);
-            const float dl = ((dim == 0 ? tl : tm[0]) + (dim == 1 ? tl : tm[1])) + (dim == 2 ? tl : tm[2]);
-            const float dr = ((dim == 0 ? tr : tm[0]) + (dim == 1 ? tr : tm[1])) + (dim == 2 ? tr : tm[2]);
-            const uint64_t wl = __ballot(dl <= thr), wr = __ballot(dr <= thr);
-            const uint32_t right_votes = (uint32_t)__popcll(wm & __ballot(qd > split));
-            const bool right_first = 2 * right_votes > (uint32_t)__popcll(wm);
-            const uint64_t wn = right_first ? wr : wl, wf = right_first ? wl : wr;
-            const int near_slot = right_first ? 2 * dim : 2 * dim + 1;
-            const int far_slot = right_first ? 2 * dim + 1 : 2 * dim;
-            const uint32_t sb = __float_as_uint(split);
-            if (wn != 0 && wf != 0) {
-                const uint32_t far_node = right_first ? nd.left : nd.right;
-                const bool me = lane == sp;
-                sk_node = me ? far_node : sk_node;
-#pragma unroll
-                for (int a = 0; a < 6; ++a) {
-                    const uint32_t fv =
-                        __builtin_amdgcn_readfirstlane(a == far_slot ? sb : __float_as_uint(bx[a]));
-                    sk_b[a] = me ? __uint_as_float(fv) : sk_b[a];
-                }
-                ++sp;
-            }
-            if (wn == 0 && wf == 0) continue;
-            const bool go_near = wn != 0;
-            const int slot = go_near ? near_slot : far_slot;
-            const bool go_right = go_near == right_first;
-            node = go_right ? nd.right : nd.left;
-            const float tnew = go_right ? tr : tl;
-#pragma unroll
-            for (int a = 0; a < 3; ++a) tm[a] = dim == a ? tnew : tm[a];
-#pragma unroll
-            for (int a = 0; a < 6; ++a)
-                bx[a] = __uint_as_float(__builtin_amdgcn_readfirstlane(a == slot ? sb : __float_as_uint(bx[a])));
-            wm = go_near ? wn : wf;
-            have = true;
-        }
+        NBKD_GWALK(found, lpos, lend);
         if (!found) break;
 
         // leaf: tight box first (lanes < 6), then the chunks
@@ -196,35 +140,26 @@ ball_packet_kernel(DevTree t, const uint32_t *__restrict__ linfo, const float *_
                 }
             }
             // count mode, few partial lanes: transpose the loop.  Lanes hold
-            // the staged points (lane & 31), each step tests them against two
-            // partial queries at once (lower / upper half of the wave, query
-            // coordinates broadcast from LDS), and a ballot's
-            // popcount per half is that query's hit count.  One step is
-            // ~14 VALU per query against ~16 per point for the whole wave
-            // below, so it pays while #partial <= tnum/8 x #points.
+            // the staged points, each step tests them against one partial
+            // query (coordinates broadcast from LDS), and the ballot's
+            // popcount is that query's hit count.  One step is ~14 VALU per
+            // query against ~16 per point for the whole wave below, so it
+            // pays while #partial <= tnum/8 x #points.
             bool trans = false;
             if constexpr (!FILL) {
                 const uint64_t pm = __ballot(part);
                 trans = (uint32_t)__popcll(pm) * 8u <= cn * tnum;
                 if (trans) {
-                    const uint32_t u = (uint32_t)lane & 31u;
-                    const bool pv = u < cn;
-                    const float px = W.pb[0][u], py = W.pb[1][u], pz = W.pb[2][u];
-                    const bool upper = lane >= 32;
+                    const bool pv = (uint32_t)lane < cn;
+                    const float px = W.pb[0][lane], py = W.pb[1][lane], pz = W.pb[2][lane];
                     uint64_t rem = pm;
                     while (rem) {
-                        const int j0 = __builtin_ctzll(rem);
+                        const int j = __builtin_ctzll(rem);
                         rem &= rem - 1;
-                        const bool two = rem != 0;
-                        const int j1 = two ? __builtin_ctzll(rem) : j0;
-                        rem &= rem - 1;
-                        const float4 sq = W.qs[upper ? j1 : j0]; // LDS broadcast
+                        const float4 sq = W.qs[j]; // LDS broadcast
                         const float d = point_d2_fast<PER>(sq.x, sq.y, sq.z, px, py, pz, L);
-                        const uint64_t hits = __ballot(pv && d <= r2);
-                        const uint32_t c0 = (uint32_t)__popc((uint32_t)hits);
-                        const uint32_t c1 = two ? (uint32_t)__popc((uint32_t)(hits >> 32)) : 0u;
-                        cnt += lane == j0 ? c0 : 0u;
-                        cnt += lane == j1 ? c1 : 0u;
+                        const uint32_t c = (uint32_t)__popcll(__ballot(pv && d <= r2));
+                        cnt += lane == j ? c : 0u;
                     }
                 }
             }
@@ -311,7 +246,7 @@ void launch_ball_packet(const Tree &t, const float *q, const uint32_t *order, ui
     // transposed count threshold (x/8 partial lanes per staged point); 0 = off
     static const uint32_t tnum = [] {
         const char *e = getenv("NBKD_BALL_T");
-        return e ? (uint32_t)atoi(e) : 6u;
+        return e ? (uint32_t)atoi(e) : 8u;
     }();
     PadLeaves pad;
     for (int j = 0; j < NBKD_PAD_LEAVES; ++j)

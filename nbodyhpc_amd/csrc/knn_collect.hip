@@ -464,139 +464,6 @@ struct CollectLdsG {
         glds_f32((TBOX), W.tb, lane, 6);                                                           \
     } while (0)
 
-// v = lanes in `mask` ? val : old, as one v_cndmask (a select of a uniform
-// value into one lane otherwise compiles to exec-masked branches)
-__device__ __forceinline__ float lane_set(float old, float val, uint64_t mask) {
-    float r;
-    asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(old), "v"(val), "s"(mask));
-    return r;
-}
-__device__ __forceinline__ uint32_t lane_set(uint32_t old, uint32_t val, uint64_t mask) {
-    uint32_t r;
-    asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(old), "v"(val), "s"(mask));
-    return r;
-}
-
-// one internal node with split axis D (compile-time): test both children for
-// every lane, push the far one when both are wanted, step into the near one
-// (the walk branches on the node's axis, so no per-lane selects pick the axis)
-#define NBKD_GSTEP(D)                                                                              \
-    {                                                                                              \
-        const float split = nd.split;                                                              \
-        const float qd = (D) == 0 ? qx : ((D) == 1 ? qy : qz);                                     \
-        const float tl = box_lb_axis<M>(qd, bx[2 * (D)], split, L);                                \
-        const float tr = box_lb_axis<M>(qd, split, bx[2 * (D) + 1], L);                            \
-        const float dl = (((D) == 0 ? tl : tm[0]) + ((D) == 1 ? tl : tm[1])) + ((D) == 2 ? tl : tm[2]); \
-        const float dr = (((D) == 0 ? tr : tm[0]) + ((D) == 1 ? tr : tm[1])) + ((D) == 2 ? tr : tm[2]); \
-        const uint64_t wl = __ballot(dl <= kth), wr = __ballot(dr <= kth);                         \
-        const uint32_t right_votes = (uint32_t)__popcll(wm & __ballot(qd > split));                \
-        const bool right_first = 2 * right_votes > (uint32_t)__popcll(wm);                         \
-        const uint64_t wn = right_first ? wr : wl, wf = right_first ? wl : wr;                     \
-        {                                                                                          \
-            /* push the far child when both are wanted: far = left child [lo, split] if          \
-               right_first, else right child [split, hi]; one v_cndmask per word */                \
-            const bool push = wn != 0 && wf != 0;                                                  \
-            const uint64_t pmask = push ? (1ull << sp) : 0ull;                                     \
-            sk_node = lane_set(sk_node, right_first ? nd.left : nd.right, pmask);                  \
-            _Pragma("unroll") for (int a = 0; a < 6; ++a) {                                        \
-                const bool is_split = right_first ? a == 2 * (D) + 1 : a == 2 * (D);               \
-                sk_b[a] = lane_set(sk_b[a], is_split ? split : bx[a], pmask);                      \
-            }                                                                                      \
-            sp += push ? 1 : 0;                                                                    \
-        }                                                                                          \
-        if (wn == 0 && wf == 0) continue;                                                          \
-        const bool go_near = wn != 0;                                                              \
-        const bool go_right = go_near == right_first;                                              \
-        node = go_right ? nd.right : nd.left;                                                      \
-        nd = cnodes[node];                                                                         \
-        tm[D] = go_right ? tr : tl;                                                                \
-        if (go_right)                                                                              \
-            bx[2 * (D)] = unif(split);                                                             \
-        else                                                                                       \
-            bx[2 * (D) + 1] = unif(split);                                                         \
-        wm = go_near ? wn : wf;                                                                    \
-        have = true;                                                                               \
-    }
-
-// one internal node (record nd): test both children for every lane, push the
-// far one when both are wanted, step into the near one.  (Tried and dropped:
-// loading both children's records on entry, consumed after the tests, to take
-// the node load off the dependent chain: collect 62.4 -> 66.4 ms, r02h.)
-#define NBKD_GSTEP_ANY                                                                             \
-    {                                                                                              \
-        const int dim = nd.dimension;                                                              \
-        const float split = nd.split;                                                              \
-        const float qd = dim == 0 ? qx : (dim == 1 ? qy : qz);                                     \
-        const float lo = dim == 0 ? bx[0] : (dim == 1 ? bx[2] : bx[4]);                            \
-        const float hi = dim == 0 ? bx[1] : (dim == 1 ? bx[3] : bx[5]);                            \
-        const float tl = box_lb_axis<M>(qd, lo, split, L);                                         \
-        const float tr = box_lb_axis<M>(qd, split, hi, L);                                         \
-        const float dl = ((dim == 0 ? tl : tm[0]) + (dim == 1 ? tl : tm[1])) + (dim == 2 ? tl : tm[2]); \
-        const float dr = ((dim == 0 ? tr : tm[0]) + (dim == 1 ? tr : tm[1])) + (dim == 2 ? tr : tm[2]); \
-        const uint64_t wl = __ballot(dl <= kth), wr = __ballot(dr <= kth);                         \
-        const uint32_t right_votes = (uint32_t)__popcll(wm & __ballot(qd > split));                \
-        const bool right_first = 2 * right_votes > (uint32_t)__popcll(wm);                         \
-        const uint64_t wn = right_first ? wr : wl, wf = right_first ? wl : wr;                     \
-        const int near_slot = right_first ? 2 * dim : 2 * dim + 1;                                 \
-        const int far_slot = right_first ? 2 * dim + 1 : 2 * dim;                                  \
-        const uint32_t sb = __float_as_uint(split);                                                \
-        const bool go_near = wn != 0;                                                              \
-        const bool go_right = go_near == right_first;                                              \
-        if (wn != 0 && wf != 0) {                                                                  \
-            const uint32_t far_node = right_first ? nd.left : nd.right;                            \
-            const bool me = lane == sp;                                                            \
-            sk_node = me ? far_node : sk_node;                                                     \
-            _Pragma("unroll") for (int a = 0; a < 6; ++a) {                                        \
-                const uint32_t fv =                                                                \
-                    __builtin_amdgcn_readfirstlane(a == far_slot ? sb : __float_as_uint(bx[a]));   \
-                sk_b[a] = me ? __uint_as_float(fv) : sk_b[a];                                      \
-            }                                                                                      \
-            ++sp;                                                                                  \
-        }                                                                                          \
-        if (wn == 0 && wf == 0) continue;                                                          \
-        const int slot = go_near ? near_slot : far_slot;                                           \
-        node = go_right ? nd.right : nd.left;                                                      \
-        nd = cnodes[node];                                                                         \
-        const float tnew = go_right ? tr : tl;                                                     \
-        _Pragma("unroll") for (int a = 0; a < 3; ++a) tm[a] = dim == a ? tnew : tm[a];             \
-        _Pragma("unroll") for (int a = 0; a < 6; ++a) bx[a] = __uint_as_float(                     \
-            __builtin_amdgcn_readfirstlane(a == slot ? sb : __float_as_uint(bx[a])));              \
-        wm = go_near ? wn : wf;                                                                    \
-        have = true;                                                                               \
-    }
-
-// advance the packet walk to the next leaf some lane wants (FOUND = false: done)
-#define NBKD_GWALK(FOUND, LPOS, LEND)                                                              \
-    FOUND = false;                                                                                 \
-    for (;;) {                                                                                     \
-        if (!have) {                                                                               \
-            if (sp == 0) break;                                                                    \
-            --sp;                                                                                  \
-            node = (uint32_t)__builtin_amdgcn_readlane((int)sk_node, sp);                          \
-            _Pragma("unroll") for (int a = 0; a < 6; ++a) bx[a] = rdlane(sk_b[a], sp);             \
-            tm[0] = box_lb_axis<M>(qx, bx[0], bx[1], L);                                           \
-            tm[1] = box_lb_axis<M>(qy, bx[2], bx[3], L);                                           \
-            tm[2] = box_lb_axis<M>(qz, bx[4], bx[5], L);                                           \
-            wm = __ballot((tm[0] + tm[1]) + tm[2] <= kth);                                         \
-            if (wm == 0) continue;                                                                 \
-            nd = cnodes[node];                                                                     \
-        }                                                                                          \
-        have = false;                                                                              \
-        if constexpr (STATS) ++st[0];                                                              \
-        if (nd.dimension < 0) {                                                                    \
-            LPOS = nd.left;                                                                        \
-            LEND = nd.right;                                                                       \
-            FOUND = true;                                                                          \
-            break;                                                                                 \
-        }                                                                                          \
-        if (nd.dimension == 0)                                                                     \
-            NBKD_GSTEP(0)                                                                          \
-        else if (nd.dimension == 1)                                                                \
-            NBKD_GSTEP(1)                                                                          \
-        else                                                                                       \
-            NBKD_GSTEP(2)                                                                          \
-    }
-
 // st: node visits, leaves scanned, points staged, dense points, sparse
 // iterations, pair evaluations, then 6 phase clocks, then lanes needing a
 // staged chunk summed over chunks (STATS only)

@@ -94,5 +94,96 @@ __device__ __forceinline__ void knn_fail_check(bool valid, bool seeded, uint32_t
 }
 
 
+// ------------------------------------------------------------------ packet walk
+// The wave's depth-first walk (knn_collect.hip, ball.hip).  The macros expect in
+// scope: lane, qx/qy/qz, the bound kth, L, cnodes, the walk state node / nd (its
+// record while `have`) / have / wm / bx[6] / tm[3], the wave stack sp / sk_node /
+// sk_b[6], the metric switch M and STATS / st (node visits in st[0]).
+// v = lanes in `mask` ? val : old, as one v_cndmask (a select of a uniform
+// value into one lane otherwise compiles to exec-masked branches)
+__device__ __forceinline__ float lane_set(float old, float val, uint64_t mask) {
+    float r;
+    asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(old), "v"(val), "s"(mask));
+    return r;
+}
+__device__ __forceinline__ uint32_t lane_set(uint32_t old, uint32_t val, uint64_t mask) {
+    uint32_t r;
+    asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(old), "v"(val), "s"(mask));
+    return r;
+}
+
+// one internal node with split axis D (compile-time): test both children for
+// every lane, push the far one when both are wanted, step into the near one
+// (the walk branches on the node's axis, so no per-lane selects pick the axis)
+#define NBKD_GSTEP(D)                                                                              \
+    {                                                                                              \
+        const float split = nd.split;                                                              \
+        const float qd = (D) == 0 ? qx : ((D) == 1 ? qy : qz);                                     \
+        const float tl = box_lb_axis<M>(qd, bx[2 * (D)], split, L);                                \
+        const float tr = box_lb_axis<M>(qd, split, bx[2 * (D) + 1], L);                            \
+        const float dl = (((D) == 0 ? tl : tm[0]) + ((D) == 1 ? tl : tm[1])) + ((D) == 2 ? tl : tm[2]); \
+        const float dr = (((D) == 0 ? tr : tm[0]) + ((D) == 1 ? tr : tm[1])) + ((D) == 2 ? tr : tm[2]); \
+        const uint64_t wl = __ballot(dl <= kth), wr = __ballot(dr <= kth);                         \
+        const uint32_t right_votes = (uint32_t)__popcll(wm & __ballot(qd > split));                \
+        const bool right_first = 2 * right_votes > (uint32_t)__popcll(wm);                         \
+        const uint64_t wn = right_first ? wr : wl, wf = right_first ? wl : wr;                     \
+        {                                                                                          \
+            /* push the far child when both are wanted: far = left child [lo, split] if          \
+               right_first, else right child [split, hi]; one v_cndmask per word */                \
+            const bool push = wn != 0 && wf != 0;                                                  \
+            const uint64_t pmask = push ? (1ull << sp) : 0ull;                                     \
+            sk_node = lane_set(sk_node, right_first ? nd.left : nd.right, pmask);                  \
+            _Pragma("unroll") for (int a = 0; a < 6; ++a) {                                        \
+                const bool is_split = right_first ? a == 2 * (D) + 1 : a == 2 * (D);               \
+                sk_b[a] = lane_set(sk_b[a], is_split ? split : bx[a], pmask);                      \
+            }                                                                                      \
+            sp += push ? 1 : 0;                                                                    \
+        }                                                                                          \
+        if (wn == 0 && wf == 0) continue;                                                          \
+        const bool go_near = wn != 0;                                                              \
+        const bool go_right = go_near == right_first;                                              \
+        node = go_right ? nd.right : nd.left;                                                      \
+        nd = cnodes[node];                                                                         \
+        tm[D] = go_right ? tr : tl;                                                                \
+        if (go_right)                                                                              \
+            bx[2 * (D)] = unif(split);                                                             \
+        else                                                                                       \
+            bx[2 * (D) + 1] = unif(split);                                                         \
+        wm = go_near ? wn : wf;                                                                    \
+        have = true;                                                                               \
+    }
+
+// advance the packet walk to the next leaf some lane wants (FOUND = false: done)
+#define NBKD_GWALK(FOUND, LPOS, LEND)                                                              \
+    FOUND = false;                                                                                 \
+    for (;;) {                                                                                     \
+        if (!have) {                                                                               \
+            if (sp == 0) break;                                                                    \
+            --sp;                                                                                  \
+            node = (uint32_t)__builtin_amdgcn_readlane((int)sk_node, sp);                          \
+            _Pragma("unroll") for (int a = 0; a < 6; ++a) bx[a] = rdlane(sk_b[a], sp);             \
+            tm[0] = box_lb_axis<M>(qx, bx[0], bx[1], L);                                           \
+            tm[1] = box_lb_axis<M>(qy, bx[2], bx[3], L);                                           \
+            tm[2] = box_lb_axis<M>(qz, bx[4], bx[5], L);                                           \
+            wm = __ballot((tm[0] + tm[1]) + tm[2] <= kth);                                         \
+            if (wm == 0) continue;                                                                 \
+            nd = cnodes[node];                                                                     \
+        }                                                                                          \
+        have = false;                                                                              \
+        if constexpr (STATS) ++st[0];                                                              \
+        if (nd.dimension < 0) {                                                                    \
+            LPOS = nd.left;                                                                        \
+            LEND = nd.right;                                                                       \
+            FOUND = true;                                                                          \
+            break;                                                                                 \
+        }                                                                                          \
+        if (nd.dimension == 0)                                                                     \
+            NBKD_GSTEP(0)                                                                          \
+        else if (nd.dimension == 1)                                                                \
+            NBKD_GSTEP(1)                                                                          \
+        else                                                                                       \
+            NBKD_GSTEP(2)                                                                          \
+    }
+
 } // namespace dev
 } // namespace nbkd
