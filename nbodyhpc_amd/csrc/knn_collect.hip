@@ -16,7 +16,7 @@
 //            only by the lanes whose query ball reaches its TIGHT bounding box
 //            (leafinfo), its points staged in LDS by direct global->LDS loads.
 //            Each query's ball is its seed radius (leaf_key3_kernel), which is
-//            expected to hold k + 4 sqrt(k) + 4 points; every point inside it
+//            expected to hold k + 3.5 sqrt(k) + 3.5 points; every point inside it
 //            is appended to the query's candidate column in HBM.  No top-k is
 //            kept, so the kernel needs few VGPRs and ~3 KB of LDS per wave and
 //            runs 8 waves per SIMD.

@@ -64,8 +64,8 @@ constexpr int SHAPE_MAX = 256;
 
 // Guessed squared search radius of a query from the point density of the
 // subtree it falls in (count points in the box lo..hi): the radius of a sphere
-// expected to hold `mu_c` * 4/3*pi points, mu = k + 4 sqrt(k) + 4 (Poisson
-// tail ~1e-4 below k).  Only a pruning seed: the kNN kernel starts with this
+// expected to hold `mu_c` * 4/3*pi points, mu = k + 3.5 sqrt(k) + 3.5 (Poisson
+// tail ~2e-4 below k; seed_params).  Only a pruning seed: the kNN kernel starts with this
 // bound instead of +inf and sends every query that finds fewer than k points
 // inside it to the reference-exact kernel, so a bad guess costs time, never
 // correctness.
@@ -757,8 +757,11 @@ struct SeedParams {
     uint32_t anchor;
 };
 SeedParams seed_params(const Tree &t, int k) {
+    // a = 3.5: at 1e8 uniform 1.400e9 q/s (20.5 k retries) vs 1.376e9 at a = 4
+    // (4.9 k), 1.393e9 at 3, 1.372e9 at 2.5, 1.361e9 at 5; log-normal 82.3 ms
+    // at both 3.5 and 4 (r02bg, r02bi).  The column capacity keeps a = 4.
     const char *e = getenv("NBKD_KNN_SEED");
-    const float a = e ? (float)atof(e) : 4.0f;
+    const float a = e ? (float)atof(e) : 3.5f;
     SeedParams p;
     p.on = a > 0.0f;
     const float mu = (float)k + a * sqrtf((float)k) + a;
@@ -977,15 +980,17 @@ nbkd_status knn_locked(const Tree &t, const float *q, uint64_t m, int k, float *
                     NBKD_HIP(hipGetLastError());
                 }
                 // packets pay off only where failures are dense enough to be
-                // coherent (clustered inputs: ~4% of queries; uniform: ~0.005%,
-                // 3 ms as packets of 64 vs 0.2 ms one per wave)
+                // coherent (clustered inputs: ~4% of queries; uniform: ~0.02%,
+                // 2.3 ms as packets of 64 vs 0.4 ms one per wave).  Crossover
+                // at 1e8 uniform (r02bi): 82 k failures 1.1 ms one per wave vs
+                // 1.9 as packets, 307 k 3.0 vs 2.0: packets from 1/512.
                 static const int force_qpp = [] { // NBKD_RETRY_QPP=1|64: A/B only
                     const char *e = getenv("NBKD_RETRY_QPP");
                     return e ? atoi(e) : 0;
                 }();
                 const uint32_t rqpp = force_qpp == 1 || force_qpp == 64
                                           ? (uint32_t)force_qpp
-                                          : ((uint64_t)nr * 256u >= (uint64_t)mm ? 64u : 1u);
+                                          : ((uint64_t)nr * 512u >= (uint64_t)mm ? 64u : 1u);
                 const uint32_t capr = collect_capacity(k) * 8u;
                 uint64_t rb = budget / ((uint64_t)capr * 8u) / 64u * 64u;
                 rb = std::max<uint64_t>(std::min<uint64_t>(rb, ((uint64_t)nr + 63) / 64 * 64), 64);
