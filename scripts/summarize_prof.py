@@ -4,6 +4,8 @@
 
 writes
   profiles/<round>_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary (copied)
+  profiles/<round>_launches.json      per-launch durations of the kNN / radius kernels by
+                                      grid size (full-size collect launches vs retries)
   profiles/<round>_pmc_knn.json       HBM bytes per knn launch from the FETCH_SIZE and
                                       WRITE_SIZE passes (separate runs), gfx950-corrected
   profiles/<round>_bench.json         the bench line of the same call
@@ -49,6 +51,25 @@ def main():
     stats = find(os.path.join(src, "trace"), "*kernel_stats.csv")
     if stats:
         shutil.copy(stats, os.path.join(prof, f"{tag}_kernel_stats.csv"))
+    trace = find(os.path.join(src, "trace"), "*kernel_trace.csv")
+    if trace:
+        # the stats summary averages every launch of a kernel; the collect
+        # kernel also runs small retry launches, so list the per-launch
+        # durations by (kernel, grid size): the full-size rows are what the
+        # bench's roofline.kernel_ms_per_launch measures with HIP events
+        launches = {}
+        with open(trace) as f:
+            for row in csv.DictReader(f):
+                name = row["Kernel_Name"]
+                if not any(r in name for r in (regex, "knn_select", "ball_packet")):
+                    continue
+                key = (name[:120], int(row["Grid_Size_X"]))
+                ms = (int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) * 1e-6
+                launches.setdefault(key, []).append(ms)
+        rows = [{"kernel": k[0], "grid_size": k[1], "launches": len(v),
+                 "avg_ms": sum(v) / len(v), "min_ms": min(v), "max_ms": max(v)}
+                for k, v in sorted(launches.items(), key=lambda kv: -kv[0][1])]
+        json.dump(rows, open(os.path.join(prof, f"{tag}_launches.json"), "w"), indent=1)
     bench = os.path.join(src, "bench.json")
     b = None
     if os.path.exists(bench) and os.path.getsize(bench) > 0:
