@@ -586,13 +586,15 @@ leafinfo_kernel(const nbkd_node *__restrict__ nodes, uint64_t nn, const float *_
 // leaf changes: leaf membership, the node table and every query result stay
 // the same (the kNN parity contract compares leaves and tie groups as sets),
 // and padding rows (FLT_MAX) sort last and are left out of the boxes.
-constexpr int GPL = NBKD_GBLOCK / 64; // points per lane
+// GPL points per lane: NBKD_GBLOCK / 64 = 2, or 1 when no leaf exceeds 64
+// points (leafsize <= 64: half the registers, no idle second point per lane)
 
 //
 // The same pass writes leafinfo (8 words per leaf: its tight box, the union of
 // its group boxes, and its point range), lists the leaves holding padding and
 // reduces the data bounding box (bbox as in leafinfo_kernel, which it replaces
 // whenever there are points: one lane per leaf there read 64 scattered points).
+template <int GPL>
 __global__ void __launch_bounds__(TB)
 group_kernel(const nbkd_node *__restrict__ nodes, uint64_t nn, float *__restrict__ x,
              float *__restrict__ y, float *__restrict__ z, uint32_t *__restrict__ idx, uint64_t n,
@@ -616,7 +618,7 @@ group_kernel(const nbkd_node *__restrict__ nodes, uint64_t nn, float *__restrict
             const uint32_t c = min((uint32_t)NBKD_GBLOCK, nd.right - b0);
             // point h of this lane: run position lane + 64 h
             float p[GPL][3];
-            uint32_t id[GPL], real[GPL], pos[GPL], s[GPL], l[GPL];
+            uint32_t id[GPL], real[GPL], pos[GPL], s[GPL], l[GPL], pc[GPL];
 #pragma unroll
             for (int h = 0; h < GPL; ++h) {
                 const uint32_t j = (uint32_t)(lane + 64 * h);
@@ -628,9 +630,38 @@ group_kernel(const nbkd_node *__restrict__ nodes, uint64_t nn, float *__restrict
                 real[h] = (on && id[h] < n) ? 1u : 0u;
                 pad |= on && id[h] >= n;
                 pos[h] = j;
+                pc[h] = 0;
                 s[h] = 0;
                 l[h] = on ? c : 0u;
             }
+            // the boxes of the first two cuts' pieces (the whole run, then its
+            // two halves) are wave reductions over the lanes' real points of
+            // each piece instead of every lane scanning its piece
+            float rlo[2][3], rhi[2][3];
+            auto piece_boxes = [&](int np) {
+#pragma unroll
+                for (int q = 0; q < 2; ++q) {
+                    if (q >= np) break;
+#pragma unroll
+                    for (int a = 0; a < 3; ++a) {
+                        float lo = FLT_MAX, hi = -FLT_MAX;
+#pragma unroll
+                        for (int h = 0; h < GPL; ++h) {
+                            const bool in = real[h] && pc[h] == (uint32_t)q;
+                            lo = in ? fminf(lo, p[h][a]) : lo;
+                            hi = in ? fmaxf(hi, p[h][a]) : hi;
+                        }
+#pragma unroll
+                        for (int o = 32; o > 0; o >>= 1) {
+                            lo = fminf(lo, __shfl_xor(lo, o, 64));
+                            hi = fmaxf(hi, __shfl_xor(hi, o, 64));
+                        }
+                        rlo[q][a] = lo;
+                        rhi[q][a] = hi;
+                    }
+                }
+            };
+            int cut = 0;
             for (;;) {
                 bool more = false;
 #pragma unroll
@@ -644,6 +675,7 @@ group_kernel(const nbkd_node *__restrict__ nodes, uint64_t nn, float *__restrict
                     R[pos[h]] = real[h];
                 }
                 wave_sync();
+                if (cut < 2) piece_boxes(cut + 1);
                 uint32_t npos[GPL];
 #pragma unroll
                 for (int h = 0; h < GPL; ++h) {
@@ -651,17 +683,28 @@ group_kernel(const nbkd_node *__restrict__ nodes, uint64_t nn, float *__restrict
                     if (l[h] <= (uint32_t)NBKD_GROUP) continue;
                     // pieces hold multiples of 8 points: both scans unrolled by 8,
                     // branch-free, so the LDS reads of an 8-run issue together
-                    float lo[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, hi[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
-                    for (uint32_t j0 = s[h]; j0 < s[h] + l[h]; j0 += 8) {
+                    const uint32_t q = pc[h] & 1u;
+                    float lo[3] = {q ? rlo[1][0] : rlo[0][0], q ? rlo[1][1] : rlo[0][1],
+                                   q ? rlo[1][2] : rlo[0][2]};
+                    float hi[3] = {q ? rhi[1][0] : rhi[0][0], q ? rhi[1][1] : rhi[0][1],
+                                   q ? rhi[1][2] : rhi[0][2]};
+                    if (cut >= 2) {
 #pragma unroll
-                        for (uint32_t u = 0; u < 8; ++u) {
-                            const uint32_t j = j0 + u;
-                            const bool rj = R[j] != 0u;
+                        for (int a = 0; a < 3; ++a) {
+                            lo[a] = FLT_MAX;
+                            hi[a] = -FLT_MAX;
+                        }
+                        for (uint32_t j0 = s[h]; j0 < s[h] + l[h]; j0 += 8) {
 #pragma unroll
-                            for (int a = 0; a < 3; ++a) {
-                                const float v = P[a][j];
-                                lo[a] = rj ? fminf(lo[a], v) : lo[a];
-                                hi[a] = rj ? fmaxf(hi[a], v) : hi[a];
+                            for (uint32_t u = 0; u < 8; ++u) {
+                                const uint32_t j = j0 + u;
+                                const bool rj = R[j] != 0u;
+#pragma unroll
+                                for (int a = 0; a < 3; ++a) {
+                                    const float v = P[a][j];
+                                    lo[a] = rj ? fminf(lo[a], v) : lo[a];
+                                    hi[a] = rj ? fmaxf(hi[a], v) : hi[a];
+                                }
                             }
                         }
                     }
@@ -679,6 +722,7 @@ group_kernel(const nbkd_node *__restrict__ nodes, uint64_t nn, float *__restrict
                     }
                     const uint32_t m = (l[h] / 2) / 8 * 8;
                     npos[h] = s[h] + rank;
+                    pc[h] = 2 * pc[h] + (rank < m ? 0u : 1u);
                     if (rank < m) {
                         l[h] = m;
                     } else {
@@ -689,6 +733,7 @@ group_kernel(const nbkd_node *__restrict__ nodes, uint64_t nn, float *__restrict
                 wave_sync();
 #pragma unroll
                 for (int h = 0; h < GPL; ++h) pos[h] = npos[h];
+                ++cut;
             }
 #pragma unroll
             for (int h = 0; h < GPL; ++h) {
@@ -1100,9 +1145,15 @@ nbkd_status build_tree(Tree &t, const float *xyz, uint64_t n, int32_t leaf_size,
             const char *eg = getenv("NBKD_GROUP_BLOCKS_PER_CU"); // A/B only
             const uint64_t per_cu = eg ? (uint64_t)std::max(1, atoi(eg)) : 128u;
             const uint64_t blocks = std::min<uint64_t>((t.nnodes + 3) / 4, (uint64_t)cus * per_cu);
-            group_kernel<<<(unsigned)std::max<uint64_t>(blocks, 1), TB, 0, s>>>(
-                t.nodes, t.nnodes, t.x, t.y, t.z, t.idx, t.n, t.ginfo, t.hinfo,
-                reinterpret_cast<uint32_t *>(t.leafinfo), d_bbox.as<uint32_t>());
+            // leaves hold <= max(leaf, 16) points
+            if (std::max<uint64_t>(t.leaf, 16) <= 64)
+                group_kernel<1><<<(unsigned)std::max<uint64_t>(blocks, 1), TB, 0, s>>>(
+                    t.nodes, t.nnodes, t.x, t.y, t.z, t.idx, t.n, t.ginfo, t.hinfo,
+                    reinterpret_cast<uint32_t *>(t.leafinfo), d_bbox.as<uint32_t>());
+            else
+                group_kernel<NBKD_GBLOCK / 64><<<(unsigned)std::max<uint64_t>(blocks, 1), TB, 0, s>>>(
+                    t.nodes, t.nnodes, t.x, t.y, t.z, t.idx, t.n, t.ginfo, t.hinfo,
+                    reinterpret_cast<uint32_t *>(t.leafinfo), d_bbox.as<uint32_t>());
         } else {
             uint64_t blocks = std::min<uint64_t>((t.nnodes + TB - 1) / TB, 16384);
             leafinfo_kernel<<<(unsigned)std::max<uint64_t>(blocks, 1), TB, 0, s>>>(
