@@ -100,45 +100,81 @@ prepare_kernel(const float *__restrict__ aos, uint64_t n, uint64_t n8, int perio
 }
 
 // ------------------------------------------------------------------ large levels
+// One block per run of `per` consecutive tiles of the level (a segment's
+// tiles are consecutive): the tile records and segment state are scalar
+// loads, the LDS histogram is flushed to the segment's global one only when
+// the run moves to another segment.  One tile per block made the top levels
+// (1-8 segments, 24 k tiles adding into the same 256 words) atomic-bound:
+// hist<1> 468 us at depth 0 vs 140 at depth 12 (r02bk trace).
 template <int PASS>
 __global__ void __launch_bounds__(TB)
 hist_kernel(const Tile *__restrict__ tiles, const LSeg *__restrict__ segs,
             const SelState *__restrict__ st, const float *__restrict__ key_src,
-            uint32_t *__restrict__ hist) {
+            uint32_t *__restrict__ hist, uint32_t ntile, uint32_t per) {
     __shared__ uint32_t h[256];
-    const Tile tl = tiles[blockIdx.x];
+    const uint32_t t0 = blockIdx.x * per, t1 = min(t0 + per, ntile);
     h[threadIdx.x] = 0;
+    uint32_t cur = t0 < t1 ? tiles[t0].seg : 0u;
     __syncthreads();
-    const LSeg sg = segs[tl.seg];
-    const uint32_t prefix = PASS > 0 ? st[tl.seg].prefix : 0u;
     constexpr int shift = 24 - 8 * PASS;
-    const float *src = key_src + sg.left + tl.begin;
-#pragma unroll
-    for (int r = 0; r < PER_T; ++r) {
-        uint32_t e = r * TB + threadIdx.x;
-        const uint32_t k = e < tl.count ? fkey(src[e]) : 0u;
-        const bool in = e < tl.count && ((uint64_t)k >> (shift + 8)) == prefix;
-        const uint32_t dg = (k >> shift) & 255u;
-        if constexpr (PASS > 0) {
-            if (in) atomicAdd(&h[dg], 1u);
-            continue;
+    for (uint32_t t = t0; t < t1; ++t) {
+        const Tile tl = tiles[t];
+        if (tl.seg != cur) {
+            __syncthreads();
+            const uint32_t c = h[threadIdx.x];
+            if (c) atomicAdd(&hist[(size_t)cur * 256 + threadIdx.x], c);
+            h[threadIdx.x] = 0;
+            cur = tl.seg;
+            __syncthreads();
         }
-        // pass 0 (sign + 7 exponent bits: most keys of a segment share the
-        // digit, and 64 same-address LDS atomics serialise): one atomic per
-        // wave when its keys share the digit.  1e8: 314 -> 198 us per level.
-        const uint64_t im = __ballot(in);
-        if (im == 0) continue;
-        const uint32_t d0 = __builtin_amdgcn_readlane(dg, __builtin_ctzll(im));
-        if (__ballot(in && dg == d0) == im) {
-            if ((threadIdx.x & 63u) == (uint32_t)__builtin_ctzll(im))
-                atomicAdd(&h[d0], (uint32_t)__popcll(im));
-        } else if (in) {
-            atomicAdd(&h[dg], 1u);
+        const LSeg sg = segs[tl.seg];
+        const uint32_t prefix = PASS > 0 ? st[tl.seg].prefix : 0u;
+        // 16-B loads (segments start at multiples of 8 points and hold
+        // multiples of 8, so a float4 never straddles a tile's end); the key
+        // order inside a tile does not matter to a histogram
+        const float4 *src4 = reinterpret_cast<const float4 *>(key_src + sg.left + tl.begin);
+        float4 v[PER_T / 4];
+#pragma unroll
+        for (int r = 0; r < PER_T / 4; ++r) {
+            const uint32_t e4 = r * TB + threadIdx.x;
+            v[r] = 4 * e4 < tl.count ? src4[e4] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        }
+#pragma unroll
+        for (int r = 0; r < PER_T; ++r) {
+            const uint32_t e = 4 * ((r / 4) * TB + threadIdx.x) + (r % 4);
+            const float4 q = v[r / 4];
+            const float f = r % 4 == 0 ? q.x : r % 4 == 1 ? q.y : r % 4 == 2 ? q.z : q.w;
+            const uint32_t k = e < tl.count ? fkey(f) : 0u;
+            const bool in = e < tl.count && ((uint64_t)k >> (shift + 8)) == prefix;
+            const uint32_t dg = (k >> shift) & 255u;
+            if constexpr (PASS > 0) {
+                if (in) atomicAdd(&h[dg], 1u);
+                continue;
+            }
+            // pass 0 (sign + 7 exponent bits: a segment's keys share one to
+            // three digits, and same-address LDS atomics serialise): the
+            // wave's first two digits take one atomic each, other keys one per
+            // lane.  1e8, 16 levels: 3.2 ms with per-lane atomics, 2.4 with the
+            // first digit aggregated, 2.0 with two (r02bk, r02br, r02bs).
+            const uint64_t im = __ballot(in);
+            if (im == 0) continue;
+            const int l0 = __builtin_ctzll(im);
+            const uint32_t d0 = __builtin_amdgcn_readlane(dg, l0);
+            const uint64_t m0 = __ballot(in && dg == d0);
+            const uint64_t r0 = im & ~m0;
+            const int lane = threadIdx.x & 63;
+            if (lane == l0) atomicAdd(&h[d0], (uint32_t)__popcll(m0));
+            if (r0 == 0) continue;
+            const int l1 = __builtin_ctzll(r0);
+            const uint32_t d1 = __builtin_amdgcn_readlane(dg, l1);
+            const uint64_t m1 = __ballot(in && dg == d1);
+            if (lane == l1) atomicAdd(&h[d1], (uint32_t)__popcll(m1));
+            if (((r0 & ~m1) >> lane) & 1u) atomicAdd(&h[dg], 1u);
         }
     }
     __syncthreads();
-    uint32_t c = h[threadIdx.x];
-    if (c) atomicAdd(&hist[(size_t)tl.seg * 256 + threadIdx.x], c);
+    const uint32_t c = h[threadIdx.x];
+    if (c && t0 < t1) atomicAdd(&hist[(size_t)cur * 256 + threadIdx.x], c);
 }
 
 // block-wide exclusive scan of one value per thread (TB threads)
@@ -187,29 +223,37 @@ select_kernel(const LSeg *__restrict__ segs, SelState *__restrict__ st,
     }
 }
 
+// per tile #< and #== pivot, over runs of `per` tiles as hist_kernel
 __global__ void __launch_bounds__(TB)
 count_kernel(const Tile *__restrict__ tiles, const LSeg *__restrict__ segs,
              const SelState *__restrict__ st, const float *__restrict__ key_src,
-             uint2 *__restrict__ tile_cnt) {
+             uint2 *__restrict__ tile_cnt, uint32_t ntile, uint32_t per) {
     __shared__ uint32_t sh[TB / 64];
-    const Tile tl = tiles[blockIdx.x];
-    const LSeg sg = segs[tl.seg];
-    const uint32_t piv = st[tl.seg].prefix;
-    const float *src = key_src + sg.left + tl.begin;
-    uint32_t lt = 0, eq = 0;
+    const uint32_t t0 = blockIdx.x * per, t1 = min(t0 + per, ntile);
+    for (uint32_t t = t0; t < t1; ++t) {
+        const Tile tl = tiles[t];
+        const LSeg sg = segs[tl.seg];
+        const uint32_t piv = st[tl.seg].prefix;
+        const float4 *src4 = reinterpret_cast<const float4 *>(key_src + sg.left + tl.begin);
+        uint32_t lt = 0, eq = 0;
 #pragma unroll
-    for (int r = 0; r < PER_T; ++r) {
-        uint32_t e = r * TB + threadIdx.x;
-        if (e < tl.count) {
-            uint32_t k = fkey(src[e]);
-            lt += k < piv;
-            eq += k == piv;
+        for (int r = 0; r < PER_T / 4; ++r) {
+            const uint32_t e4 = r * TB + threadIdx.x;
+            if (4 * e4 < tl.count) {
+                const float4 q = src4[e4];
+                const uint32_t k[4] = {fkey(q.x), fkey(q.y), fkey(q.z), fkey(q.w)};
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    lt += k[u] < piv;
+                    eq += k[u] == piv;
+                }
+            }
         }
+        uint32_t tlt, teq;
+        block_excl_scan(lt, sh, &tlt);
+        block_excl_scan(eq, sh, &teq);
+        if (threadIdx.x == 0) tile_cnt[t] = make_uint2(tlt, teq);
     }
-    uint32_t tlt, teq;
-    block_excl_scan(lt, sh, &tlt);
-    block_excl_scan(eq, sh, &teq);
-    if (threadIdx.x == 0) tile_cnt[blockIdx.x] = make_uint2(tlt, teq);
 }
 
 // one block per segment: exclusive prefix of (lt, eq) over its tiles
@@ -1065,6 +1109,16 @@ nbkd_status build_tree(Tree &t, const float *xyz, uint64_t n, int32_t leaf_size,
 
     {
         TimedScope ts("build_levels", s);
+        uint32_t run_blocks = 2048;
+        {
+            int dev = 0, cus = 256;
+            if (hipGetDevice(&dev) == hipSuccess &&
+                hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
+                run_blocks = 8u * (uint32_t)std::max(cus, 1);
+            (void)hipGetLastError();
+            const char *e = getenv("NBKD_RUN_BLOCKS"); // A/B only
+            if (e) run_blocks = (uint32_t)std::max(1, atoi(e));
+        }
         for (size_t d = 0; d < info.size(); ++d) {
             const LevelInfo &li = info[d];
             if (li.nseg == 0) continue;
@@ -1076,16 +1130,20 @@ nbkd_status build_tree(Tree &t, const float *xyz, uint64_t n, int32_t leaf_size,
             const Tile *ltiles = d_tiles.as<Tile>() + li.tile0;
             SelState *st = d_st.as<SelState>();
             uint32_t *hist = d_hist.as<uint32_t>();
+            // runs of `per` tiles, ~8 blocks per CU
+            const uint32_t per = std::max<uint32_t>(1u, (li.ntile + run_blocks - 1) / run_blocks);
+            const uint32_t nrun = (li.ntile + per - 1) / per;
 #define NBKD_PASS(P)                                                                               \
     NBKD_HIP(hipMemsetAsync(hist, 0, (size_t)li.nseg * 256 * 4, s));                              \
-    hist_kernel<P><<<li.ntile, TB, 0, s>>>(ltiles, lsegs, st, key, hist);                         \
+    hist_kernel<P><<<nrun, TB, 0, s>>>(ltiles, lsegs, st, key, hist, li.ntile, per);              \
     select_kernel<P><<<li.nseg, TB, 0, s>>>(lsegs, st, hist, t.nodes, dim);
             NBKD_PASS(0)
             NBKD_PASS(1)
             NBKD_PASS(2)
             NBKD_PASS(3)
 #undef NBKD_PASS
-            count_kernel<<<li.ntile, TB, 0, s>>>(ltiles, lsegs, st, key, d_cnt.as<uint2>());
+            count_kernel<<<nrun, TB, 0, s>>>(ltiles, lsegs, st, key, d_cnt.as<uint2>(), li.ntile,
+                                             per);
             scan_kernel<<<li.nseg, TB, 0, s>>>(lsegs, d_cnt.as<uint2>(), d_off.as<uint2>(),
                                                li.tile0);
             scatter_kernel<<<li.ntile, TB, 0, s>>>(ltiles, lsegs, st, d_off.as<uint2>(), dim,
