@@ -447,10 +447,34 @@ small_kernel(const SSeg *__restrict__ list, uint32_t leaf, Soa bufA, Soa bufB,
                 for (int j = 0; j < 4; ++j) h[lane * 4 + j] = 0;
                 wave_sync();
                 // 64-bit shift: a 32-bit shift by 32 (pass 0) is poison in LLVM IR
-                for (uint32_t e = lane; e < ss.count; e += 64) {
-                    uint32_t k = fkey(kx[ss.off + e]);
-                    if (((uint64_t)k >> (shift + 8)) == prefix)
-                        atomicAdd(&h[(k >> shift) & 255u], 1u);
+                if (pass == 0) {
+                    // the sign + top exponent bits: a sub-segment's keys share
+                    // one to three digits; same-address LDS atomics serialise,
+                    // so the wave's first two digits take one atomic each (as
+                    // hist_kernel<0>)
+                    for (uint32_t e0 = 0; e0 < ss.count; e0 += 64) {
+                        const uint32_t e = e0 + lane;
+                        const bool in = e < ss.count;
+                        const uint32_t dg = in ? fkey(kx[ss.off + e]) >> 24 : 0u;
+                        const uint64_t im = __ballot(in);
+                        const int l0 = __builtin_ctzll(im);
+                        const uint32_t d0 = __builtin_amdgcn_readlane(dg, l0);
+                        const uint64_t m0 = __ballot(in && dg == d0);
+                        const uint64_t r0 = im & ~m0;
+                        if (lane == l0) atomicAdd(&h[d0], (uint32_t)__popcll(m0));
+                        if (r0 == 0) continue;
+                        const int l1 = __builtin_ctzll(r0);
+                        const uint32_t d1 = __builtin_amdgcn_readlane(dg, l1);
+                        const uint64_t m1 = __ballot(in && dg == d1);
+                        if (lane == l1) atomicAdd(&h[d1], (uint32_t)__popcll(m1));
+                        if (((r0 & ~m1) >> lane) & 1u) atomicAdd(&h[dg], 1u);
+                    }
+                } else {
+                    for (uint32_t e = lane; e < ss.count; e += 64) {
+                        uint32_t k = fkey(kx[ss.off + e]);
+                        if (((uint64_t)k >> (shift + 8)) == prefix)
+                            atomicAdd(&h[(k >> shift) & 255u], 1u);
+                    }
                 }
                 wave_sync();
                 uint32_t c0 = h[lane * 4], c1 = h[lane * 4 + 1], c2 = h[lane * 4 + 2],
