@@ -382,12 +382,200 @@ struct SmallLds {
     uint32_t hist[TB / 64][256];
     SubSeg list[2][MAX_SUB];
     uint32_t nlist[2];
+    uint32_t tsel[2][4];       // team split: per team, the pass's digit / before / eq count
+    uint32_t tcnt[TB / 64][4]; // team split: per wave, its chunk's < / == / > counts
 };
+
+// A level with one or two sub-segments (the first two levels of a block):
+// each is split by a team of TS = 4 or 2 waves instead of one wave while the
+// others idle.  Team-wide radix select (shared LDS histogram, the team's first
+// wave picks the digit) and a stable partition in which wave wt of the team
+// takes the contiguous chunk wt of the sub-segment after an exclusive count
+// over the team's earlier chunks.  Every wave reaches the same barriers (a
+// team whose sub-segment is a leaf only copies it out), and the result equals
+// the one-wave path's: the same order statistic, the same stable order.
+template <int TS>
+__device__ void team_level(SmallLds &L, const SSeg &sg, uint32_t leaf, Soa out,
+                           nbkd_node *__restrict__ nodes, const uint32_t *__restrict__ tab_c,
+                           const uint32_t *__restrict__ tab_n, int tab_len, int cur, int lc) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t s = (uint32_t)wave / TS, wt = (uint32_t)wave % TS;
+    const SubSeg ss = L.list[lc][s];
+    const bool work = ss.count > leaf;
+    const uint32_t tl = wt * 64 + lane; // thread within the team
+    if (!work) {
+        if (tl == 0)
+            nodes[ss.node] = nbkd_node{-1, 0.0f, sg.left + ss.off, sg.left + ss.off + ss.count};
+        for (uint32_t e = tl; e < ss.count; e += 64 * TS) {
+            const uint32_t g = sg.left + ss.off + e;
+            out.x[g] = L.x[cur][ss.off + e];
+            out.y[g] = L.y[cur][ss.off + e];
+            out.z[g] = L.z[cur][ss.off + e];
+            out.i[g] = L.i[cur][ss.off + e];
+        }
+    }
+    const float *kx = ss.dim == 0 ? L.x[cur] : (ss.dim == 1 ? L.y[cur] : L.z[cur]);
+    const uint32_t m = (ss.count / 2) / 8 * 8;
+    uint32_t rank = m, prefix = 0, below = 0, eqc = 0;
+    uint32_t *h = L.hist[s * TS];
+#pragma unroll 1
+    for (int pass = 0; pass < 4; ++pass) {
+        const int shift = 24 - 8 * pass;
+        for (uint32_t b = tl; b < 256; b += 64 * TS) h[b] = 0;
+        __syncthreads();
+        if (work) {
+            if (pass == 0) {
+                // first two digits of the wave aggregated, as small_kernel's pass 0
+                for (uint32_t e0 = wt * 64; e0 < ss.count; e0 += 64 * TS) {
+                    const uint32_t e = e0 + lane;
+                    const bool in = e < ss.count;
+                    const uint32_t dg = in ? fkey(kx[ss.off + e]) >> 24 : 0u;
+                    const uint64_t im = __ballot(in);
+                    const int l0 = __builtin_ctzll(im);
+                    const uint32_t d0 = __builtin_amdgcn_readlane(dg, l0);
+                    const uint64_t m0 = __ballot(in && dg == d0);
+                    const uint64_t r0 = im & ~m0;
+                    if (lane == l0) atomicAdd(&h[d0], (uint32_t)__popcll(m0));
+                    if (r0 == 0) continue;
+                    const int l1 = __builtin_ctzll(r0);
+                    const uint32_t d1 = __builtin_amdgcn_readlane(dg, l1);
+                    const uint64_t m1 = __ballot(in && dg == d1);
+                    if (lane == l1) atomicAdd(&h[d1], (uint32_t)__popcll(m1));
+                    if (((r0 & ~m1) >> lane) & 1u) atomicAdd(&h[dg], 1u);
+                }
+            } else {
+                for (uint32_t e = tl; e < ss.count; e += 64 * TS) {
+                    const uint32_t k = fkey(kx[ss.off + e]);
+                    if (((uint64_t)k >> (shift + 8)) == prefix) atomicAdd(&h[(k >> shift) & 255u], 1u);
+                }
+            }
+        }
+        __syncthreads();
+        if (work && wt == 0) {
+            const uint32_t c0 = h[lane * 4], c1 = h[lane * 4 + 1], c2 = h[lane * 4 + 2],
+                           c3 = h[lane * 4 + 3];
+            const uint32_t sum = c0 + c1 + c2 + c3;
+            uint32_t x = sum;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = __shfl_up(x, o, 64);
+                if (lane >= o) x += y;
+            }
+            const uint32_t ex = x - sum;
+            const bool hit = rank >= ex && rank < x;
+            const int sel = __ffsll((unsigned long long)__ballot(hit)) - 1;
+            const uint32_t r = rank - ex;
+            uint32_t j = 0, acc = 0, cc = c0;
+            if (r >= c0) {
+                acc = c0;
+                j = 1;
+                cc = c1;
+                if (r >= c0 + c1) {
+                    acc = c0 + c1;
+                    j = 2;
+                    cc = c2;
+                    if (r >= c0 + c1 + c2) {
+                        acc = c0 + c1 + c2;
+                        j = 3;
+                        cc = c3;
+                    }
+                }
+            }
+            const uint32_t digit = 4u * (uint32_t)sel + __shfl(j, sel, 64);
+            const uint32_t before = __shfl(ex + acc, sel, 64);
+            const uint32_t ecnt = __shfl(cc, sel, 64);
+            if (lane == 0) {
+                L.tsel[s][0] = digit;
+                L.tsel[s][1] = before;
+                L.tsel[s][2] = ecnt;
+            }
+        }
+        __syncthreads();
+        if (work) {
+            const uint32_t digit = L.tsel[s][0], before = L.tsel[s][1];
+            eqc = L.tsel[s][2];
+            prefix = (prefix << 8) | digit;
+            below += before;
+            rank -= before;
+        }
+    }
+    const uint32_t piv = prefix, need = m - below;
+    // the team's chunks: wave wt takes [wt * cw, (wt + 1) * cw), cw a multiple of 64
+    const uint32_t cw = (ss.count + 64 * TS - 1) / (64 * TS) * 64;
+    const uint32_t c_lo = min(wt * cw, ss.count), c_hi = min(c_lo + cw, ss.count);
+    uint32_t clt = 0, ceq = 0;
+    if (work) {
+        for (uint32_t e0 = c_lo; e0 < c_hi; e0 += 64) {
+            const uint32_t e = e0 + lane;
+            const bool valid = e < c_hi;
+            const uint32_t k = valid ? fkey(kx[ss.off + e]) : 0u;
+            clt += (uint32_t)__popcll(__ballot(valid && k < piv));
+            ceq += (uint32_t)__popcll(__ballot(valid && k == piv));
+        }
+        if (lane == 0) {
+            L.tcnt[wave][0] = clt;
+            L.tcnt[wave][1] = ceq;
+        }
+    }
+    __syncthreads();
+    if (work) {
+        uint32_t nlt = 0, neq = 0, ngt = 0;
+        for (uint32_t w = 0; w < wt; ++w) {
+            const uint32_t a = L.tcnt[s * TS + w][0], b = L.tcnt[s * TS + w][1];
+            const uint32_t n = min(cw, ss.count - min(w * cw, ss.count));
+            nlt += a;
+            neq += b;
+            ngt += n - a - b;
+        }
+        for (uint32_t e0 = c_lo; e0 < c_hi; e0 += 64) {
+            const uint32_t e = e0 + lane;
+            const bool valid = e < c_hi;
+            uint32_t c = 3;
+            float px = 0, py = 0, pz = 0;
+            uint32_t pi = 0;
+            if (valid) {
+                px = L.x[cur][ss.off + e];
+                py = L.y[cur][ss.off + e];
+                pz = L.z[cur][ss.off + e];
+                pi = L.i[cur][ss.off + e];
+                const uint32_t k = fkey(pick(ss.dim, px, py, pz));
+                c = k < piv ? 0u : (k == piv ? 1u : 2u);
+            }
+            const uint64_t b0 = __ballot(c == 0), b1 = __ballot(c == 1), b2 = __ballot(c == 2);
+            if (valid) {
+                uint32_t d;
+                if (c == 0) {
+                    d = nlt + mbcnt64(b0);
+                } else if (c == 1) {
+                    const uint32_t er = neq + mbcnt64(b1);
+                    d = er < need ? below + er : m + (er - need);
+                } else {
+                    d = m + (eqc - need) + ngt + mbcnt64(b2);
+                }
+                L.x[cur ^ 1][ss.off + d] = px;
+                L.y[cur ^ 1][ss.off + d] = py;
+                L.z[cur ^ 1][ss.off + d] = pz;
+                L.i[cur ^ 1][ss.off + d] = pi;
+            }
+            nlt += __popcll(b0);
+            neq += __popcll(b1);
+            ngt += __popcll(b2);
+        }
+        if (tl == 0) {
+            const uint32_t rid = ss.node + 1 + subtree_nodes(m, leaf, tab_c, tab_n, tab_len);
+            nodes[ss.node] = nbkd_node{(int32_t)ss.dim, fkey_inv(piv), ss.node + 1, rid};
+            const uint32_t slot = atomicAdd(&L.nlist[lc ^ 1], 2u);
+            const uint32_t nd = (ss.dim + 1) % 3;
+            L.list[lc ^ 1][slot] = SubSeg{ss.node + 1, ss.off, m, nd};
+            L.list[lc ^ 1][slot + 1] = SubSeg{rid, ss.off + m, ss.count - m, nd};
+        }
+    }
+}
 
 __global__ void __launch_bounds__(TB)
 small_kernel(const SSeg *__restrict__ list, uint32_t leaf, Soa bufA, Soa bufB,
              nbkd_node *__restrict__ nodes, const uint32_t *__restrict__ tab_c,
-             const uint32_t *__restrict__ tab_n, int tab_len) {
+             const uint32_t *__restrict__ tab_n, int tab_len, int team) {
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
     SmallLds &L = *reinterpret_cast<SmallLds *>(smem_raw);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -421,6 +609,12 @@ small_kernel(const SSeg *__restrict__ list, uint32_t leaf, Soa bufA, Soa bufB,
     int cur = 0, lc = 0;
     while (L.nlist[lc] > 0) {
         const uint32_t nsub = L.nlist[lc];
+        if (nsub <= 2 && team) {
+            if (nsub == 1)
+                team_level<4>(L, sg, leaf, out, nodes, tab_c, tab_n, tab_len, cur, lc);
+            else
+                team_level<2>(L, sg, leaf, out, nodes, tab_c, tab_n, tab_len, cur, lc);
+        } else
         for (uint32_t s = wave; s < nsub; s += TB / 64) {
             const SubSeg ss = L.list[lc][s];
             if (ss.count <= leaf) {
@@ -1177,13 +1371,17 @@ nbkd_status build_tree(Tree &t, const float *xyz, uint64_t n, int32_t leaf_size,
     }
     {
         TimedScope ts("build_small", s);
+        static const int small_team = [] { // NBKD_SMALL_TEAM=0: one wave per sub-segment (A/B)
+            const char *e = getenv("NBKD_SMALL_TEAM");
+            return (e && atoi(e) == 0) ? 0 : 1;
+        }();
         if (!sk.small.empty()) {
             NBKD_HIP(hipFuncSetAttribute((const void *)small_kernel,
                                          hipFuncAttributeMaxDynamicSharedMemorySize,
                                          (int)sizeof(SmallLds)));
             small_kernel<<<(unsigned)sk.small.size(), TB, sizeof(SmallLds), s>>>(
                 d_small.as<SSeg>(), leaf, A, B, t.nodes, d_tabc.as<uint32_t>(),
-                d_tabn.as<uint32_t>(), (int)tab_c.size());
+                d_tabn.as<uint32_t>(), (int)tab_c.size(), small_team);
             NBKD_HIP(hipGetLastError());
         }
     }
