@@ -41,18 +41,20 @@ struct DeviceGuard {
 };
 
 void free_tree(Tree &t) {
-    if (t.x) (void)hipFree(t.x);
-    if (t.y) (void)hipFree(t.y);
-    if (t.z) (void)hipFree(t.z);
-    if (t.idx) (void)hipFree(t.idx);
-    if (t.nodes) (void)hipFree(t.nodes);
-    if (t.splits) (void)hipFree(t.splits);
-    if (t.shape_c) (void)hipFree(t.shape_c);
-    if (t.shape_n) (void)hipFree(t.shape_n);
-    if (t.leafinfo) (void)hipFree(t.leafinfo);
-    if (t.hsplit) (void)hipFree(t.hsplit);
-    if (t.ginfo) (void)hipFree(t.ginfo);
-    if (t.hinfo) (void)hipFree(t.hinfo);
+    // no kernel of this tree may still run when its blocks are reused
+    if (t.x || t.nodes) (void)hipDeviceSynchronize();
+    tree_free(t.x);
+    tree_free(t.y);
+    tree_free(t.z);
+    tree_free(t.idx);
+    tree_free(t.nodes);
+    tree_free(t.splits);
+    tree_free(t.shape_c);
+    tree_free(t.shape_n);
+    tree_free(t.leafinfo);
+    tree_free(t.hsplit);
+    tree_free(t.ginfo);
+    tree_free(t.hinfo);
     t.ginfo = t.hinfo = nullptr;
     t.leafinfo = nullptr;
     t.hsplit = nullptr;
@@ -64,6 +66,78 @@ void free_tree(Tree &t) {
     t.ws.release();
 }
 } // namespace
+
+namespace {
+struct BlockCache {
+    std::mutex mu;
+    std::map<void *, std::pair<int, size_t>> live;             // block -> (device, bytes)
+    std::multimap<std::pair<int, size_t>, void *> idle;         // (device, bytes) -> block
+    size_t idle_bytes = 0;
+    static constexpr size_t CAP = 64ull << 30;                  // idle bytes kept, all devices
+};
+BlockCache &block_cache() {
+    static BlockCache c;
+    return c;
+}
+} // namespace
+
+hipError_t tree_malloc(void **p, size_t bytes) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    bytes = bytes ? bytes : 16;
+    BlockCache &c = block_cache();
+    {
+        std::lock_guard<std::mutex> g(c.mu);
+        auto it = c.idle.find({dev, bytes});
+        if (it != c.idle.end()) {
+            *p = it->second;
+            c.idle.erase(it);
+            c.idle_bytes -= bytes;
+            c.live[*p] = {dev, bytes};
+            return hipSuccess;
+        }
+    }
+    e = hipMalloc(p, bytes);
+    if (e == hipErrorOutOfMemory) { // return this device's idle blocks and retry once
+        (void)hipGetLastError();
+        std::lock_guard<std::mutex> g(c.mu);
+        for (auto it = c.idle.begin(); it != c.idle.end();) {
+            if (it->first.first == dev) {
+                (void)hipFree(it->second);
+                c.idle_bytes -= it->first.second;
+                it = c.idle.erase(it);
+            } else {
+                ++it;
+            }
+        }
+        e = hipMalloc(p, bytes);
+    }
+    if (e != hipSuccess) return e;
+    std::lock_guard<std::mutex> g(c.mu);
+    c.live[*p] = {dev, bytes};
+    return hipSuccess;
+}
+
+void tree_free(void *p) {
+    if (!p) return;
+    BlockCache &c = block_cache();
+    std::lock_guard<std::mutex> g(c.mu);
+    auto it = c.live.find(p);
+    if (it == c.live.end()) {
+        (void)hipFree(p);
+        return;
+    }
+    const auto key = it->second;
+    c.live.erase(it);
+    if (c.idle_bytes + key.second <= BlockCache::CAP) {
+        c.idle.insert({key, p});
+        c.idle_bytes += key.second;
+    } else {
+        (void)hipFree(p);
+    }
+}
+
 
 void set_error(const std::string &msg) { g_err = msg; }
 

@@ -1202,6 +1202,54 @@ struct Skeleton {
 
 } // namespace
 
+namespace {
+
+// Build scratch (the B ping-pong copy of the points, the level tables, the
+// input staging copy): one device buffer per device, kept between builds and
+// grown on demand, carved into 256-B aligned pieces.  A build holds its
+// device's lock until it has synchronised its stream, so builds on one device
+// never share the buffer while kernels use it.  Per build this saves ~15
+// hipMalloc/hipFree pairs, four of them n * 4 bytes (r02ce).
+struct LevelInfo {
+    uint32_t seg0, nseg, tile0, ntile;
+};
+// The tree's shape (segments, tiles, small subtrees, the count -> node-count
+// table) is a pure function of (n8, leaf): rebuilding a tree of the same size
+// (a simulation's every step) reuses the host tables and their device copies.
+// Enumerating them took ~3.4 ms of host time before the first kernel at 1e8.
+struct ShapeTables {
+    bool valid = false, uploaded = false;
+    uint64_t n8 = 0;
+    uint32_t leaf = 0;
+    std::vector<LSeg> segs;
+    std::vector<Tile> tiles;
+    std::vector<LevelInfo> info;
+    std::vector<SSeg> small;
+    std::vector<uint32_t> tab_c, tab_n;
+    size_t max_seg = 0, max_tile = 0;
+};
+struct BuildScratch {
+    std::mutex mu;
+    void *p = nullptr;
+    size_t bytes = 0;
+    ShapeTables shape;
+};
+BuildScratch &build_scratch(int dev) {
+    static BuildScratch pool[64];
+    return pool[dev & 63];
+}
+
+struct Carve {
+    size_t off = 0;
+    size_t take(size_t b) {
+        const size_t o = off;
+        off += (std::max<size_t>(b, 16) + 255) / 256 * 256;
+        return o;
+    }
+};
+
+} // namespace
+
 nbkd_status build_tree(Tree &t, const float *xyz, uint64_t n, int32_t leaf_size, bool input_dev,
                        hipStream_t s) {
     const uint64_t n8 = (n + 7) / 8 * 8;
@@ -1224,107 +1272,143 @@ nbkd_status build_tree(Tree &t, const float *xyz, uint64_t n, int32_t leaf_size,
     t.depth = sk.depth_of(n8);
 
     const size_t pbytes = (size_t)std::max<uint64_t>(n8, 1) * 4;
-    NBKD_HIP(hipMalloc(&t.x, pbytes));
-    NBKD_HIP(hipMalloc(&t.y, pbytes));
-    NBKD_HIP(hipMalloc(&t.z, pbytes));
-    NBKD_HIP(hipMalloc(&t.idx, pbytes));
-    NBKD_HIP(hipMalloc(&t.nodes, t.nnodes * sizeof(nbkd_node)));
+    NBKD_HIP(tree_malloc((void **)&t.x, pbytes));
+    NBKD_HIP(tree_malloc((void **)&t.y, pbytes));
+    NBKD_HIP(tree_malloc((void **)&t.z, pbytes));
+    NBKD_HIP(tree_malloc((void **)&t.idx, pbytes));
+    NBKD_HIP(tree_malloc((void **)&t.nodes, t.nnodes * sizeof(nbkd_node)));
     Soa A{t.x, t.y, t.z, t.idx};
 
-    DevBuf bx, by, bz, bi, dev_in, bad;
-    NBKD_HIP(bx.alloc(pbytes, s));
-    NBKD_HIP(by.alloc(pbytes, s));
-    NBKD_HIP(bz.alloc(pbytes, s));
-    NBKD_HIP(bi.alloc(pbytes, s));
-    Soa B{bx.as<float>(), by.as<float>(), bz.as<float>(), bi.as<uint32_t>()};
+    int dev = 0;
+    NBKD_HIP(hipGetDevice(&dev));
+    BuildScratch &scr = build_scratch(dev);
+    // held until the stream has drained, on every return path
+    struct ScratchLock {
+        BuildScratch &b;
+        hipStream_t s;
+        ScratchLock(BuildScratch &b_, hipStream_t s_) : b(b_), s(s_) { b.mu.lock(); }
+        ~ScratchLock() {
+            (void)hipStreamSynchronize(s);
+            b.mu.unlock();
+        }
+    } scr_lock(scr, s);
+    ShapeTables &sh = scr.shape;
+    if (!(sh.valid && sh.n8 == n8 && sh.leaf == leaf)) {
+        // enumerate the shape down to SMALL-point segments
+        sh.valid = sh.uploaded = false;
+        sk.rec(0, 0, (uint32_t)n8, 0);
+        sh.tab_c.clear();
+        sh.tab_n.clear();
+        for (auto &kv : sk.memo) {
+            sh.tab_c.push_back((uint32_t)kv.first);
+            sh.tab_n.push_back(kv.second);
+        }
+        if (sh.tab_c.empty()) {
+            sh.tab_c.push_back(0);
+            sh.tab_n.push_back(1);
+        }
+        // flatten large levels and their tiles
+        sh.segs.clear();
+        sh.tiles.clear();
+        sh.info.clear();
+        sh.max_seg = sh.max_tile = 0;
+        for (auto &lv : sk.levels) {
+            LevelInfo li{(uint32_t)sh.segs.size(), (uint32_t)lv.size(), (uint32_t)sh.tiles.size(), 0};
+            for (uint32_t si = 0; si < lv.size(); ++si) {
+                LSeg g = lv[si];
+                g.tile_begin = (uint32_t)sh.tiles.size();
+                for (uint32_t b = 0; b < g.count; b += TILE)
+                    sh.tiles.push_back(Tile{si, b, std::min<uint32_t>(TILE, g.count - b), 0});
+                g.tile_end = (uint32_t)sh.tiles.size();
+                sh.segs.push_back(g);
+            }
+            li.ntile = (uint32_t)sh.tiles.size() - li.tile0;
+            sh.max_seg = std::max<size_t>(sh.max_seg, li.nseg);
+            sh.max_tile = std::max<size_t>(sh.max_tile, li.ntile);
+            sh.info.push_back(li);
+        }
+        sh.small = std::move(sk.small);
+        sh.n8 = n8;
+        sh.leaf = leaf;
+        sh.valid = true;
+    }
+    const std::vector<LSeg> &segs = sh.segs;
+    const std::vector<Tile> &tiles = sh.tiles;
+    const std::vector<LevelInfo> &info = sh.info;
+    const std::vector<SSeg> &small = sh.small;
+    const std::vector<uint32_t> &tab_c = sh.tab_c, &tab_n = sh.tab_n;
+    const size_t max_seg = sh.max_seg, max_tile = sh.max_tile;
+
+    // scratch: carve every temporary from the device's cached buffer (the
+    // read-only shape tables first, so their place does not depend on the input)
+    constexpr int NW = 7 + NBKD_PAD_LEAVES; // data box, padding leaves (group_kernel)
+    Carve cv;
+    const size_t o_segs = cv.take(segs.size() * sizeof(LSeg));
+    const size_t o_tiles = cv.take(tiles.size() * sizeof(Tile));
+    const size_t o_small = cv.take(small.size() * sizeof(SSeg));
+    const size_t o_tabc = cv.take(tab_c.size() * 4);
+    const size_t o_tabn = cv.take(tab_n.size() * 4);
+    const size_t o_bx = cv.take(pbytes), o_by = cv.take(pbytes), o_bz = cv.take(pbytes),
+                 o_bi = cv.take(pbytes);
+    const size_t o_bad = cv.take(sizeof(uint32_t) * (NW + 1));
+    const size_t o_st = cv.take(max_seg * sizeof(SelState));
+    const size_t o_hist = cv.take(max_seg * 256 * sizeof(uint32_t));
+    const size_t o_cnt = cv.take(max_tile * sizeof(uint2));
+    const size_t o_off = cv.take(max_tile * sizeof(uint2));
+    const size_t o_in = cv.take(!input_dev && n > 0 ? n * 3 * sizeof(float) : 0);
+    if (scr.bytes < cv.off) {
+        sh.uploaded = false;
+        if (scr.p) NBKD_HIP(hipFree(scr.p));
+        scr.p = nullptr;
+        scr.bytes = 0;
+        NBKD_HIP(hipMalloc(&scr.p, cv.off));
+        scr.bytes = cv.off;
+    }
+    char *const base = static_cast<char *>(scr.p);
+    auto at = [&](size_t o) { return static_cast<void *>(base + o); };
+    Soa B{(float *)at(o_bx), (float *)at(o_by), (float *)at(o_bz), (uint32_t *)at(o_bi)};
+    uint32_t *const d_bad = (uint32_t *)at(o_bad); // [0]: box check, [1..]: group_kernel words
+    const LSeg *const d_segs = (const LSeg *)at(o_segs);
+    const Tile *const d_tiles = (const Tile *)at(o_tiles);
+    SelState *const d_st = (SelState *)at(o_st);
+    uint32_t *const d_hist = (uint32_t *)at(o_hist);
+    uint2 *const d_cnt = (uint2 *)at(o_cnt), *const d_off = (uint2 *)at(o_off);
+    const SSeg *const d_small = (const SSeg *)at(o_small);
+    const uint32_t *const d_tabc = (const uint32_t *)at(o_tabc);
+    const uint32_t *const d_tabn = (const uint32_t *)at(o_tabn);
 
     const float *aos = xyz;
     if (!input_dev && n > 0) {
-        NBKD_HIP(dev_in.alloc(n * 3 * sizeof(float), s));
-        NBKD_HIP(hipMemcpyAsync(dev_in.p, xyz, n * 3 * sizeof(float), hipMemcpyHostToDevice, s));
-        NBKD_HIP(hipStreamSynchronize(s));
-        aos = dev_in.as<float>();
+        NBKD_HIP(hipMemcpyAsync(at(o_in), xyz, n * 3 * sizeof(float), hipMemcpyHostToDevice, s));
+        aos = (const float *)at(o_in);
     }
-    NBKD_HIP(bad.alloc(sizeof(uint32_t), s));
-    NBKD_HIP(hipMemsetAsync(bad.p, 0, sizeof(uint32_t), s));
+    NBKD_HIP(hipMemsetAsync(d_bad, 0, sizeof(uint32_t), s));
     {
         TimedScope ts("prepare", s);
         uint64_t blocks = std::min<uint64_t>((n8 + TB - 1) / TB, 8192);
         if (blocks == 0) blocks = 1;
-        prepare_kernel<<<(unsigned)blocks, TB, 0, s>>>(aos, n, n8, t.periodic, t.box, A,
-                                                        bad.as<uint32_t>());
+        prepare_kernel<<<(unsigned)blocks, TB, 0, s>>>(aos, n, n8, t.periodic, t.box, A, d_bad);
         NBKD_HIP(hipGetLastError());
     }
-    if (t.periodic) {
-        uint32_t hbad = 0;
-        NBKD_HIP(hipMemcpyAsync(&hbad, bad.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-        NBKD_HIP(hipStreamSynchronize(s));
-        if (hbad) {
-            set_error("When using periodic boundary conditions, all points must be within the "
-                      "box (0 <= x <= box_size).");
-            return NBKD_EBOX;
+    // the shape tables (pageable copies, stream-ordered after prepare), once
+    // per shape and scratch buffer
+    if (!sh.uploaded) {
+        if (!segs.empty()) {
+            NBKD_HIP(hipMemcpyAsync(at(o_segs), segs.data(), segs.size() * sizeof(LSeg),
+                                    hipMemcpyHostToDevice, s));
+            NBKD_HIP(hipMemcpyAsync(at(o_tiles), tiles.data(), tiles.size() * sizeof(Tile),
+                                    hipMemcpyHostToDevice, s));
         }
-    }
-
-    // enumerate the shape down to SMALL-point segments
-    sk.rec(0, 0, (uint32_t)n8, 0);
-    std::vector<uint32_t> tab_c, tab_n;
-    for (auto &kv : sk.memo) {
-        tab_c.push_back((uint32_t)kv.first);
-        tab_n.push_back(kv.second);
-    }
-    if (tab_c.empty()) {
-        tab_c.push_back(0);
-        tab_n.push_back(1);
-    }
-
-    // flatten large levels and their tiles
-    std::vector<LSeg> segs;
-    std::vector<Tile> tiles;
-    struct LevelInfo {
-        uint32_t seg0, nseg, tile0, ntile;
-    };
-    std::vector<LevelInfo> info;
-    size_t max_seg = 0, max_tile = 0;
-    for (auto &lv : sk.levels) {
-        LevelInfo li{(uint32_t)segs.size(), (uint32_t)lv.size(), (uint32_t)tiles.size(), 0};
-        for (uint32_t si = 0; si < lv.size(); ++si) {
-            LSeg g = lv[si];
-            g.tile_begin = (uint32_t)tiles.size();
-            for (uint32_t b = 0; b < g.count; b += TILE)
-                tiles.push_back(Tile{si, b, std::min<uint32_t>(TILE, g.count - b), 0});
-            g.tile_end = (uint32_t)tiles.size();
-            segs.push_back(g);
-        }
-        li.ntile = (uint32_t)tiles.size() - li.tile0;
-        max_seg = std::max<size_t>(max_seg, li.nseg);
-        max_tile = std::max<size_t>(max_tile, li.ntile);
-        info.push_back(li);
-    }
-
-    DevBuf d_segs, d_tiles, d_st, d_hist, d_cnt, d_off, d_small, d_tabc, d_tabn;
-    if (!segs.empty()) {
-        NBKD_HIP(d_segs.alloc(segs.size() * sizeof(LSeg), s));
-        NBKD_HIP(d_tiles.alloc(tiles.size() * sizeof(Tile), s));
-        NBKD_HIP(d_st.alloc(max_seg * sizeof(SelState), s));
-        NBKD_HIP(d_hist.alloc(max_seg * 256 * sizeof(uint32_t), s));
-        NBKD_HIP(d_cnt.alloc(max_tile * sizeof(uint2), s));
-        NBKD_HIP(d_off.alloc(max_tile * sizeof(uint2), s));
-        NBKD_HIP(hipMemcpyAsync(d_segs.p, segs.data(), segs.size() * sizeof(LSeg),
+        NBKD_HIP(hipMemcpyAsync(at(o_small), small.data(), small.size() * sizeof(SSeg),
                                 hipMemcpyHostToDevice, s));
-        NBKD_HIP(hipMemcpyAsync(d_tiles.p, tiles.data(), tiles.size() * sizeof(Tile),
-                                hipMemcpyHostToDevice, s));
-        NBKD_HIP(hipStreamSynchronize(s));
+        NBKD_HIP(hipMemcpyAsync(at(o_tabc), tab_c.data(), tab_c.size() * 4, hipMemcpyHostToDevice,
+                                s));
+        NBKD_HIP(hipMemcpyAsync(at(o_tabn), tab_n.data(), tab_n.size() * 4, hipMemcpyHostToDevice,
+                                s));
+        sh.uploaded = true;
     }
-    NBKD_HIP(d_small.alloc(sk.small.size() * sizeof(SSeg), s));
-    NBKD_HIP(hipMemcpyAsync(d_small.p, sk.small.data(), sk.small.size() * sizeof(SSeg),
-                            hipMemcpyHostToDevice, s));
-    NBKD_HIP(d_tabc.alloc(tab_c.size() * 4, s));
-    NBKD_HIP(d_tabn.alloc(tab_n.size() * 4, s));
-    NBKD_HIP(hipMemcpyAsync(d_tabc.p, tab_c.data(), tab_c.size() * 4, hipMemcpyHostToDevice, s));
-    NBKD_HIP(hipMemcpyAsync(d_tabn.p, tab_n.data(), tab_n.size() * 4, hipMemcpyHostToDevice, s));
-    NBKD_HIP(hipStreamSynchronize(s));
-
+    // periodic box check: read back with the build's last words (the kernels
+    // below run on any input; a bad box discards the tree)
     {
         TimedScope ts("build_levels", s);
         uint32_t run_blocks = 2048;
@@ -1344,10 +1428,10 @@ nbkd_status build_tree(Tree &t, const float *xyz, uint64_t n, int32_t leaf_size,
             const Soa src = (d & 1) ? B : A;
             const Soa dst = (d & 1) ? A : B;
             const float *key = dim == 0 ? src.x : (dim == 1 ? src.y : src.z);
-            const LSeg *lsegs = d_segs.as<LSeg>() + li.seg0;
-            const Tile *ltiles = d_tiles.as<Tile>() + li.tile0;
-            SelState *st = d_st.as<SelState>();
-            uint32_t *hist = d_hist.as<uint32_t>();
+            const LSeg *lsegs = d_segs + li.seg0;
+            const Tile *ltiles = d_tiles + li.tile0;
+            SelState *st = d_st;
+            uint32_t *hist = d_hist;
             // runs of `per` tiles, ~8 blocks per CU
             const uint32_t per = std::max<uint32_t>(1u, (li.ntile + run_blocks - 1) / run_blocks);
             const uint32_t nrun = (li.ntile + per - 1) / per;
@@ -1360,11 +1444,11 @@ nbkd_status build_tree(Tree &t, const float *xyz, uint64_t n, int32_t leaf_size,
             NBKD_PASS(2)
             NBKD_PASS(3)
 #undef NBKD_PASS
-            count_kernel<<<nrun, TB, 0, s>>>(ltiles, lsegs, st, key, d_cnt.as<uint2>(), li.ntile,
+            count_kernel<<<nrun, TB, 0, s>>>(ltiles, lsegs, st, key, d_cnt, li.ntile,
                                              per);
-            scan_kernel<<<li.nseg, TB, 0, s>>>(lsegs, d_cnt.as<uint2>(), d_off.as<uint2>(),
+            scan_kernel<<<li.nseg, TB, 0, s>>>(lsegs, d_cnt, d_off,
                                                li.tile0);
-            scatter_kernel<<<li.ntile, TB, 0, s>>>(ltiles, lsegs, st, d_off.as<uint2>(), dim,
+            scatter_kernel<<<li.ntile, TB, 0, s>>>(ltiles, lsegs, st, d_off, dim,
                                                    src, dst);
             NBKD_HIP(hipGetLastError());
         }
@@ -1375,20 +1459,20 @@ nbkd_status build_tree(Tree &t, const float *xyz, uint64_t n, int32_t leaf_size,
             const char *e = getenv("NBKD_SMALL_TEAM");
             return (e && atoi(e) == 0) ? 0 : 1;
         }();
-        if (!sk.small.empty()) {
+        if (!small.empty()) {
             NBKD_HIP(hipFuncSetAttribute((const void *)small_kernel,
                                          hipFuncAttributeMaxDynamicSharedMemorySize,
                                          (int)sizeof(SmallLds)));
-            small_kernel<<<(unsigned)sk.small.size(), TB, sizeof(SmallLds), s>>>(
-                d_small.as<SSeg>(), leaf, A, B, t.nodes, d_tabc.as<uint32_t>(),
-                d_tabn.as<uint32_t>(), (int)tab_c.size(), small_team);
+            small_kernel<<<(unsigned)small.size(), TB, sizeof(SmallLds), s>>>(
+                d_small, leaf, A, B, t.nodes, d_tabc,
+                d_tabn, (int)tab_c.size(), small_team);
             NBKD_HIP(hipGetLastError());
         }
     }
     // descent helpers for query bucketing: split per node + the shape table
-    NBKD_HIP(hipMalloc(&t.splits, std::max<uint64_t>(t.nnodes, 1) * 4));
-    NBKD_HIP(hipMalloc(&t.shape_c, tab_c.size() * 4));
-    NBKD_HIP(hipMalloc(&t.shape_n, tab_n.size() * 4));
+    NBKD_HIP(tree_malloc((void **)&t.splits, std::max<uint64_t>(t.nnodes, 1) * 4));
+    NBKD_HIP(tree_malloc((void **)&t.shape_c, tab_c.size() * 4));
+    NBKD_HIP(tree_malloc((void **)&t.shape_n, tab_n.size() * 4));
     t.shape_len = (int)tab_c.size();
     NBKD_HIP(hipMemcpyAsync(t.shape_c, tab_c.data(), tab_c.size() * 4, hipMemcpyHostToDevice, s));
     NBKD_HIP(hipMemcpyAsync(t.shape_n, tab_n.data(), tab_n.size() * 4, hipMemcpyHostToDevice, s));
@@ -1399,7 +1483,7 @@ nbkd_status build_tree(Tree &t, const float *xyz, uint64_t n, int32_t leaf_size,
         NBKD_HIP(hipGetLastError());
     }
     if (t.depth <= 30) {
-        NBKD_HIP(hipMalloc(&t.hsplit, std::max<uint64_t>(hblk_blocks(t.depth), 1) * 64));
+        NBKD_HIP(tree_malloc((void **)&t.hsplit, std::max<uint64_t>(hblk_blocks(t.depth), 1) * 64));
         uint64_t blocks = std::min<uint64_t>((t.nnodes + TB - 1) / TB, 16384);
         heap_splits_kernel<<<(unsigned)std::max<uint64_t>(blocks, 1), TB, 0, s>>>(
             t.nodes, t.nnodes, t.splits, t.shape_c, t.shape_n, t.shape_len, (uint32_t)t.n8,
@@ -1410,15 +1494,13 @@ nbkd_status build_tree(Tree &t, const float *xyz, uint64_t n, int32_t leaf_size,
         // groups (ginfo, hinfo) and leafinfo + padding leaves + data box in one pass
         // (leafinfo_kernel only for a tree without points)
         TimedScope ts("build_groups", s);
-        NBKD_HIP(hipMalloc(&t.leafinfo, std::max<uint64_t>(t.nnodes, 1) * 32));
-        DevBuf d_bbox;
-        constexpr int NW = 7 + NBKD_PAD_LEAVES;
-        NBKD_HIP(d_bbox.alloc(NW * 4, s));
-        uint32_t init[NW] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u, 0u, 0u};
-        NBKD_HIP(hipMemcpyAsync(d_bbox.p, init, sizeof(init), hipMemcpyHostToDevice, s));
+        NBKD_HIP(tree_malloc((void **)&t.leafinfo, std::max<uint64_t>(t.nnodes, 1) * 32));
+        uint32_t *const d_bbox = d_bad + 1;
+        static const uint32_t init[NW] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u, 0u, 0u};
+        NBKD_HIP(hipMemcpyAsync(d_bbox, init, sizeof(init), hipMemcpyHostToDevice, s));
         if (n8 > 0) {
-            NBKD_HIP(hipMalloc(&t.ginfo, (n8 / NBKD_GROUP) * 6 * sizeof(float)));
-            if (t.leaf > 64) NBKD_HIP(hipMalloc(&t.hinfo, t.nnodes * 12 * sizeof(float)));
+            NBKD_HIP(tree_malloc((void **)&t.ginfo, (n8 / NBKD_GROUP) * 6 * sizeof(float)));
+            if (t.leaf > 64) NBKD_HIP(tree_malloc((void **)&t.hinfo, t.nnodes * 12 * sizeof(float)));
             int dev = 0, cus = 256;
             NBKD_HIP(hipGetDevice(&dev));
             (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
@@ -1429,20 +1511,26 @@ nbkd_status build_tree(Tree &t, const float *xyz, uint64_t n, int32_t leaf_size,
             if (std::max<uint64_t>(t.leaf, 16) <= 64)
                 group_kernel<1><<<(unsigned)std::max<uint64_t>(blocks, 1), TB, 0, s>>>(
                     t.nodes, t.nnodes, t.x, t.y, t.z, t.idx, t.n, t.ginfo, t.hinfo,
-                    reinterpret_cast<uint32_t *>(t.leafinfo), d_bbox.as<uint32_t>());
+                    reinterpret_cast<uint32_t *>(t.leafinfo), d_bbox);
             else
                 group_kernel<NBKD_GBLOCK / 64><<<(unsigned)std::max<uint64_t>(blocks, 1), TB, 0, s>>>(
                     t.nodes, t.nnodes, t.x, t.y, t.z, t.idx, t.n, t.ginfo, t.hinfo,
-                    reinterpret_cast<uint32_t *>(t.leafinfo), d_bbox.as<uint32_t>());
+                    reinterpret_cast<uint32_t *>(t.leafinfo), d_bbox);
         } else {
             uint64_t blocks = std::min<uint64_t>((t.nnodes + TB - 1) / TB, 16384);
             leafinfo_kernel<<<(unsigned)std::max<uint64_t>(blocks, 1), TB, 0, s>>>(
-                t.nodes, t.nnodes, t.x, t.y, t.z, t.idx, t.n, t.leafinfo, d_bbox.as<uint32_t>());
+                t.nodes, t.nnodes, t.x, t.y, t.z, t.idx, t.n, t.leafinfo, d_bbox);
         }
         NBKD_HIP(hipGetLastError());
-        uint32_t hb[NW];
-        NBKD_HIP(hipMemcpyAsync(hb, d_bbox.p, sizeof(hb), hipMemcpyDeviceToHost, s));
+        uint32_t hw[NW + 1]; // box-check flag, then the data box and padding leaves
+        NBKD_HIP(hipMemcpyAsync(hw, d_bad, sizeof(hw), hipMemcpyDeviceToHost, s));
         NBKD_HIP(hipStreamSynchronize(s));
+        if (t.periodic && hw[0]) {
+            set_error("When using periodic boundary conditions, all points must be within the "
+                      "box (0 <= x <= box_size).");
+            return NBKD_EBOX;
+        }
+        const uint32_t *const hb = hw + 1;
         // padding sits in the last leaf; should ties ever spread it, up to
         // NBKD_PAD_LEAVES leaves are listed, beyond that the shortcut is off
         t.npad_leaves = (int)hb[6];

@@ -136,6 +136,14 @@ struct DevBuf {
     template <typename T> T *as() const { return static_cast<T *>(p); }
 };
 
+// Device block cache for a tree's own arrays (api.cpp): a freed tree's blocks
+// are kept per (device, size) and handed to the next allocation of that size,
+// as framework caching allocators do; hipMalloc of the four n * 4-byte point
+// arrays dominated a rebuild's host time.  tree_free follows a device
+// synchronisation in free_tree (hipFree's own semantics).
+hipError_t tree_malloc(void **p, size_t bytes);
+void tree_free(void *p);
+
 // build.hip
 nbkd_status build_tree(Tree &t, const float *xyz, uint64_t n, int32_t leaf_size, bool input_dev,
                        hipStream_t s);
