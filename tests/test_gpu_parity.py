@@ -394,3 +394,47 @@ def test_group_leaves_vs_oracle(gpu, oracle, case):
     d, i = t.query(q, k)
     dr, ir = o.query(q, k, workers=8)
     assert_knn_equal(d, i, dr, ir, pts, q, box)
+
+
+def test_build_caches_alternating_sizes_and_threads(gpu, oracle):
+    """build.hip keeps per-device scratch and shape tables keyed by (n8, leaf),
+    and api.cpp a block cache for freed trees' arrays: alternating sizes,
+    repeated same-size rebuilds (freed trees' blocks reused), builds from
+    several threads at once and a failed (out-of-box) build in between must
+    all give the oracle's node table."""
+    import threading
+
+    cases = [(70_000, 32, 1.0), (9_000, 16, None), (70_000, 32, 1.0), (131_072, 64, 1.0)]
+    refs = {}
+    for n, leaf, box in cases:
+        pts = uniform(n, 5 + n, L=box or 1.0)
+        refs[(n, leaf, box)] = (pts, oracle.tree(pts, leaf, box).export()[0].view(np.uint32))
+    for rnd in range(2):
+        for key in cases:
+            pts, ref = refs[key]
+            t = gpu.Tree(pts, leafsize=key[1], boxsize=key[2])
+            assert np.array_equal(t.export()[0].view(np.uint32), ref), (rnd, key)
+            t.close()
+        with pytest.raises(Exception, match=r"all points must be within the box"):
+            bad = np.array(refs[cases[0]][0], copy=True)
+            bad[7, 2] = 1.5
+            gpu.Tree(bad, leafsize=32, boxsize=1.0)
+    errors = []
+
+    def worker(key):
+        try:
+            pts, ref = refs[key]
+            for _ in range(3):
+                t = gpu.Tree(pts, leafsize=key[1], boxsize=key[2])
+                if not np.array_equal(t.export()[0].view(np.uint32), ref):
+                    errors.append(key)
+                t.close()
+        except Exception as e:  # reported below
+            errors.append(repr(e))
+
+    th = [threading.Thread(target=worker, args=(key,)) for key in cases]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not errors, errors
