@@ -413,7 +413,8 @@ def run_c5(args, rank, world, local_rank, dist, same_dev, barrier, allmax):
             "n_particles": int(sums[0]), "particles_per_rank": per_rank, "k": k, "r": r,
             "leafsize": args.leafsize,
             "parallelism": ("single" if world == 1 else
-                            f"count-quantile x-slab x{world} + RCCL halo"),
+                            f"count-quantile x-slab x{world} + halo over "
+                            f"{getattr(ds, 'transport', 'rccl')}"),
         },
         "radius_count": {"queries_per_s": q_total / t_r, "ms_per_step": t_r / args.steps * 1e3,
                          "mean_count": sums[1] / sums[0],
