@@ -544,8 +544,14 @@ def main():
             t.set_ids(dev_ptr=ds.ids.ptr, stream=stream.handle)
         return t
 
-    # build: one untimed (code-object load), then timed builds
+    # build: one untimed (code-object load; also the process's first build,
+    # which pays the shape enumeration and the allocations the later builds
+    # reuse), then timed rebuilds of the same size
+    hip.synchronize()
+    t0 = time.perf_counter()
     build_tree().close()
+    hip.synchronize()
+    build_ms_first = allmax((time.perf_counter() - t0) * 1e3)
     build_ms = []
     for _ in range(2):
         hip.synchronize()
@@ -555,7 +561,7 @@ def main():
         build_ms.append((time.perf_counter() - t0) * 1e3)
         if _ == 0:
             tree.close()
-    build_ms = min(build_ms)
+    build_ms = allmax(min(build_ms))
 
     od = hip.DeviceArray((own, k), np.float32)
     oi = hip.DeviceArray((own, k), np.uint32)
@@ -694,6 +700,7 @@ def main():
         },
         "halo": halo,
         "build_ms": build_ms,
+        "build_ms_first": build_ms_first,
         "roofline": {
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
