@@ -434,16 +434,20 @@ def init_comm(dist, rank, world, device, log=None):
     import torch
 
     buf = torch.zeros(capi.COMM_ID_BYTES, dtype=torch.uint8)
+    # every rank loads RCCL (a unique id is the cheapest call that does) before
+    # any rank enters ncclCommInitRank, which blocks until all ranks join: a
+    # rank that cannot load it would leave the others waiting there for ever
     ok = torch.zeros(1, dtype=torch.int64)
-    if rank == 0:
-        try:
-            buf = torch.tensor(list(capi.comm_unique_id()), dtype=torch.uint8)
-            ok[0] = 1
-        except Exception as e:
-            log(f"RCCL unavailable: {e}")
-    dist.broadcast(ok, 0)
+    try:
+        uid = capi.comm_unique_id()
+        ok[0] = 1
+    except Exception as e:
+        log(f"rank {rank}: RCCL unavailable: {e}")
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN)
     if not int(ok[0]):
         return None
+    if rank == 0:
+        buf = torch.tensor(list(uid), dtype=torch.uint8)
     dist.broadcast(buf, 0)
     try:
         c = capi.Comm(bytes(buf.numpy().tobytes()), rank, world, device)

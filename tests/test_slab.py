@@ -347,3 +347,44 @@ def test_deposit_slabs_tile_the_single_deposit(world, tmp_path, oracle):
     ref = oracle.deposit(xyz, w, r, grid, float(grid[0]), (1.0, 1.0, 1.0), 4)
     np.testing.assert_allclose(got, ref, rtol=1e-9, atol=1e-12)
     assert abs(got.sum() - w.sum()) < 0.01 * w.sum()
+
+
+def _comm_worker(rank, world, port, fail_rank, outdir):
+    import torch.distributed as dist
+
+    from nbodyhpc_amd import capi
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    calls = []
+    try:
+        def uid():
+            if rank == fail_rank:
+                raise RuntimeError("cannot load librccl.so.1 (test)")
+            return bytes(capi.COMM_ID_BYTES)
+
+        class NoInit:  # must never be reached when some rank lacks RCCL
+            def __init__(self, *a):
+                calls.append(a)
+                raise AssertionError("ncclCommInitRank entered")
+
+        capi.comm_unique_id, capi.Comm = uid, NoInit
+        c = slab.init_comm(dist, rank, world, 0)
+        np.savez(os.path.join(outdir, f"c{rank}.npz"), none=c is None, init_calls=len(calls))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,fail_rank", [(2, 1), (3, 0)])
+def test_init_comm_agrees_before_rccl_init(world, fail_rank, tmp_path):
+    """slab.init_comm: ncclCommInitRank blocks until every rank joins, so a rank
+    that cannot load RCCL must stop all ranks before any enters it (gloo, CPU)."""
+    import torch.multiprocessing as mp
+
+    port = _free_port()
+    mp.start_processes(_comm_worker, args=(world, port, fail_rank, str(tmp_path)), nprocs=world,
+                       join=True, start_method="spawn")
+    for r in range(world):
+        res = np.load(os.path.join(tmp_path, f"c{r}.npz"))
+        assert bool(res["none"]) and int(res["init_calls"]) == 0, r
