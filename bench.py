@@ -247,7 +247,6 @@ def suite(args, capi, hip, tree, dev_pts, n, k, L, stream, od, oi):
     lp = synth.lognormal(n, box=L, grid=args.lognormal_grid)
     gen_s = time.perf_counter() - t0
     dl = hip.DeviceArray.from_numpy(lp)
-    del lp
     bt = []
     for _ in range(2):
         hip.synchronize()
@@ -276,6 +275,14 @@ def suite(args, capi, hip, tree, dev_pts, n, k, L, stream, od, oi):
                             "fallback_queries": st["fallback_queries"],
                             "grid": args.lognormal_grid, "generate_s": gen_s,
                             "seed": synth.SEED_LOGNORMAL}
+    if not args.no_parity:
+        # the first 1e6 rows (retried queries included) against the compiled
+        # reference over the same log-normal points (the checker, not timed)
+        rows = min(1_000_000, n)
+        _, parity = cpu_baseline(lp, k, args.leafsize, L, rows, od.numpy_head(rows),
+                                 oi.numpy_head(rows))
+        out["knn_lognormal"]["parity_vs_cpu"] = parity
+    del lp
     log(f"suite: log-normal kNN {n / sec:.3e} q/s, build {min(bt):.1f} ms")
     lt.close()
     dl.free()
