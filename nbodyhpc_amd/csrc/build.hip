@@ -863,8 +863,8 @@ group_kernel(const nbkd_node *__restrict__ nodes, uint64_t nn, float *__restrict
              float *__restrict__ ginfo, float *__restrict__ hinfo, uint32_t *__restrict__ info,
              uint32_t *__restrict__ bbox) {
     constexpr int WPB = TB / 64;
-    __shared__ float sp[WPB][3][NBKD_GBLOCK];
-    __shared__ uint32_t sr[WPB][NBKD_GBLOCK];
+    __shared__ __attribute__((aligned(16))) float sp[WPB][3][NBKD_GBLOCK];
+    __shared__ __attribute__((aligned(16))) uint32_t sr[WPB][NBKD_GBLOCK];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     float (*const P)[NBKD_GBLOCK] = sp[wave];
     uint32_t *const R = sr[wave];
@@ -957,15 +957,18 @@ group_kernel(const nbkd_node *__restrict__ nodes, uint64_t nn, float *__restrict
                             hi[a] = -FLT_MAX;
                         }
                         for (uint32_t j0 = s[h]; j0 < s[h] + l[h]; j0 += 8) {
+                            const uint4 r0 = *reinterpret_cast<const uint4 *>(&R[j0]);
+                            const uint4 r1 = *reinterpret_cast<const uint4 *>(&R[j0 + 4]);
+                            const uint32_t rv[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
 #pragma unroll
-                            for (uint32_t u = 0; u < 8; ++u) {
-                                const uint32_t j = j0 + u;
-                                const bool rj = R[j] != 0u;
+                            for (int a = 0; a < 3; ++a) {
+                                const float4 v0 = *reinterpret_cast<const float4 *>(&P[a][j0]);
+                                const float4 v1 = *reinterpret_cast<const float4 *>(&P[a][j0 + 4]);
+                                const float vv[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
 #pragma unroll
-                                for (int a = 0; a < 3; ++a) {
-                                    const float v = P[a][j];
-                                    lo[a] = rj ? fminf(lo[a], v) : lo[a];
-                                    hi[a] = rj ? fmaxf(hi[a], v) : hi[a];
+                                for (uint32_t u = 0; u < 8; ++u) {
+                                    lo[a] = rv[u] ? fminf(lo[a], vv[u]) : lo[a];
+                                    hi[a] = rv[u] ? fmaxf(hi[a], vv[u]) : hi[a];
                                 }
                             }
                         }
@@ -974,12 +977,15 @@ group_kernel(const nbkd_node *__restrict__ nodes, uint64_t nn, float *__restrict
                     const int ax = (ey > ex && ey >= ez) ? 1 : (ez > ex && ez > ey ? 2 : 0);
                     const float key = p[h][ax];
                     uint32_t rank = 0;
+                    // pieces start at multiples of 8: two 16-B LDS reads per 8 keys
                     for (uint32_t j0 = s[h]; j0 < s[h] + l[h]; j0 += 8) {
+                        const float4 k0 = *reinterpret_cast<const float4 *>(&P[ax][j0]);
+                        const float4 k1 = *reinterpret_cast<const float4 *>(&P[ax][j0 + 4]);
+                        const float kv[8] = {k0.x, k0.y, k0.z, k0.w, k1.x, k1.y, k1.z, k1.w};
 #pragma unroll
                         for (uint32_t u = 0; u < 8; ++u) {
                             const uint32_t j = j0 + u;
-                            const float kj = P[ax][j];
-                            rank += (kj < key || (kj == key && j < pos[h])) ? 1u : 0u;
+                            rank += (kv[u] < key || (kv[u] == key && j < pos[h])) ? 1u : 0u;
                         }
                     }
                     const uint32_t m = (l[h] / 2) / 8 * 8;
