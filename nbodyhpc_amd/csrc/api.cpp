@@ -81,6 +81,31 @@ BlockCache &block_cache() {
 }
 } // namespace
 
+void release_idle_blocks(int dev) {
+    BlockCache &c = block_cache();
+    std::lock_guard<std::mutex> g(c.mu);
+    for (auto it = c.idle.begin(); it != c.idle.end();) {
+        if (it->first.first == dev) {
+            (void)hipFree(it->second);
+            c.idle_bytes -= it->first.second;
+            it = c.idle.erase(it);
+        } else {
+            ++it;
+        }
+    }
+}
+
+hipError_t malloc_or_release(void **p, size_t bytes) {
+    hipError_t e = hipMalloc(p, bytes);
+    if (e != hipErrorOutOfMemory) return e;
+    // the device's idle cached blocks go back to the driver, then one retry
+    (void)hipGetLastError();
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return e;
+    release_idle_blocks(dev);
+    return hipMalloc(p, bytes);
+}
+
 hipError_t tree_malloc(void **p, size_t bytes) {
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
@@ -98,21 +123,7 @@ hipError_t tree_malloc(void **p, size_t bytes) {
             return hipSuccess;
         }
     }
-    e = hipMalloc(p, bytes);
-    if (e == hipErrorOutOfMemory) { // return this device's idle blocks and retry once
-        (void)hipGetLastError();
-        std::lock_guard<std::mutex> g(c.mu);
-        for (auto it = c.idle.begin(); it != c.idle.end();) {
-            if (it->first.first == dev) {
-                (void)hipFree(it->second);
-                c.idle_bytes -= it->first.second;
-                it = c.idle.erase(it);
-            } else {
-                ++it;
-            }
-        }
-        e = hipMalloc(p, bytes);
-    }
+    e = malloc_or_release(p, bytes);
     if (e != hipSuccess) return e;
     std::lock_guard<std::mutex> g(c.mu);
     c.live[*p] = {dev, bytes};
@@ -471,7 +482,7 @@ void *Workspace::get(int slot, size_t bytes, hipStream_t s) {
         cap[slot] = 0;
     }
     size_t want = bytes + bytes / 8; // some headroom for the next, slightly larger call
-    hipError_t e = hipMalloc(&p[slot], want);
+    hipError_t e = malloc_or_release(&p[slot], want);
     if (e != hipSuccess) {
         (void)hip_fail(e, "hipMalloc(workspace)");
         p[slot] = nullptr;

@@ -1367,7 +1367,7 @@ nbkd_status build_tree(Tree &t, const float *xyz, uint64_t n, int32_t leaf_size,
         if (scr.p) NBKD_HIP(hipFree(scr.p));
         scr.p = nullptr;
         scr.bytes = 0;
-        NBKD_HIP(hipMalloc(&scr.p, cv.off));
+        NBKD_HIP(malloc_or_release(&scr.p, cv.off));
         scr.bytes = cv.off;
     }
     char *const base = static_cast<char *>(scr.p);

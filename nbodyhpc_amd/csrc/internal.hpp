@@ -114,6 +114,11 @@ bool stats_enabled();
 constexpr int NBKD_NSTATS = 17; // see capi.STATS_NAMES (collect kernel) + exact-kernel and retried queries
 void stats_store(const uint64_t *v);
 
+// hipMalloc that, when the device is out of memory, first returns the
+// device's idle cached tree blocks (api.cpp, tree_malloc) and retries once; the
+// query workspace, the build scratch and DevBuf allocate through it
+hipError_t malloc_or_release(void **p, size_t bytes);
+
 // RAII device allocation (plain hipMalloc; freed after the stream drained).
 // The stream-ordered pool (hipMallocAsync) is deliberately not used: mixing it
 // with hipMalloc'd tree storage and pageable copies produced corrupted inputs.
@@ -131,7 +136,7 @@ struct DevBuf {
     }
     hipError_t alloc(size_t bytes, hipStream_t stream) {
         s = stream;
-        return hipMalloc(&p, bytes ? bytes : 16);
+        return malloc_or_release(&p, bytes ? bytes : 16);
     }
     template <typename T> T *as() const { return static_cast<T *>(p); }
 };
@@ -143,6 +148,7 @@ struct DevBuf {
 // synchronisation in free_tree (hipFree's own semantics).
 hipError_t tree_malloc(void **p, size_t bytes);
 void tree_free(void *p);
+
 
 // build.hip
 nbkd_status build_tree(Tree &t, const float *xyz, uint64_t n, int32_t leaf_size, bool input_dev,
