@@ -5,11 +5,15 @@
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
-One step = one pass of the hot path over one batch: every local particle
-queried for its k=32 nearest neighbours (query bucketing + radix sort + packet
-collect / select kernels), inputs and outputs resident in HBM.  N > 1: the particles are
-sharded by x-slab, each rank holds its slab plus a periodic halo exchanged
-over RCCL at setup, and queries its own particles (weak scaling: 1e8 per GPU).
+One step = one pass of the hot path over one batch: every particle queried
+for its k=32 nearest neighbours (query bucketing + radix sort + packet collect /
+select kernels), inputs and outputs resident in HBM.  N > 1 (strong scaling by
+default: --particles is the total, the same 1e8 points at every N): the
+particles are sharded by x-slab, each rank holds its slab plus a periodic halo
+exchanged over RCCL at setup, queries its own particles, and the rows whose
+k-th neighbour lies past the halo go through the second-round exchange
+(slab.second_round) inside the step, so every row is
+exact.  --scaling weak: --particles per GPU.
 
 Rank 0 prints ONE JSON line.  Device plumbing goes through the same HIP
 runtime as libnbkd (nbodyhpc_amd/hip.py); torch is used only for
@@ -46,6 +50,35 @@ def _phase_frac(st):
     return {kk[4:]: st[kk] / tot for kk in keys} if tot else None
 
 
+def lib_sha256():
+    import hashlib
+
+    from nbodyhpc_amd import capi
+    h = hashlib.sha256()
+    with open(capi.LIB_PATH, "rb") as f:
+        for blk in iter(lambda: f.read(1 << 20), b""):
+            h.update(blk)
+    return h.hexdigest()
+
+
+def pmc_traffic(n_particles, k, q_per_launch):
+    """(HBM bytes per collect launch, source file) from the PMC summary measured
+    with this very library build, or (None, None)."""
+    import glob
+    sha = lib_sha256()
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_knn.json"))):
+        try:
+            pm = json.load(open(path))
+        except Exception:
+            continue
+        if (pm.get("lib_sha256") == sha and pm.get("n_particles") == n_particles
+                and pm.get("k") == k and str(pm.get("kernel", "")).startswith("knn_collect")
+                and abs(float(pm.get("queries_per_launch") or 0) - q_per_launch)
+                <= 1e-9 * q_per_launch):
+            return pm.get("hbm_bytes_per_launch"), os.path.relpath(path, ROOT)
+    return None, None
+
+
 def bytes_per_query(k, nodes=REF_NODES_1E8, points=REF_POINTS_1E8):
     return 16.0 * nodes + 12.0 * points + 12.0 + 8.0 * k
 
@@ -55,7 +88,13 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--particles", dest="n", type=float, default=1e8, help="particles per GPU")
+    p.add_argument("--particles", dest="n", type=float, default=1e8,
+                   help="particles: the total over all GPUs (strong scaling, default) or per "
+                        "GPU (--scaling weak)")
+    p.add_argument("--scaling", choices=("strong", "weak"), default="strong",
+                   help="strong: the same --particles points at every N, split by x-slab (the "
+                        "metric's 1/2/4/8-GPU curve); weak: --particles per GPU (C4 = --scaling "
+                        "weak --particles 1.25e8 at 8 GPUs)")
     p.add_argument("--k", type=int, default=32)
     p.add_argument("--leafsize", type=int, default=64,
                    help="tree leaf size (default 64: the reference _impl.KDTree default, "
@@ -289,7 +328,7 @@ def suite(args, capi, hip, tree, dev_pts, n, k, L, stream, od, oi):
     return out
 
 
-def run_c5(args, rank, world, local_rank, dist, same_dev, barrier, allmax):
+def run_c5(args, rank, world, local_rank, dist, same_dev, barrier, allmax, allsum):
     """Config C5: log-normal particles (synth.lognormal_slab,
     the C5 recipe) cut into x-slabs at particle-count quantiles, one halo of
     width max(r, kNN halo) over RCCL, then two timed passes over every own
@@ -299,7 +338,7 @@ def run_c5(args, rank, world, local_rank, dist, same_dev, barrier, allmax):
     construction (halo >= r).  Weak scaling: --particles per GPU on average."""
     from nbodyhpc_amd import capi, hip, slab, synth
 
-    n_total = int(args.n) * world
+    n_total = int(args.n) * (world if args.scaling == "weak" else 1)
     k, L = args.k, args.box
     r = args.radius * L
     h_r = slab.ball_halo(r, L)
@@ -345,25 +384,25 @@ def run_c5(args, rank, world, local_rank, dist, same_dev, barrier, allmax):
     def kth_step():
         tree.query_kth_device(dev_pts.ptr, own, k, rk.ptr, stream.handle)
 
+    # the k-th distances reaching past the halo go through the second-round
+    # exchange inside the timed step: every one is exact
+    rows = None if ds is None else slab.DeviceRows(ds, tree, k, kth_ptr=rk.ptr,
+                                                   stream=stream.handle)
+    sr_acc = {"rows_forwarded": 0, "forwards": 0, "hops": 0, "calls": 0}
+
+    def kth_pass():
+        tree.query_kth_device(dev_pts.ptr, own, k, rk.ptr, stream.handle)
+        if rows is not None:
+            st = slab.second_round(rows, rank, world, bounds, L, ds.h, k, dist)
+            for kk in ("rows_forwarded", "forwards"):
+                sr_acc[kk] += st[kk]
+            sr_acc["hops"] = max(sr_acc["hops"], st["hops"])
+            sr_acc["calls"] += 1
+
+    kth_step = kth_pass
     kth_step()
     stream.synchronize()
-    violations = 0
-    if ds is not None:
-        for _ in range(6):
-            violations = int(allmax(float(ds.violations(rk.ptr, 1, stream.handle))))
-            if violations == 0:
-                break
-            try:
-                slab.check_halo(2.0 * ds.h, bounds)
-            except ValueError:
-                break  # reported below as rows that are not exact
-            log(f"{violations} k-th distances reach past the halo (h={ds.h:.3g}); widening")
-            tree.close()
-            ds.exchange(ds.h * 2.0, stream.handle)
-            dev_pts, n_local = ds.xyz, ds.n_local
-            tree = build_tree()
-            kth_step()
-            stream.synchronize()
+    violations = 0 if ds is None else int(allsum(float(sr_acc["rows_forwarded"])))
 
     def timed_max(fn):
         for _ in range(args.warmup):
@@ -409,7 +448,7 @@ def run_c5(args, rank, world, local_rank, dist, same_dev, barrier, allmax):
         "warmup": args.warmup,
         "ms_per_step": t_r / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": args.scaling,
         "vs_baseline": None,
         "dtype": "f32",
         "data": (f"synthetic: C5 log-normal recipe (GRF {args.lognormal_grid}^3, P(k)~k^-2, "
@@ -429,9 +468,15 @@ def run_c5(args, rank, world, local_rank, dist, same_dev, barrier, allmax):
         "kth_density": {"queries_per_s": q_total / t_k, "ms_per_step": t_k / args.steps * 1e3,
                         "mean_density_over_mean": sums[3] / sums[0],
                         "geomean_density_over_mean": math.exp(sums[4] / sums[0])},
-        "halo": None if ds is None else {"h": ds.h, "h_radius": h_r,
-                                         "transport": ds.transport,
-                                         "kth_rows_past_halo": violations},
+        "halo": None if ds is None else {
+            "h": ds.h, "h_radius": h_r, "transport": ds.transport,
+            # k-th distances of the first pass that reached past the halo: each
+            # was resolved by the second-round exchange (no rebuild, no widening)
+            "kth_rows_past_halo": violations,
+            "second_round": {"transport": rows.transport,
+                             "rows_forwarded_per_pass": allsum(float(sr_acc["rows_forwarded"]))
+                             / max(sr_acc["calls"], 1),
+                             "max_hops": int(allmax(float(sr_acc["hops"])))}},
         "bounds": bounds,
         "build_ms": build_ms,
         "generate_s": gen_s,
@@ -472,6 +517,14 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
         return float(t.item())
 
+    def allgather_int(v):
+        if dist is None:
+            return [int(v)]
+        import torch
+        out = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
+        dist.all_gather(out, torch.tensor([int(v)], dtype=torch.int64))
+        return [int(x.item()) for x in out]
+
     def allmax(v):
         if dist is None:
             return v
@@ -481,7 +534,7 @@ def main():
         return float(t.item())
 
     if args.workload == "c5":
-        return run_c5(args, rank, world, local_rank, dist, same_dev, barrier, allmax)
+        return run_c5(args, rank, world, local_rank, dist, same_dev, barrier, allmax, allsum)
 
     n = int(args.n)
     k, L = args.k, args.box
@@ -529,6 +582,8 @@ def main():
         elif args.input:
             from nbodyhpc_amd import io as nio
             own_xyz, own_ids = nio.read_slab(args.input, rank, world, L)
+        elif args.scaling == "strong":  # the one-GPU point set, cut into slabs
+            own_xyz, own_ids = slab.gen_uniform_slab(n, args.seed, L, rank, world)
         else:
             own_xyz, own_ids = slab.gen_slab_points(n, args.seed, L, rank, world)
         own = own_xyz.shape[0]
@@ -573,33 +628,36 @@ def main():
     od = hip.DeviceArray((own, k), np.float32)
     oi = hip.DeviceArray((own, k), np.uint32)
 
+    # N > 1: rows whose k-th neighbour lies past the halo are forwarded to the
+    # neighbours and merged (second-round exchange) inside
+    # every step, so every row of every step is exact; no rebuild, no widening
+    rows = None if ds is None else slab.DeviceRows(ds, tree, k, od.ptr, oi.ptr,
+                                                   stream=stream.handle)
+    sr_acc = {"rows_forwarded": 0, "forwards": 0, "hops": 0, "calls": 0}
+
     def step():
         tree.query_device(dev_pts.ptr, own, k, od.ptr, oi.ptr, stream.handle)
+        if rows is not None:
+            st = slab.second_round(rows, rank, world, ds.bounds, L, ds.h, k, dist)
+            for kk in ("rows_forwarded", "forwards"):
+                sr_acc[kk] += st[kk]
+            sr_acc["hops"] = max(sr_acc["hops"], st["hops"])
+            sr_acc["calls"] += 1
 
     for _ in range(args.warmup):
         step()
     stream.synchronize()
     if ds is not None:
-        # exactness of the slab-local result; widen the halo until every row is exact
-        # (checked after every rebuild, so the reported count is that of the timed tree)
-        for attempt in range(5):
-            step()
-            stream.synchronize()
-            v = int(allmax(float(ds.violations(od.ptr, k, stream.handle))))
-            halo["violations"] = v
-            if v == 0 or attempt == 4:
-                break
-            try:
-                slab.check_halo(2.0 * ds.h, ds.bounds)
-            except ValueError as e:
-                log(f"{v} rows reach past the halo and it cannot widen: {e}")
-                break  # reported as halo.violations: rows that are not exact
-            log(f"{v} rows reach past the halo (h={ds.h:.3g}); widening")
-            tree.close()
-            ds.exchange(ds.h * 2.0, stream.handle)
-            dev_pts, n_local = ds.xyz, ds.n_local
-            tree = build_tree()
+        # the slab-local rows before the second round: how many reach past the halo
+        tree.query_device(dev_pts.ptr, own, k, od.ptr, oi.ptr, stream.handle)
+        stream.synchronize()
+        halo["rows_past_halo_before_second_round"] = int(
+            allsum(float(ds.violations(od.ptr, k, stream.handle))))
+        step()  # and resolved again, so the checked rows below are the exact ones
+        stream.synchronize()
         halo.update({"h": ds.h, "local_points": n_local, "transport": ds.transport})
+        for kk in sr_acc:
+            sr_acc[kk] = 0
     capi.timing_enable(True)
     capi.timing_reset()
     barrier()
@@ -610,6 +668,7 @@ def main():
     hip.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
+    sr_timed = dict(sr_acc)
     knn_ms, knn_launches = capi.timing_read("knn")
     sort_ms, _ = capi.timing_read("sort")
     key_ms, _ = capi.timing_read("leaf_key")
@@ -637,6 +696,16 @@ def main():
         gpu_d = od.numpy_head(parity_rows)
         gpu_i = oi.numpy_head(parity_rows)
 
+    if ds is not None:
+        halo["second_round"] = {
+            "transport": rows.transport,
+            "rows_forwarded_per_step": allsum(float(sr_timed["rows_forwarded"])) / max(args.steps, 1),
+            "forwards_per_step": allsum(float(sr_timed["forwards"])) / max(args.steps, 1),
+            "max_hops": int(allmax(float(sr_timed["hops"]))),
+        }
+        counts = allgather_int(own)
+    else:
+        counts = [own]
     if rank != 0:
         return
     total_q = own_total * args.steps
@@ -651,27 +720,11 @@ def main():
     col_avg_ms = col_ms / col_launches
     q_per_launch = own * args.steps / col_launches
     achieved = bq * q_per_launch / (col_avg_ms * 1e-3) / 1e9
-    traffic = None
-    # HBM bytes per knn launch from the newest committed rocprofv3 PMC summary
-    # (profiles/rNN_pmc_knn.json: FETCH_SIZE x2 (gfx950) + WRITE_SIZE passes)
-    # (tags run r01, r01b, ..., r02z, r02aa, ...: newest = longest suffix, then last)
-    import glob
-
-    def tag_key(path):
-        tag = os.path.basename(path).split("_pmc")[0]
-        return tag[:3], len(tag) - 3, tag[3:]
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_knn.json")), key=tag_key,
-                       reverse=True):
-        try:
-            pm = json.load(open(path))
-        except Exception:
-            continue
-        if (pm.get("n_particles") == own and pm.get("k") == k
-                and str(pm.get("kernel", "")).startswith("knn_collect")
-                and abs(float(pm.get("queries_per_launch") or 0) - q_per_launch)
-                <= 1e-9 * q_per_launch):
-            traffic = pm.get("hbm_bytes_per_launch")
-            break
+    # HBM bytes per collect launch from rocprofv3 PMC passes of THIS build: a
+    # committed profiles/rNN_pmc_knn.json (scripts/summarize_prof.py: FETCH_SIZE
+    # x2 (gfx950) + WRITE_SIZE, separate runs) whose recorded libnbkd.so SHA-256
+    # equals the loaded library's, for the same workload; else null
+    traffic, traffic_source = pmc_traffic(own, k, q_per_launch)
     extra = None
     if world == 1 and args.suite:
         extra = suite(args, capi, hip, tree, dev_pts, n, k, L, stream, od, oi)
@@ -688,7 +741,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": ms_per_step,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": args.scaling,
         "vs_baseline": None,
         "dtype": "f32",
         "data": (f"file: {os.path.basename(args.input)} ({args.input_format}); self-queries"
@@ -698,9 +751,11 @@ def main():
             "workload": (f"kNN k={k} self-query of every particle of {os.path.basename(args.input)}"
                          f" ({own_total} particles, periodic L={L}), leafsize {args.leafsize}"
                          if args.input else
-                         f"kNN k={k} self-query of every particle, {n:.0e} uniform periodic "
-                         f"particles per GPU (L={L}), leafsize {args.leafsize}"),
-            "n_particles_per_gpu": own, "k": k, "leafsize": args.leafsize,
+                         f"kNN k={k} self-query of every particle, {own_total:.3g} uniform "
+                         f"periodic particles{' per GPU' if args.scaling == 'weak' else ''} "
+                         f"(L={L}), leafsize {args.leafsize}"),
+            "n_particles": own_total, "n_particles_per_gpu": own, "particles_per_rank": counts,
+            "k": k, "leafsize": args.leafsize,
             "queries_per_step": own_total,
             "parallelism": ("single" if world == 1 else
                             f"x-slab x{world} + halo over {(halo or {}).get('transport', 'rccl')}"),
@@ -711,6 +766,14 @@ def main():
         "roofline": {
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+            "traffic_source": traffic_source,
+            # counter bytes / kernel time / peak: the HBM fraction rocprof sees
+            # (achieved / frac are a work rate in the reference's bytes: the
+            # packet kernel reads a staged leaf once for 64 queries)
+            "hbm_frac": (None if traffic is None else
+                         traffic / (col_avg_ms * 1e-3) / (HBM_PEAK_GBS * 1e9)),
+            # whole-step rate in the reference's bytes over all GPUs' peak
+            "step_frac": value * bq / (HBM_PEAK_GBS * 1e9 * world),
             "kernel": "knn_collect_grp_kernel<periodic> (nbodyhpc_amd/csrc/knn_collect.hip)",
             "kernel_ms_per_launch": col_avg_ms,
             "launches_per_step": col_launches / args.steps,

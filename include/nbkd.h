@@ -11,8 +11,15 @@
  * the tree handle and everything on the device behind it.  Buffers are host
  * memory unless the matching NBKD_*_DEVICE flag is set, in which case they are
  * device pointers on the tree's device.  `stream` is a hipStream_t (NULL = the
- * null stream); with host outputs the call returns after the results are
- * copied back, with device outputs it returns once the work is enqueued.
+ * null stream).  With host outputs a call returns after the results are
+ * copied back.  With device outputs the results are complete when the work
+ * enqueued on `stream` so far has completed; the call itself may wait on
+ * `stream` once before it returns: nbkd_query_knn / nbkd_query_kth to size the
+ * re-walk of the queries whose seed ball held fewer than k points (on uniform
+ * inputs about 2e-4 of them), nbkd_query_ball_count on a periodic tree to
+ * count the queries outside [0, L]^3.  Calls on one tree are serialised, and a
+ * call on another stream first waits for the tree's previous call to finish
+ * on the device (the tree's scratch memory is reused).
  *
  * Every entry point returns an nbkd_status; on failure nbkd_last_error()
  * (thread-local) holds a message.  Statuses NBKD_EINVAL / NBKD_EBOX /
@@ -43,6 +50,8 @@ enum {
 #define NBKD_INPUT_DEVICE 0x1u  /* point / query arrays are device pointers */
 #define NBKD_OUTPUT_DEVICE 0x2u /* output arrays are device pointers        */
 #define NBKD_ACCUMULATE 0x4u    /* nbkd_deposit: add into `out` instead of overwriting it */
+#define NBKD_SQUARED 0x8u       /* nbkd_query_knn / _kth: output d2 (no sqrtf), the values
+                                   the reference sorts by (kdtree.cpp:149-151) */
 
 typedef struct nbkd_tree nbkd_tree;
 
@@ -121,6 +130,16 @@ nbkd_status nbkd_export(const nbkd_tree *tree, nbkd_node *nodes, float *x, float
 
 void nbkd_free(nbkd_tree *tree);
 
+/* Process-wide tuning knobs (the library reads no environment variable):
+ *   "knn_seed_margin"  a in the seed ball's expected count mu = k + a sqrt(k) + a
+ *                      (default 3.5; > 0).  Results never depend on it: a query
+ *                      whose seed ball holds fewer than k points is re-walked.
+ *   "candidate_bytes"  HBM budget of one collect / select batch's candidate
+ *                      columns (default 0 = min(24 GiB, free / 4)).
+ * NEW (no reference counterpart: kdtree/src/cpp/pybind.cpp:196-216 has no knobs). */
+nbkd_status nbkd_set_tuning(const char *name, double value);
+nbkd_status nbkd_get_tuning(const char *name, double *value);
+
 /* thread-local message of the last failure on this thread ("" if none) */
 const char *nbkd_last_error(void);
 
@@ -174,12 +193,34 @@ nbkd_status nbkd_slab_violations(const float *q, const float *dist, uint64_t m, 
                                  float lo, float hi, float h, uint64_t *count, int32_t device,
                                  void *stream);
 
+/* Second-round exchange of a slab-local kNN result: the
+ * own queries whose k-th distance (column k-1 of the (m, k) rows `dist`, or
+ * the m distances with k = 1) reaches past the left face cl or the right face
+ * ch of the covered x-range: bit 0 of out_sides = left, bit 1 = right (the
+ * same f32 test as nbkd_slab_violations, split by side).  Up to `capacity`
+ * query indices go to out_list (in no particular order); *count receives the
+ * total, which may exceed the capacity (call again with a larger buffer). */
+nbkd_status nbkd_slab_forward(const float *q, const float *dist, uint64_t m, int32_t k, float cl,
+                              float ch, uint32_t *out_list, uint8_t *out_sides, uint64_t capacity,
+                              uint64_t *count, int32_t device, void *stream);
+
+/* Row gather / scatter of device arrays: dst[i] = src[idx[i]] (gather) or
+ * dst[idx[i]] = src[i] (scatter) for n rows of row_bytes (a multiple of 4)
+ * bytes; idx is a device array of uint32 row numbers. */
+nbkd_status nbkd_rows_gather(const void *src, uint64_t row_bytes, const uint32_t *idx, uint64_t n,
+                             void *dst, int32_t device, void *stream);
+nbkd_status nbkd_rows_scatter(const void *src, uint64_t row_bytes, const uint32_t *idx, uint64_t n,
+                              void *dst, int32_t device, void *stream);
+
 /* RCCL communicator (librccl.so.1 loaded on first use).  Rank 0 calls
  * nbkd_comm_unique_id and distributes the NBKD_COMM_ID_BYTES bytes out of band
  * (e.g. torch.distributed over gloo); every rank then calls nbkd_comm_init. */
 #define NBKD_COMM_ID_BYTES 128
 typedef struct nbkd_comm nbkd_comm;
 nbkd_status nbkd_comm_unique_id(uint8_t *out);
+/* NBKD_OK iff librccl.so.1 loads with every symbol the exchange uses; unlike
+ * nbkd_comm_unique_id it starts no bootstrap listener (every rank may call it). */
+nbkd_status nbkd_comm_probe(void);
 nbkd_status nbkd_comm_init(const uint8_t *id, int32_t rank, int32_t world, int32_t device,
                            nbkd_comm **out);
 /* One grouped set of point-to-point byte transfers: for each i, send

@@ -2,9 +2,13 @@
 
   nbodyhpc_amd/lib/libnbkd.so              hipcc --offload-arch=gfx950: C ABI + HIP kernels
   nbodyhpc_amd/kdtree/_impl<ext-suffix>    g++: pybind11 module over the C ABI
+  nbodyhpc_amd/lib/exp/libnbkd.so          (--experiments only) the same sources with
+                                           -DNBKD_EXPERIMENTS: the A/B kernels and the
+                                           NBKD_* environment overrides; loaded only
+                                           through NBKD_LIB, never by default
 
 Both are built in-tree so they travel with the repo snapshot to the GPU box.
-`python -m nbodyhpc_amd.build [--force]`.
+`python -m nbodyhpc_amd.build [--force] [--experiments]`.
 """
 from __future__ import annotations
 
@@ -48,24 +52,31 @@ def _run(cmd, verbose):
     return subprocess.Popen(cmd)
 
 
-def build_lib(force=False, verbose=True):
-    os.makedirs(OBJ_DIR, exist_ok=True)
+EXP_DIR = os.path.join(LIB_DIR, "exp")
+EXP_LIB = os.path.join(EXP_DIR, "libnbkd.so")
+
+
+def build_lib(force=False, verbose=True, experiments=False):
+    obj_dir = os.path.join(EXP_DIR, "obj") if experiments else OBJ_DIR
+    lib = EXP_LIB if experiments else LIB
+    flags = HIP_FLAGS + (["-DNBKD_EXPERIMENTS"] if experiments else [])
+    os.makedirs(obj_dir, exist_ok=True)
     procs, objs = [], []
     for src in SOURCES:
         path = os.path.join(CSRC, src)
-        obj = os.path.join(OBJ_DIR, src + ".o")
+        obj = os.path.join(obj_dir, src + ".o")
         objs.append(obj)
         if force or _newer(obj, [path] + HEADERS):
             lang = [] if src.endswith(".hip") else ["-x", "hip"]
-            procs.append(_run([HIPCC] + HIP_FLAGS + lang + ["-c", path, "-o", obj], verbose))
+            procs.append(_run([HIPCC] + flags + lang + ["-c", path, "-o", obj], verbose))
     for p in procs:
         if p.wait() != 0:
             raise RuntimeError("hipcc failed")
-    if force or procs or _newer(LIB, objs):
-        cmd = [HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", LIB] + objs + ["-ldl"]
+    if force or procs or _newer(lib, objs):
+        cmd = [HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", lib] + objs + ["-ldl"]
         if _run(cmd, verbose).wait() != 0:
             raise RuntimeError("link of libnbkd.so failed")
-    return LIB
+    return lib
 
 
 def build_ext(force=False, verbose=True):
@@ -90,4 +101,7 @@ def build(force=False, verbose=True):
 
 
 if __name__ == "__main__":
-    build(force="--force" in sys.argv)
+    if "--experiments" in sys.argv:
+        build_lib(force="--force" in sys.argv, experiments=True)
+    else:
+        build(force="--force" in sys.argv)

@@ -19,6 +19,7 @@ NBKD_OK, NBKD_EINVAL, NBKD_EBOX, NBKD_ETOOMANY, NBKD_ENOMEM, NBKD_EDEVICE = rang
 NBKD_INPUT_DEVICE = 0x1
 NBKD_OUTPUT_DEVICE = 0x2
 NBKD_ACCUMULATE = 0x4
+NBKD_SQUARED = 0x8
 
 NODE_DTYPE = np.dtype([("dim", "<i4"), ("split", "<f4"), ("left", "<u4"), ("right", "<u4")])
 
@@ -61,6 +62,13 @@ _PROTOS = {
                                 _u64, ctypes.POINTER(_u64), _i32, _c_p]),
     "nbkd_slab_violations": (_i32, [_c_p, _c_p, _u64, _i32, ctypes.c_float, ctypes.c_float,
                                     ctypes.c_float, ctypes.POINTER(_u64), _i32, _c_p]),
+    "nbkd_slab_forward": (_i32, [_c_p, _c_p, _u64, _i32, ctypes.c_float, ctypes.c_float, _c_p,
+                                 _c_p, _u64, ctypes.POINTER(_u64), _i32, _c_p]),
+    "nbkd_rows_gather": (_i32, [_c_p, _u64, _c_p, _u64, _c_p, _i32, _c_p]),
+    "nbkd_rows_scatter": (_i32, [_c_p, _u64, _c_p, _u64, _c_p, _i32, _c_p]),
+    "nbkd_set_tuning": (_i32, [ctypes.c_char_p, ctypes.c_double]),
+    "nbkd_get_tuning": (_i32, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_double)]),
+    "nbkd_comm_probe": (_i32, []),
     "nbkd_comm_unique_id": (_i32, [_c_p]),
     "nbkd_comm_init": (_i32, [_c_p, _i32, _i32, _i32, ctypes.POINTER(_c_p)]),
     "nbkd_comm_exchange": (_i32, [_c_p, _i32, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p]),
@@ -155,17 +163,20 @@ class Tree:
                                  z.ctypes.data, idx.ctypes.data))
         return nodes, x, y, z, idx
 
-    def query(self, q, k):
-        q = _host_f32(q)
+    def query(self, q, k, squared=False):
+        """(m, k) distances and ids; squared=True: d2 instead of sqrtf(d2)."""
+        q = _host_f32(q).reshape(-1, 3)
         m = q.shape[0]
         d = np.empty((m, k), np.float32)
         i = np.empty((m, k), np.uint32)
         _check(lib().nbkd_query_knn(self.h, q.ctypes.data, m, int(k), d.ctypes.data,
-                                    i.ctypes.data, 0, None))
+                                    i.ctypes.data, NBKD_SQUARED if squared else 0, None))
         return d, i
 
-    def query_device(self, q_ptr, m, k, d_ptr, i_ptr, stream=None, input_device=True):
-        flags = NBKD_OUTPUT_DEVICE | (NBKD_INPUT_DEVICE if input_device else 0)
+    def query_device(self, q_ptr, m, k, d_ptr, i_ptr, stream=None, input_device=True,
+                     squared=False):
+        flags = (NBKD_OUTPUT_DEVICE | (NBKD_INPUT_DEVICE if input_device else 0)
+                 | (NBKD_SQUARED if squared else 0))
         _check(lib().nbkd_query_knn(self.h, q_ptr, int(m), int(k), d_ptr, i_ptr, flags, stream))
 
     def query_kth(self, q, k):
@@ -247,6 +258,17 @@ def deposit_device(xyz_ptr, weight_ptr, radius_ptr, n, grid, ppu, out_ptr,
                               int(device), flags, stream))
 
 
+def set_tuning(name, value):
+    """nbkd_set_tuning: "knn_seed_margin" (default 3.5), "candidate_bytes" (0 = auto)."""
+    _check(lib().nbkd_set_tuning(name.encode(), float(value)))
+
+
+def get_tuning(name):
+    v = ctypes.c_double()
+    _check(lib().nbkd_get_tuning(name.encode(), ctypes.byref(v)))
+    return v.value
+
+
 def timing_enable(on=True):
     _check(lib().nbkd_timing_enable(1 if on else 0))
 
@@ -306,6 +328,31 @@ def slab_violations(q_ptr, dist_ptr, m, k, lo, hi, h, device=0, stream=None):
     _check(lib().nbkd_slab_violations(q_ptr, dist_ptr, int(m), int(k), float(lo), float(hi),
                                       float(h), ctypes.byref(c), int(device), stream))
     return c.value
+
+
+def slab_forward(q_ptr, dist_ptr, m, k, cl, ch, list_ptr=None, sides_ptr=None, capacity=0,
+                 device=0, stream=None):
+    """nbkd_slab_forward: total count of own queries whose k-th distance reaches
+    past cl (left) or ch (right); up to `capacity` (index, side bits) entries."""
+    c = _u64()
+    _check(lib().nbkd_slab_forward(q_ptr, dist_ptr, int(m), int(k), float(cl), float(ch), list_ptr,
+                                   sides_ptr, int(capacity), ctypes.byref(c), int(device), stream))
+    return c.value
+
+
+def rows_gather(src_ptr, row_bytes, idx_ptr, n, dst_ptr, device=0, stream=None):
+    _check(lib().nbkd_rows_gather(src_ptr, int(row_bytes), idx_ptr, int(n), dst_ptr, int(device),
+                                  stream))
+
+
+def rows_scatter(src_ptr, row_bytes, idx_ptr, n, dst_ptr, device=0, stream=None):
+    _check(lib().nbkd_rows_scatter(src_ptr, int(row_bytes), idx_ptr, int(n), dst_ptr, int(device),
+                                   stream))
+
+
+def comm_probe() -> None:
+    """Raises unless RCCL loads (no bootstrap listener is started)."""
+    _check(lib().nbkd_comm_probe())
 
 
 def comm_unique_id() -> bytes:

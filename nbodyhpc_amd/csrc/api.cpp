@@ -2,6 +2,7 @@
 // build.hip / query.hip.  No exception crosses the boundary.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cmath>
 #include <cstring>
 #include <map>
@@ -149,6 +150,14 @@ void tree_free(void *p) {
     }
 }
 
+
+namespace {
+// nbkd_set_tuning knobs (process-wide); defaults are the measured optima
+std::atomic<double> g_tune[TUNE_N] = {{3.5}, {0.0}};
+const char *const g_tune_names[TUNE_N] = {"knn_seed_margin", "candidate_bytes"};
+} // namespace
+
+double tuning(int id) { return g_tune[id].load(std::memory_order_relaxed); }
 
 void set_error(const std::string &msg) { g_err = msg; }
 
@@ -414,6 +423,40 @@ void nbkd_free(nbkd_tree *tree) {
     delete tree;
 }
 
+nbkd_status nbkd_set_tuning(const char *name, double value) {
+    if (!name) {
+        set_error("nbkd_set_tuning: NULL name");
+        return NBKD_EINVAL;
+    }
+    for (int i = 0; i < TUNE_N; ++i) {
+        if (std::strcmp(name, g_tune_names[i]) != 0) continue;
+        const bool ok = i == TUNE_KNN_SEED ? (value > 0.0 && value <= 1e3)
+                                           : (value >= 0.0 && value < 1e15);
+        if (!ok || !std::isfinite(value)) {
+            set_error(std::string("nbkd_set_tuning: value out of range for ") + name);
+            return NBKD_EINVAL;
+        }
+        g_tune[i].store(value, std::memory_order_relaxed);
+        return NBKD_OK;
+    }
+    set_error(std::string("nbkd_set_tuning: unknown knob ") + name);
+    return NBKD_EINVAL;
+}
+
+nbkd_status nbkd_get_tuning(const char *name, double *value) {
+    if (!name || !value) {
+        set_error("nbkd_get_tuning: NULL argument");
+        return NBKD_EINVAL;
+    }
+    for (int i = 0; i < TUNE_N; ++i)
+        if (std::strcmp(name, g_tune_names[i]) == 0) {
+            *value = tuning(i);
+            return NBKD_OK;
+        }
+    set_error(std::string("nbkd_get_tuning: unknown knob ") + name);
+    return NBKD_EINVAL;
+}
+
 nbkd_status nbkd_timing_enable(int32_t enable) {
     g_timing = enable != 0;
     return NBKD_OK;
@@ -498,6 +541,32 @@ void Workspace::release() {
         p[i] = nullptr;
         cap[i] = 0;
     }
+    if (done) (void)hipEventDestroy(done);
+    done = nullptr;
+    used = false;
+}
+
+hipError_t Workspace::enter(hipStream_t s) {
+    if (used && s != last && done) return hipStreamWaitEvent(s, done, 0);
+    return hipSuccess;
+}
+
+void Workspace::leave(hipStream_t s) {
+    if (!done && hipEventCreateWithFlags(&done, hipEventDisableTiming) != hipSuccess) {
+        (void)hipGetLastError();
+        done = nullptr;
+        (void)hipStreamSynchronize(s); // no event: drain instead
+        used = false;
+        return;
+    }
+    if (hipEventRecord(done, s) != hipSuccess) {
+        (void)hipGetLastError();
+        (void)hipStreamSynchronize(s);
+        used = false;
+        return;
+    }
+    last = s;
+    used = true;
 }
 
 } // namespace nbkd

@@ -245,7 +245,7 @@ void launch_ball_packet(const Tree &t, const float *q, const uint32_t *order, ui
     const unsigned blocks = (unsigned)((m + TB - 1) / TB);
     // transposed count threshold (x/8 partial lanes per staged point); 0 = off
     static const uint32_t tnum = [] {
-        const char *e = getenv("NBKD_BALL_T");
+        const char *e = knob("NBKD_BALL_T");
         return e ? (uint32_t)atoi(e) : 8u;
     }();
     PadLeaves pad;

@@ -1424,7 +1424,7 @@ nbkd_status build_tree(Tree &t, const float *xyz, uint64_t n, int32_t leaf_size,
                 hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
                 run_blocks = 8u * (uint32_t)std::max(cus, 1);
             (void)hipGetLastError();
-            const char *e = getenv("NBKD_RUN_BLOCKS"); // A/B only
+            const char *e = knob("NBKD_RUN_BLOCKS"); // A/B only
             if (e) run_blocks = (uint32_t)std::max(1, atoi(e));
         }
         for (size_t d = 0; d < info.size(); ++d) {
@@ -1462,7 +1462,7 @@ nbkd_status build_tree(Tree &t, const float *xyz, uint64_t n, int32_t leaf_size,
     {
         TimedScope ts("build_small", s);
         static const int small_team = [] { // NBKD_SMALL_TEAM=0: one wave per sub-segment (A/B)
-            const char *e = getenv("NBKD_SMALL_TEAM");
+            const char *e = knob("NBKD_SMALL_TEAM");
             return (e && atoi(e) == 0) ? 0 : 1;
         }();
         if (!small.empty()) {
@@ -1510,7 +1510,7 @@ nbkd_status build_tree(Tree &t, const float *xyz, uint64_t n, int32_t leaf_size,
             int dev = 0, cus = 256;
             NBKD_HIP(hipGetDevice(&dev));
             (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-            const char *eg = getenv("NBKD_GROUP_BLOCKS_PER_CU"); // A/B only
+            const char *eg = knob("NBKD_GROUP_BLOCKS_PER_CU"); // A/B only
             const uint64_t per_cu = eg ? (uint64_t)std::max(1, atoi(eg)) : 128u;
             const uint64_t blocks = std::min<uint64_t>((t.nnodes + 3) / 4, (uint64_t)cus * per_cu);
             // leaves hold <= max(leaf, 16) points

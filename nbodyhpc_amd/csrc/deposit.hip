@@ -355,7 +355,11 @@ template <bool FILL> __global__ void __launch_bounds__(DB) deposit_pairs_kernel(
         y = a.xyz[3 * i + 1];
         z = a.xyz[3 * i + 2];
     }
-    const bool ball = valid && !(r * a.ppu < 0.5f); // sub-voxel balls: deposit_tiny_kernel
+    // sub-voxel balls: deposit_tiny_kernel.  A non-finite radius or centre
+    // contributes nothing: the shader's w / (4/3 pi R^3) is 0 for R = inf (the
+    // kth_distance padding when k > n), and NaN vertices are not rasterised
+    const bool finite = isfinite(r) && isfinite(x) && isfinite(y) && isfinite(z);
+    const bool ball = valid && finite && !(r * a.ppu < 0.5f);
     float sx[3], sy[3], sz[3];
     int nx = 0, ny = 0, nzi = 0;
     if (ball) {
@@ -487,6 +491,7 @@ __global__ void __launch_bounds__(DB) deposit_tiny_kernel(DepositArgs a) {
     const float r = a.r[p], ppu = a.ppu;
     if (!(r * ppu < 0.5f)) return;
     const float x = a.xyz[3 * p], y = a.xyz[3 * p + 1], z = a.xyz[3 * p + 2], w = a.w[p];
+    if (!isfinite(x) || !isfinite(y) || !isfinite(z)) return; // as deposit_pairs_kernel
     float sx[3], sy[3], sz[3];
     const int nx = images(x, r, a.period[0], sx), ny = images(y, r, a.period[1], sy),
               nzi = images(z, r, a.period[2], sz);
@@ -576,11 +581,13 @@ __global__ void __launch_bounds__(SB) scan_add_kernel(uint64_t *out, uint64_t n,
     if (i <= n) out[i] += bsum[blockIdx.x];
 }
 
-// one workspace per device for the deposit's scratch (held for the whole call)
-Workspace &deposit_ws(int dev, std::unique_lock<std::mutex> &lk) {
+// one workspace per device for the deposit's scratch, locked for the whole
+// call (WsCall: a call on another stream first waits for the previous call's
+// kernels, which may still use the scratch after a device-output call returned)
+Workspace &deposit_ws(int dev) {
     static std::mutex mu;
     static std::map<int, Workspace *> ws;
-    lk = std::unique_lock<std::mutex>(mu);
+    std::lock_guard<std::mutex> lk(mu);
     Workspace *&w = ws[dev];
     if (!w) w = new Workspace();
     return *w;
@@ -611,8 +618,9 @@ nbkd_status deposit(const float *xyz, const float *weight, const float *radius, 
     int dev = 0, cus = 256;
     NBKD_HIP(hipGetDevice(&dev));
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    std::unique_lock<std::mutex> lk;
-    Workspace &ws = deposit_ws(dev, lk);
+    Workspace &ws = deposit_ws(dev);
+    WsCall call(ws, s);
+    NBKD_HIP(call.err);
     const float *dx = xyz, *dw = weight, *dr = radius;
     if (!in_dev && n) {
         float *b = (float *)ws.get(WS_Q, n * 20, s);

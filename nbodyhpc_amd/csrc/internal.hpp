@@ -5,6 +5,7 @@
 
 #include <cfloat>
 #include <cstdint>
+#include <cstdlib>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -24,9 +25,27 @@ struct Workspace {
     std::mutex mu;
     void *p[WS_NSLOTS] = {};
     size_t cap[WS_NSLOTS] = {};
+    // the last call's stream and an event recorded at its end: a call on
+    // another stream first waits for it on the device (enter), since its
+    // kernels may still read or write the slots when the host call returned
+    hipStream_t last = nullptr;
+    hipEvent_t done = nullptr;
+    bool used = false;
     // returns nullptr on failure (hip error recorded via set_error)
     void *get(int slot, size_t bytes, hipStream_t s);
     void release();
+    hipError_t enter(hipStream_t s); // with mu held, before the first enqueue
+    void leave(hipStream_t s);       // with mu held, after the last enqueue
+};
+
+// one call's use of a workspace: lock, order after the previous call, record the end
+struct WsCall {
+    std::unique_lock<std::mutex> lk;
+    Workspace &w;
+    hipStream_t s;
+    hipError_t err;
+    WsCall(Workspace &w_, hipStream_t s_) : lk(w_.mu), w(w_), s(s_) { err = w.enter(s); }
+    ~WsCall() { w.leave(s); }
 };
 
 constexpr int NBKD_PAD_LEAVES = 8;
@@ -90,6 +109,20 @@ struct DevTree {
 inline DevTree view(const Tree &t) {
     return DevTree{t.x, t.y, t.z, t.idx, t.nodes, (uint32_t)t.n8, (uint32_t)t.nnodes, t.box};
 }
+
+// Tuning.  The production library reads no environment variable: every
+// algorithm choice is its measured default, and the caller can change the
+// few exposed knobs only through nbkd_set_tuning.  A build with
+// -DNBKD_EXPERIMENTS (`python -m nbodyhpc_amd.build --experiments`, a separate
+// library under lib/exp/) compiles in the A/B variants and lets the NBKD_*
+// environment variables override the knobs.
+#ifdef NBKD_EXPERIMENTS
+inline const char *knob(const char *env) { return getenv(env); }
+#else
+inline const char *knob(const char *) { return nullptr; }
+#endif
+enum TuneId { TUNE_KNN_SEED = 0, TUNE_CAND_BYTES, TUNE_N };
+double tuning(int id); // api.cpp (nbkd_set_tuning)
 
 // error plumbing (api.cpp)
 void set_error(const std::string &msg);
@@ -175,7 +208,7 @@ nbkd_status launch_knn_collect(const Tree &t, const float *q, const uint32_t *or
                                int k, const float *tg, float seed_mul, uint32_t qpp, uint2 *cand,
                                uint32_t capg, uint32_t *ccount, float *od, uint32_t *oi,
                                uint32_t *fail_list, uint32_t *fail_count, uint32_t pos_base,
-                               bool retry, bool fix_seed, unsigned long long *stats,
+                               bool retry, bool fix_seed, bool sq, unsigned long long *stats,
                                hipStream_t s);
 
 // ball.hip: radius count (out_idx == nullptr) or CSR fill over m kd-ordered

@@ -40,18 +40,6 @@ constexpr int CHUNK = 32; // leaf points staged per step (leaves hold <= 32 at l
 
 constexpr int NB = 16; // distance buckets of the bound histogram
 
-struct CollectLds {
-    // sparse mode, indexed by slot (the rank of a needing lane): its query xyz +
-    // bound, its bucket factor (d2_bucket) and its lane
-    float4 sq[64];
-    float scl[64];
-    uint8_t owners[64];
-    uint32_t cnt[64];          // per lane: candidates appended
-    uint32_t hist[NB / 4][64]; // per lane: NB 8-bit counts of candidates by d2 bucket
-    float pb[2][3][CHUNK]; // leaf points, double-buffered (PIPE)
-    float tb[2][8];        // the leaf's tight box (leafinfo words)
-};
-
 // Bound tightening without a top-k: the seed ball [0, S) is cut into NB
 // buckets of width S/NB in d2; a candidate is counted in bucket j only if
 // d2 < fl((j+1) * fl(S/NB)).  Once the buckets 0..j hold >= k candidates, k
@@ -65,6 +53,19 @@ struct CollectLds {
 __device__ __forceinline__ uint32_t d2_bucket(float d, float c) {
     return min((uint32_t)(d * c), (uint32_t)(NB - 1));
 }
+
+#ifdef NBKD_EXPERIMENTS // the round-1 leaf-level scan, A/B only (NBKD_GROUPS=0)
+struct CollectLds {
+    // sparse mode, indexed by slot (the rank of a needing lane): its query xyz +
+    // bound, its bucket factor (d2_bucket) and its lane
+    float4 sq[64];
+    float scl[64];
+    uint8_t owners[64];
+    uint32_t cnt[64];          // per lane: candidates appended
+    uint32_t hist[NB / 4][64]; // per lane: NB 8-bit counts of candidates by d2 bucket
+    float pb[2][3][CHUNK]; // leaf points, double-buffered (PIPE)
+    float tb[2][8];        // the leaf's tight box (leafinfo words)
+};
 
 // Candidate columns, entries {d2 bits, tree position}: packet pk owns
 // cand[pk * 64 * capg ...) as capg/16 blocks of 64 lanes x 16 slots; slot s of
@@ -412,6 +413,8 @@ knn_collect_kernel(DevTree t, const uint32_t *__restrict__ linfo, const float *_
     }
 }
 
+#endif // NBKD_EXPERIMENTS
+
 // ---------------------------------------------------------------- group variant
 // The same packet walk over a tree whose leaves are cut into 8-point groups
 // with their own tight boxes (build.hip group_kernel).  At a leaf the lanes
@@ -726,7 +729,7 @@ knn_select_kernel(DevTree t, const float *__restrict__ q, const uint32_t *__rest
                   const uint32_t *__restrict__ ccount, float *__restrict__ out_d,
                   uint32_t *__restrict__ out_i, uint32_t *__restrict__ fail_list,
                   uint32_t *__restrict__ fail_count, uint32_t pos_base, uint64_t all_rows,
-                  float *__restrict__ tg_fix, float mu) {
+                  float *__restrict__ tg_fix, float mu, bool sq) {
     constexpr int NS = 16;                  // candidates merged per pass
     constexpr int CC = KC < 32 ? KC : 32;   // top-k registers staged per output pass
     constexpr int SW = CC < 32 ? 32 * 64 : CC * 64; // >= 8 KB: one candidate block
@@ -833,7 +836,7 @@ knn_select_kernel(DevTree t, const float *__restrict__ q, const uint32_t *__rest
     }
 
     if (out_i == nullptr) { // k-th distance only (nbkd_query_kth): column k-1
-        if (valid) out_d[qo] = sqrtf(td[KC - 1]);
+        if (valid) out_d[qo] = sq ? td[KC - 1] : sqrtf(td[KC - 1]);
         return;
     }
     rowq[lane] = valid ? qo : 0xFFFFFFFFu;
@@ -841,7 +844,8 @@ knn_select_kernel(DevTree t, const float *__restrict__ q, const uint32_t *__rest
     for (int j0 = 0; j0 < KC; j0 += CC) {
         wave_sync();
 #pragma unroll
-        for (int j = 0; j < CC; ++j) stage[j * 64 + (lane ^ j)] = __float_as_uint(sqrtf(td[j0 + j]));
+        for (int j = 0; j < CC; ++j)
+            stage[j * 64 + (lane ^ j)] = __float_as_uint(sq ? td[j0 + j] : sqrtf(td[j0 + j]));
         wave_sync();
         store_rows<CC>(stage, rowq, reinterpret_cast<uint32_t *>(out_d), k, j0 - (KC - k), lane);
     }
@@ -862,14 +866,17 @@ knn_select_kernel(DevTree t, const float *__restrict__ q, const uint32_t *__rest
     }
 }
 
+#ifdef NBKD_EXPERIMENTS
 int dense_min() {
-    const char *e = getenv("NBKD_DENSE_MIN"); // tuning experiments only
+    const char *e = knob("NBKD_DENSE_MIN"); // tuning experiments only
     return e ? atoi(e) : 33;
 }
 
+#endif
+
 bool groups_enabled() {
     static const bool on = [] { // NBKD_GROUPS=0: leaf-level scan (A/B)
-        const char *e = getenv("NBKD_GROUPS");
+        const char *e = knob("NBKD_GROUPS");
         return !(e && atoi(e) == 0);
     }();
     return on;
@@ -884,7 +891,7 @@ void launch_collect(const Tree &t, const float *q, const uint32_t *order, uint32
     if (t.ginfo && groups_enabled()) {
         // NBKD_XCD_MAP=0: hardware block order (A/B of the XCD-contiguous packet ranges)
         static const bool xcd = [] {
-            const char *e = getenv("NBKD_XCD_MAP");
+            const char *e = knob("NBKD_XCD_MAP");
             return !(e && atoi(e) == 0);
         }();
         TimedScope ts(name, s);
@@ -898,9 +905,10 @@ void launch_collect(const Tree &t, const float *q, const uint32_t *order, uint32
                 ccount, nullptr, xcd);
         return;
     }
+#ifdef NBKD_EXPERIMENTS
     TimedScope ts(name, s);
     const int dm = dense_min();
-    const char *eo = getenv("NBKD_COLLECT_OCC"); // tuning experiments only
+    const char *eo = knob("NBKD_COLLECT_OCC"); // tuning experiments only
     const int occ = eo ? atoi(eo) : 8;
 #define NBKD_COLLECT(DM, OC, G, P)                                                                 \
     do {                                                                                           \
@@ -916,7 +924,7 @@ void launch_collect(const Tree &t, const float *q, const uint32_t *order, uint32
     // default: measured 74.5 vs 72.6 ms at 1e8 (8 waves per SIMD already hide
     // the staging latency; the kernel is VALU-issue bound)
     static const bool pipe = [] {
-        const char *e = getenv("NBKD_COLLECT_PIPE");
+        const char *e = knob("NBKD_COLLECT_PIPE");
         return e && atoi(e) != 0;
     }();
     if (occ <= 6) {
@@ -936,22 +944,25 @@ void launch_collect(const Tree &t, const float *q, const uint32_t *order, uint32
         NBKD_COLLECT(65, 8, 4, true);
     }
 #undef NBKD_COLLECT
+#else
+    (void)stats;
+#endif
 }
 
 template <int KC>
 void launch_select(const Tree &t, const float *q, const uint32_t *order, uint32_t m, int k,
                    uint32_t qpp, const uint2 *cand, uint32_t capg, const uint32_t *ccount,
                    float *od, uint32_t *oi, uint32_t *fail_list, uint32_t *fail_count,
-                   uint32_t pos_base, float *tg_fix, float mu, hipStream_t s) {
+                   uint32_t pos_base, float *tg_fix, float mu, bool sq, hipStream_t s) {
     const unsigned blocks = (m + TB - 1) / TB;
     static const uint64_t all_rows = [] { // NBKD_SELECT_ROWMASK=0: read whole blocks
-        const char *e = getenv("NBKD_SELECT_ROWMASK");
+        const char *e = knob("NBKD_SELECT_ROWMASK");
         return (e && atoi(e) == 0) ? ~0ull : 0ull;
     }();
 #define NBKD_SELECT(PER, WH)                                                                       \
     knn_select_kernel<KC, PER, WH><<<blocks, TB, 0, s>>>(view(t), q, order, m, k, qpp, cand, capg, \
                                                         ccount, od, oi, fail_list, fail_count,     \
-                                                        pos_base, all_rows, tg_fix, mu)
+                                                        pos_base, all_rows, tg_fix, mu, sq)
     if (t.periodic) {
         if (qpp == 64) NBKD_SELECT(true, true); else NBKD_SELECT(true, false);
     } else {
@@ -964,7 +975,7 @@ void launch_select(const Tree &t, const float *q, const uint32_t *order, uint32_
 
 bool retry_adaptive() {
     static const bool on = [] { // NBKD_RETRY_ADAPT=0: every retry seed is 4x (A/B)
-        const char *e = getenv("NBKD_RETRY_ADAPT");
+        const char *e = knob("NBKD_RETRY_ADAPT");
         return !(e && atoi(e) == 0);
     }();
     return on;
@@ -982,7 +993,7 @@ nbkd_status launch_knn_collect(const Tree &t, const float *q, const uint32_t *or
                                int k, const float *tg, float seed_mul, uint32_t qpp, uint2 *cand,
                                uint32_t capg, uint32_t *ccount, float *od, uint32_t *oi,
                                uint32_t *fail_list, uint32_t *fail_count, uint32_t pos_base,
-                               bool retry, bool fix_seed, unsigned long long *stats,
+                               bool retry, bool fix_seed, bool sq, unsigned long long *stats,
                                hipStream_t s) {
     if (m == 0) return NBKD_OK;
     if (t.periodic)
@@ -999,13 +1010,13 @@ nbkd_status launch_knn_collect(const Tree &t, const float *q, const uint32_t *or
         const float mu = (float)k + 4.0f * sqrtf((float)k) + 4.0f;
         if (k <= 16)
             launch_select<16>(t, q, order, m, k, qpp, cand, capg, ccount, od, oi, fail_list,
-                              fail_count, pos_base, tg_fix, mu, s);
+                              fail_count, pos_base, tg_fix, mu, sq, s);
         else if (k <= 32)
             launch_select<32>(t, q, order, m, k, qpp, cand, capg, ccount, od, oi, fail_list,
-                              fail_count, pos_base, tg_fix, mu, s);
+                              fail_count, pos_base, tg_fix, mu, sq, s);
         else
             launch_select<64>(t, q, order, m, k, qpp, cand, capg, ccount, od, oi, fail_list,
-                              fail_count, pos_base, tg_fix, mu, s);
+                              fail_count, pos_base, tg_fix, mu, sq, s);
         NBKD_HIP(hipGetLastError());
     }
     return NBKD_OK;

@@ -29,6 +29,9 @@
 
 #include <cstdlib>
 
+// A/B only: the production library (no NBKD_EXPERIMENTS) always has a seed
+// bound and runs the collect / select path (knn_collect.hip).
+#ifdef NBKD_EXPERIMENTS
 namespace nbkd {
 namespace {
 using namespace dev;
@@ -740,7 +743,7 @@ void launch5(const Tree &t, const float *q, const uint32_t *order, uint32_t m, i
 }
 
 int variant() {
-    const char *e = getenv("NBKD_KNN_VARIANT"); // read per call: tuning sweeps flip it
+    const char *e = knob("NBKD_KNN_VARIANT"); // read per call: tuning sweeps flip it
     return e ? atoi(e) : 0;
 }
 
@@ -771,3 +774,4 @@ void launch_knn_packet(const Tree &t, const float *q, const uint32_t *order, uin
 }
 
 } // namespace nbkd
+#endif // NBKD_EXPERIMENTS

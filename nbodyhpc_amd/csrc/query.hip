@@ -543,7 +543,7 @@ nbkd_status radix_sort(Workspace &ws, uint32_t *k0, uint32_t *v0, uint32_t *k1, 
     *vout = v0;
     if (n <= 1) return NBKD_OK;
     {
-        static const bool old_sort = getenv("NBKD_OLD_SORT") != nullptr; // A/B only
+        static const bool old_sort = knob("NBKD_OLD_SORT") != nullptr; // A/B only
         const int passes = (nbits + 7) / 8;
         if (!old_sort && n < OS_VAL && passes <= OS_MAXP) {
             *vout = (passes & 1) ? v1 : v0;
@@ -632,7 +632,7 @@ __global__ void __launch_bounds__(TB)
 knn_exact_kernel(DevTree t, const float *__restrict__ q, const uint32_t *__restrict__ list,
                  const uint32_t *__restrict__ list_count, uint32_t m_all, int k,
                  LtEntry *__restrict__ scratch, float *__restrict__ out_d,
-                 uint32_t *__restrict__ out_i) {
+                 uint32_t *__restrict__ out_i, bool sq) {
     const uint32_t tid = blockIdx.x * TB + threadIdx.x;
     const uint32_t nthreads = gridDim.x * TB;
     const uint32_t count = list_count ? *list_count : m_all;
@@ -708,12 +708,12 @@ knn_exact_kernel(DevTree t, const float *__restrict__ q, const uint32_t *__restr
             res[j] = v;
         }
         if (!out_i) { // k-th distance only
-            out_d[qi] = sqrtf(res[k - 1].d);
+            out_d[qi] = sq ? res[k - 1].d : sqrtf(res[k - 1].d);
             continue;
         }
         const size_t row = (size_t)qi * (size_t)k;
         for (int j = 0; j < k; ++j) {
-            out_d[row + j] = sqrtf(res[j].d);
+            out_d[row + j] = sq ? res[j].d : sqrtf(res[j].d);
             const uint32_t p = res[j].id;
             out_i[row + j] = p == 0xFFFFFFFFu ? p : t.idx[p];
         }
@@ -760,8 +760,10 @@ SeedParams seed_params(const Tree &t, int k) {
     // a = 3.5: at 1e8 uniform 1.400e9 q/s (20.5 k retries) vs 1.376e9 at a = 4
     // (4.9 k), 1.393e9 at 3, 1.372e9 at 2.5, 1.361e9 at 5; log-normal 82.3 ms
     // at both 3.5 and 4 (r02bg, r02bi).  The column capacity keeps a = 4.
-    const char *e = getenv("NBKD_KNN_SEED");
-    const float a = e ? (float)atof(e) : 3.5f;
+    // nbkd_set_tuning("knn_seed_margin") (default 3.5); NBKD_KNN_SEED in an
+    // experiments build (0 there: no seed, the register top-k packet kernel)
+    const char *e = knob("NBKD_KNN_SEED");
+    const float a = e ? (float)atof(e) : (float)tuning(TUNE_KNN_SEED);
     SeedParams p;
     p.on = a > 0.0f;
     const float mu = (float)k + a * sqrtf((float)k) + a;
@@ -770,7 +772,7 @@ SeedParams seed_params(const Tree &t, int k) {
     // descent: 128 points, or the leaf when leaves are larger (at leafsize 64
     // the former 4-leaf anchor, 256 points, smoothed clustered densities too
     // much: log-normal 1e8 retried 5.7 M queries)
-    const char *ea = getenv("NBKD_KNN_ANCHOR"); // tuning only: anchor in points
+    const char *ea = knob("NBKD_KNN_ANCHOR"); // tuning only: anchor in points
     p.anchor = std::max<uint32_t>((uint32_t)t.leaf, ea ? (uint32_t)std::max(1, atoi(ea)) : 128u);
     return p;
 }
@@ -785,7 +787,7 @@ nbkd_status sort_queries(const Tree &t, const float *dq, uint32_t m, uint32_t *&
     if (!order || !tmp || !keys || !keys2) return NBKD_ENOMEM;
     {
         TimedScope ts("leaf_key", s);
-        static const bool no_heap = getenv("NBKD_NO_HEAP_SPLITS") != nullptr; // A/B only
+        static const bool no_heap = knob("NBKD_NO_HEAP_SPLITS") != nullptr; // A/B only
         if (t.hsplit && !no_heap) {
             const unsigned blocks = (unsigned)std::min<uint64_t>((m + TB - 1) / TB, 8192);
             const float3 lo = t.periodic ? make_float3(0.0f, 0.0f, 0.0f)
@@ -838,12 +840,16 @@ nbkd_status stage_queries(const Tree &t, const float *q, uint64_t m, uint32_t fl
 // batches shorten the per-launch tails: 9 batches of 11 M queries (8 GiB) ->
 // 3 at 1e8 is 53.9 -> 51.5 ms of collect (r02at).
 uint64_t cand_budget() {
-    const char *eb = getenv("NBKD_CAND_BYTES");
+    const char *eb = knob("NBKD_CAND_BYTES");
     if (eb) return strtoull(eb, nullptr, 10);
+    const double tb = tuning(TUNE_CAND_BYTES); // nbkd_set_tuning("candidate_bytes"), 0 = auto
+    if (tb > 0.0) return (uint64_t)tb;
     size_t free_b = 0, total_b = 0;
     uint64_t b = 24ull << 30;
     if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b > 0)
-        b = std::min<uint64_t>(b, std::max<uint64_t>(free_b / 4, 1ull << 30));
+        // a quarter of the free memory, never more than what is free (the
+        // callers' minimum is one 64-query packet's column)
+        b = std::min<uint64_t>(b, free_b / 4);
     else
         (void)hipGetLastError();
     return b;
@@ -859,7 +865,7 @@ namespace {
 
 bool collect_disabled() {
     static const bool off = [] {
-        const char *e = getenv("NBKD_KNN_COLLECT");
+        const char *e = knob("NBKD_KNN_COLLECT");
         return e && atoi(e) == 0;
     }();
     return off;
@@ -871,11 +877,14 @@ nbkd_status knn_locked(const Tree &t, const float *q, uint64_t m, int k, float *
                        uint32_t *out_i, uint32_t flags, hipStream_t s) {
     const uint32_t mm = (uint32_t)m;
     const bool kth_only = out_i == nullptr;
+    const bool sq = (flags & NBKD_SQUARED) != 0;
     const size_t row_words = kth_only ? 1 : (size_t)k;
     const float *dq = nullptr;
     nbkd_status rc = stage_queries(t, q, m, flags, dq, s);
     if (rc) return rc;
-    const bool packet = k <= 64;
+    // the collect / select path needs the sub-leaf groups (every non-empty
+    // tree has them); k > 64 and the empty tree take the exact kernel
+    const bool packet = k <= 64 && t.ginfo != nullptr;
     const SeedParams sp = seed_params(t, k);
     float *tg = nullptr;
     if (packet && sp.on) {
@@ -923,10 +932,10 @@ nbkd_status knn_locked(const Tree &t, const float *q, uint64_t m, int k, float *
         if (!lt) return NBKD_ENOMEM;
         if (t.periodic)
             knn_exact_kernel<true><<<threads / TB, TB, 0, s>>>(view(t), dq, ord, nullptr, mm, k,
-                                                                lt, dd, di);
+                                                                lt, dd, di, sq);
         else
             knn_exact_kernel<false><<<threads / TB, TB, 0, s>>>(view(t), dq, ord, nullptr, mm, k,
-                                                                 lt, dd, di);
+                                                                 lt, dd, di, sq);
         NBKD_HIP(hipGetLastError());
     } else {
         if (tg && !collect_disabled()) {
@@ -953,7 +962,7 @@ nbkd_status knn_locked(const Tree &t, const float *q, uint64_t m, int k, float *
                     const uint32_t nb = (uint32_t)std::min<uint64_t>(batch, mm - b0);
                     rc = launch_knn_collect(t, dq, ord + b0, nb, k, tg, 1.0f, 64u, cand, capg,
                                             ccount, dd, di, rlist, rcount, (uint32_t)b0, false,
-                                            retry_adaptive(), stats, s);
+                                            retry_adaptive(), sq, stats, s);
                     if (rc) return rc;
                 }
             }
@@ -985,7 +994,7 @@ nbkd_status knn_locked(const Tree &t, const float *q, uint64_t m, int k, float *
                 // at 1e8 uniform (r02bi): 82 k failures 1.1 ms one per wave vs
                 // 1.9 as packets, 307 k 3.0 vs 2.0: packets from 1/512.
                 static const int force_qpp = [] { // NBKD_RETRY_QPP=1|64: A/B only
-                    const char *e = getenv("NBKD_RETRY_QPP");
+                    const char *e = knob("NBKD_RETRY_QPP");
                     return e ? atoi(e) : 0;
                 }();
                 const uint32_t rqpp = force_qpp == 1 || force_qpp == 64
@@ -1007,7 +1016,7 @@ nbkd_status knn_locked(const Tree &t, const float *q, uint64_t m, int k, float *
                     rc = launch_knn_collect(t, dq, rq + b0, nb, k, tg, second ? 1.0f : 4.0f,
                                             rqpp, rcand, capr, rcc, dd, di,
                                             second ? rlist : list, second ? rcount : count,
-                                            0xFFFFFFFFu, true, second, nullptr, s);
+                                            0xFFFFFFFFu, true, second, sq, nullptr, s);
                     if (rc) return rc;
                 }
                 uint32_t nr2 = 0;
@@ -1030,15 +1039,20 @@ nbkd_status knn_locked(const Tree &t, const float *q, uint64_t m, int k, float *
                         const uint32_t nb = (uint32_t)std::min<uint64_t>(rb2, nr2 - b0);
                         rc = launch_knn_collect(t, dq, rlist + b0, nb, k, tg, 1.0f, 1u, rcand2,
                                                 capr2, rcc2, dd, di, list, count, 0xFFFFFFFFu,
-                                                true, false, nullptr, s);
+                                                true, false, sq, nullptr, s);
                         if (rc) return rc;
                     }
                 }
             }
         } else {
+#ifdef NBKD_EXPERIMENTS
             TimedScope ts("knn", s);
             launch_knn_packet(t, dq, ord, mm, k, tg, dd, di, list, count, stats, s);
             NBKD_HIP(hipGetLastError());
+#else
+            set_error("internal: the kNN query has no seed bound (experiments-only path)");
+            return NBKD_EDEVICE;
+#endif
         }
         if (list) {
             TimedScope ts("knn_fallback", s);
@@ -1047,10 +1061,10 @@ nbkd_status knn_locked(const Tree &t, const float *q, uint64_t m, int k, float *
             if (!lt) return NBKD_ENOMEM;
             if (t.periodic)
                 knn_exact_kernel<true><<<threads / TB, TB, 0, s>>>(view(t), dq, list, count, mm, k,
-                                                                   lt, dd, di);
+                                                                   lt, dd, di, sq);
             else
                 knn_exact_kernel<false><<<threads / TB, TB, 0, s>>>(view(t), dq, list, count, mm,
-                                                                    k, lt, dd, di);
+                                                                    k, lt, dd, di, sq);
             NBKD_HIP(hipGetLastError());
             if (stats) NBKD_HIP(hipMemcpyAsync(stats + 8, count, 4, hipMemcpyDeviceToDevice, s));
         }
@@ -1095,7 +1109,8 @@ nbkd_status query_knn(const Tree &t, const float *q, uint64_t m, int k, float *o
                       uint32_t *out_i, uint32_t flags, hipStream_t s) {
     nbkd_status rc = knn_args(k, m);
     if (rc || m == 0) return rc;
-    std::lock_guard<std::mutex> lk(t.ws.mu);
+    WsCall call(t.ws, s);
+    NBKD_HIP(call.err);
     return knn_locked(t, q, m, k, out_d, out_i, flags, s);
 }
 
@@ -1103,10 +1118,11 @@ nbkd_status query_kth(const Tree &t, const float *q, uint64_t m, int k, float *o
                       uint32_t flags, hipStream_t s) {
     nbkd_status rc = knn_args(k, m);
     if (rc || m == 0) return rc;
-    std::lock_guard<std::mutex> lk(t.ws.mu);
+    WsCall call(t.ws, s);
+    NBKD_HIP(call.err);
     // the collect/select path writes the k-th distance alone; elsewhere the
     // rows go to scratch and column k-1 is copied out
-    if (k <= 64 && seed_params(t, k).on && !collect_disabled())
+    if (k <= 64 && t.ginfo && seed_params(t, k).on && !collect_disabled())
         return knn_locked(t, q, m, k, out_d, nullptr, flags, s);
     float *rd = (float *)t.ws.get(WS_KTHD, m * (size_t)k * 4, s);
     uint32_t *ri = (uint32_t *)t.ws.get(WS_KTHI, m * (size_t)k * 4, s);
@@ -1139,7 +1155,8 @@ static nbkd_status ball_common(const Tree &t, const float *q, uint64_t m, float 
         return NBKD_OK;
     }
     const uint32_t mm = (uint32_t)m;
-    std::lock_guard<std::mutex> lk(t.ws.mu);
+    WsCall call(t.ws, s);
+    NBKD_HIP(call.err);
     const float *dq = nullptr;
     nbkd_status rc = stage_queries(t, q, m, flags, dq, s);
     if (rc) return rc;

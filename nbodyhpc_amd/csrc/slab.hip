@@ -9,6 +9,7 @@
 #include <dlfcn.h>
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 #include <mutex>
@@ -115,6 +116,57 @@ __global__ void violations_kernel(const float *__restrict__ q, const float *__re
     if ((threadIdx.x & 63) == 0 && bal) atomicAdd(count, (unsigned long long)__popcll(bal));
 }
 
+// Second-round forwarding: the queries whose k-th
+// distance reaches past the left face cl (bit 0) or the right face ch (bit 1)
+// of the x-range the local result covers.  Per side the same f32 test as
+// violations_kernel (whose margin is the min of the two sides' gaps).
+__global__ void forward_kernel(const float *__restrict__ q, const float *__restrict__ dist,
+                               uint64_t m, int k, float cl, float ch, float slack,
+                               uint32_t *__restrict__ list, uint8_t *__restrict__ sides,
+                               uint64_t cap, unsigned long long *__restrict__ count) {
+    const int lane = threadIdx.x & 63;
+    for (uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x; i0 < m;
+         i0 += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t i = i0 + threadIdx.x;
+        uint32_t side = 0;
+        if (i < m) {
+            const float x = q[3 * i];
+            const float dk = dist[i * (uint64_t)k + (uint64_t)(k - 1)];
+            const float rel = 1.0f - 4e-7f;
+            if (!(dk < (x - cl) * rel - slack)) side |= 1u;
+            if (!(dk < (ch - x) * rel - slack)) side |= 2u;
+        }
+        const uint64_t bal = __ballot(side != 0u);
+        if (bal == 0) continue;
+        unsigned long long base = 0;
+        if (lane == 0) base = atomicAdd(count, (unsigned long long)__popcll(bal));
+        base = __shfl(base, 0, 64);
+        if (side) {
+            const uint64_t pos = base + (uint64_t)__popcll(bal & ((1ull << lane) - 1ull));
+            if (pos < cap) {
+                list[pos] = (uint32_t)i;
+                sides[pos] = (uint8_t)side;
+            }
+        }
+    }
+}
+
+// rows of `words` 32-bit words: gather dst[i] = src[idx[i]], scatter dst[idx[i]] = src[i]
+template <bool SCATTER>
+__global__ void rows_kernel(const uint32_t *__restrict__ src, uint32_t words,
+                            const uint32_t *__restrict__ idx, uint64_t n, uint32_t *__restrict__ dst) {
+    const uint64_t total = n * words;
+    for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+         t += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t r = t / words, w = t - r * words;
+        const uint64_t j = idx[r];
+        if (SCATTER)
+            dst[j * words + w] = src[t];
+        else
+            dst[t] = src[j * words + w];
+    }
+}
+
 // ------------------------------------------------------------------ RCCL (dlopen)
 struct Rccl {
     bool tried = false, ok = false;
@@ -219,7 +271,8 @@ nbkd_status nbkd_set_ids(nbkd_tree *tree, const uint32_t *ids, uint32_t flags, v
     if (t.n8 == 0) return NBKD_OK;
     DevGuard g(t.device);
     hipStream_t s = (hipStream_t)stream;
-    std::lock_guard<std::mutex> lk(t.ws.mu);
+    WsCall call(t.ws, s);
+    NBKD_HIP(call.err);
     const uint32_t *dids = ids;
     DevBuf tmp;
     if (!(flags & NBKD_INPUT_DEVICE)) {
@@ -308,6 +361,74 @@ nbkd_status nbkd_slab_violations(const float *q, const float *dist, uint64_t m, 
     NBKD_HIP(hipStreamSynchronize(s));
     return NBKD_OK;
     SLAB_CATCH
+}
+
+nbkd_status nbkd_slab_forward(const float *q, const float *dist, uint64_t m, int32_t k, float cl,
+                              float ch, uint32_t *out_list, uint8_t *out_sides, uint64_t capacity,
+                              uint64_t *count, int32_t device, void *stream) {
+    SLAB_TRY
+    if (!count || k <= 0 || (m > 0 && (!q || !dist)) || (capacity > 0 && (!out_list || !out_sides))) {
+        set_error("nbkd_slab_forward: bad argument");
+        return NBKD_EINVAL;
+    }
+    *count = 0;
+    if (m == 0) return NBKD_OK;
+    DevGuard g(device);
+    hipStream_t s = (hipStream_t)stream;
+    DevBuf dc;
+    NBKD_HIP(dc.alloc(8, s));
+    NBKD_HIP(hipMemsetAsync(dc.p, 0, 8, s));
+    const float mag = std::fmax(std::fabs(cl), std::fabs(ch));
+    const float slack = 4.0f * (std::nextafter(mag, INFINITY) - mag);
+    const unsigned blocks = (unsigned)std::min<uint64_t>((m + 255) / 256, 65536);
+    forward_kernel<<<blocks, 256, 0, s>>>(q, dist, m, k, cl, ch, slack, out_list, out_sides,
+                                          capacity, dc.as<unsigned long long>());
+    NBKD_HIP(hipGetLastError());
+    NBKD_HIP(hipMemcpyAsync(count, dc.p, 8, hipMemcpyDeviceToHost, s));
+    NBKD_HIP(hipStreamSynchronize(s));
+    return NBKD_OK;
+    SLAB_CATCH
+}
+
+static nbkd_status rows_common(const void *src, uint64_t row_bytes, const uint32_t *idx, uint64_t n,
+                               void *dst, int32_t device, void *stream, bool scatter) {
+    if (row_bytes == 0 || row_bytes % 4 != 0 || (n > 0 && (!src || !idx || !dst))) {
+        set_error("nbkd_rows_gather / nbkd_rows_scatter: bad argument");
+        return NBKD_EINVAL;
+    }
+    if (n == 0) return NBKD_OK;
+    DevGuard g(device);
+    hipStream_t s = (hipStream_t)stream;
+    const uint32_t words = (uint32_t)(row_bytes / 4);
+    const unsigned blocks = (unsigned)std::min<uint64_t>((n * words + 255) / 256, 65536);
+    if (scatter)
+        rows_kernel<true><<<blocks, 256, 0, s>>>((const uint32_t *)src, words, idx, n, (uint32_t *)dst);
+    else
+        rows_kernel<false><<<blocks, 256, 0, s>>>((const uint32_t *)src, words, idx, n, (uint32_t *)dst);
+    NBKD_HIP(hipGetLastError());
+    return NBKD_OK;
+}
+
+nbkd_status nbkd_rows_gather(const void *src, uint64_t row_bytes, const uint32_t *idx, uint64_t n,
+                             void *dst, int32_t device, void *stream) {
+    SLAB_TRY
+    return rows_common(src, row_bytes, idx, n, dst, device, stream, false);
+    SLAB_CATCH
+}
+
+nbkd_status nbkd_rows_scatter(const void *src, uint64_t row_bytes, const uint32_t *idx, uint64_t n,
+                              void *dst, int32_t device, void *stream) {
+    SLAB_TRY
+    return rows_common(src, row_bytes, idx, n, dst, device, stream, true);
+    SLAB_CATCH
+}
+
+nbkd_status nbkd_comm_probe(void) {
+    if (!rccl()) {
+        set_error(g_rccl.err);
+        return NBKD_EDEVICE;
+    }
+    return NBKD_OK;
 }
 
 nbkd_status nbkd_comm_unique_id(uint8_t *out) {

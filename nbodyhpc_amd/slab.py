@@ -92,6 +92,28 @@ def gen_slab_points(n_per: int, seed: int, box: float, rank: int, world: int):
     return out, ids.astype(np.uint32)
 
 
+def gen_uniform_slab(n_total: int, seed: int, box: float, rank: int, world: int, bounds=None):
+    """Rank `rank`'s slab of the SAME uniform set at every world size (strong
+    scaling): the stream of synth.uniform(n_total, seed, box) - PCG64(seed),
+    rows drawn in chunks of 2^24 - kept where slab_of(x) == rank.  Global ids
+    are the row numbers, so the union over ranks is exactly the one-GPU set."""
+    bounds = bounds_list(world, box) if bounds is None else bounds
+    if n_total > 0xFFFFFFFF:
+        raise ValueError("global ids exceed uint32")
+    rng = np.random.Generator(np.random.PCG64(seed))
+    xs, ids = [], []
+    chunk = 1 << 24
+    for s0 in range(0, n_total, chunk):
+        e = min(n_total, s0 + chunk)
+        c = rng.uniform(0.0, box, size=(e - s0, 3)).astype(np.float32)
+        m = slab_of(c[:, 0], bounds) == rank
+        xs.append(c[m])
+        ids.append((s0 + np.nonzero(m)[0]).astype(np.uint32))
+    if not xs:
+        return np.zeros((0, 3), np.float32), np.zeros(0, np.uint32)
+    return np.concatenate(xs), np.concatenate(ids)
+
+
 def _enqueue_agreed(dist, rank, what, enqueue):
     """Run `enqueue` (an RCCL grouped send/recv, enqueue only) and agree over
     gloo whether it succeeded everywhere.  Returns None when every rank
@@ -433,24 +455,31 @@ def init_comm(dist, rank, world, device, log=None):
         return None
     import torch
 
-    buf = torch.zeros(capi.COMM_ID_BYTES, dtype=torch.uint8)
-    # every rank loads RCCL (a unique id is the cheapest call that does) before
-    # any rank enters ncclCommInitRank, which blocks until all ranks join: a
-    # rank that cannot load it would leave the others waiting there for ever
+    # every rank loads RCCL (nbkd_comm_probe: no bootstrap listener) before any
+    # rank enters ncclCommInitRank, which blocks until all ranks join: a rank
+    # that cannot load it would leave the others waiting there for ever
     ok = torch.zeros(1, dtype=torch.int64)
     try:
-        uid = capi.comm_unique_id()
+        capi.comm_probe()
         ok[0] = 1
     except Exception as e:
         log(f"rank {rank}: RCCL unavailable: {e}")
     dist.all_reduce(ok, op=dist.ReduceOp.MIN)
     if not int(ok[0]):
         return None
+    # only rank 0 creates the unique id (ncclGetUniqueId starts the bootstrap
+    # root); its last byte says whether that worked
+    buf = torch.zeros(capi.COMM_ID_BYTES + 1, dtype=torch.uint8)
     if rank == 0:
-        buf = torch.tensor(list(uid), dtype=torch.uint8)
+        try:
+            buf = torch.tensor(list(capi.comm_unique_id()) + [1], dtype=torch.uint8)
+        except Exception as e:
+            log(f"rank 0: ncclGetUniqueId failed: {e}")
     dist.broadcast(buf, 0)
+    if int(buf[-1]) != 1:
+        return None
     try:
-        c = capi.Comm(bytes(buf.numpy().tobytes()), rank, world, device)
+        c = capi.Comm(bytes(buf[:-1].numpy().tobytes()), rank, world, device)
     except Exception as e:
         log(f"rank {rank}: ncclCommInitRank failed: {e}")
         c = None
@@ -540,3 +569,293 @@ def deposit_slab(own_xyz, own_w, own_r, rank, world, box, grid, ppu, dist, bound
     slab_grid = engine(payload[:, :3], payload[:, 3], payload[:, 4], tuple(int(g) for g in grid),
                        float(ppu), (box, box, box), subsample, (c0, wx))
     return c0, slab_grid
+
+
+# ------------------------------------------------ second-round exchange (§8(e)(3))
+# A slab-local kNN row is exact iff its k-th distance stays inside the x-range
+# the local tree covers (own slab +- h).  The rows that reach past a face are
+# forwarded: the query goes to the neighbour that owns the far side, which
+# answers with its own local kNN (in d2, NBKD_SQUARED), and the owner merges
+# the two rows: the union deduplicated by global id (a particle held by both
+# trees has the same coordinates, so the same d2), the k smallest by d2, then
+# sqrtf (KDTree::find_closest, kdtree/src/cpp/kdtree.cpp:133-159: insertion of
+# d2 < k-th, sorted by d2, sqrt last; tournament_tree.hpp:86-91).  The covered
+# range then extends to that neighbour's range; a row still reaching past it
+# goes one rank further, until every rank has been consulted (then the merge
+# is over all particles).  No tree is rebuilt and the halo never widens.
+LEFT, RIGHT = 1, 2
+_PAD = np.uint32(0xFFFFFFFF)
+_D2_PAD = np.float32(np.finfo(np.float32).max)
+_TAG_Q_R, _TAG_Q_L, _TAG_A_R, _TAG_A_L = 41, 42, 43, 44
+
+
+def unwrapped_bound(bounds, i: int, box: float) -> float:
+    """Cut i of the periodic sequence of slabs (i may be < 0 or > W)."""
+    world = len(bounds) - 1
+    return float(bounds[i % world]) + box * (i // world)
+
+
+def side_needs(x, dk, cl, ch):
+    """(needs left, needs right): the f32 test of nbkd_slab_forward / violations_kernel
+    (a k-th distance must stay strictly inside [cl, ch) with a relative gap of 4e-7
+    and 4 ulps of the larger face)."""
+    f32 = np.float32
+    x = np.asarray(x, f32)
+    dk = np.asarray(dk, f32)
+    cl, ch = f32(cl), f32(ch)
+    mag = max(abs(cl), abs(ch))
+    slack = f32(4.0) * np.spacing(f32(mag))
+    rel = f32(1.0 - 4e-7)
+    left = ~(dk < (x - cl) * rel - slack)
+    right = ~(dk < (ch - x) * rel - slack)
+    return left, right
+
+
+def merge_rows(d2a, ia, d2b, ib, k):
+    """Row-wise merge of two (n, k) d2-row sets: the k smallest d2 of the union,
+    deduplicated by id, sorted by (d2, id); padding entries (id 0xFFFFFFFF) fill
+    the rows that hold fewer than k particles, with d2 = FLT_MAX (the
+    reference's k > n rows, sqrtf(FLT_MAX))."""
+    d2 = np.concatenate([np.asarray(d2a, np.float32), np.asarray(d2b, np.float32)], axis=1)
+    ii = np.concatenate([np.asarray(ia, np.uint32), np.asarray(ib, np.uint32)], axis=1)
+    n = d2.shape[0]
+    od = np.full((n, k), _D2_PAD, np.float32)
+    oi = np.full((n, k), _PAD, np.uint32)
+    if n == 0:
+        return od, oi
+    o = np.lexsort((ii, d2), axis=-1)
+    d2 = np.take_along_axis(d2, o, axis=1)
+    ii = np.take_along_axis(ii, o, axis=1)
+    keep = ii != _PAD
+    keep[:, 1:] &= ~((ii[:, 1:] == ii[:, :-1]) & (d2[:, 1:] == d2[:, :-1]))
+    rank = np.cumsum(keep, axis=1) - 1
+    sel = keep & (rank < k)
+    r, c = np.nonzero(sel)
+    od[r, rank[r, c]] = d2[r, c]
+    oi[r, rank[r, c]] = ii[r, c]
+    return od, oi
+
+
+def _bytes_sendrecv(dist, right, left, send_r, send_l, n_fl, n_fr, row_shape, dtype, tags):
+    """gloo point-to-point of row arrays with explicit peers: send_r -> right,
+    send_l -> left; receive n_fl rows from left (its rightward message) and n_fr
+    from right (its leftward message).  Distinct tags keep the two directions
+    apart when left == right."""
+    import torch
+
+    itemsize = int(np.prod(row_shape)) * np.dtype(dtype).itemsize
+    rl = torch.empty(max(n_fl, 0) * itemsize, dtype=torch.uint8)
+    rr = torch.empty(max(n_fr, 0) * itemsize, dtype=torch.uint8)
+    reqs = []
+    for arr, peer, tag in ((send_r, right, tags[0]), (send_l, left, tags[1])):
+        a = np.ascontiguousarray(arr, dtype)
+        if a.size:
+            reqs.append(dist.isend(torch.from_numpy(a.reshape(-1).view(np.uint8).copy()), peer,
+                                   tag=tag))
+    if n_fl:
+        reqs.append(dist.irecv(rl, left, tag=tags[0]))
+    if n_fr:
+        reqs.append(dist.irecv(rr, right, tag=tags[1]))
+    for r in reqs:
+        r.wait()
+    shape = lambda n: (n,) + tuple(row_shape)
+    return (rl.numpy().view(dtype).reshape(shape(n_fl)),
+            rr.numpy().view(dtype).reshape(shape(n_fr)))
+
+
+class HostRows:
+    """Second-round backend over host arrays (the CPU tests: the oracle is the
+    local kNN engine).  knn_sq(q) -> (d2 (n, k) f32, global ids (n, k) u32)."""
+
+    def __init__(self, own_xyz, rows_d, rows_i, knn_sq, k, dist=None, rank=0, world=1):
+        self.own_xyz = np.asarray(own_xyz, np.float32)
+        self.rows_d, self.rows_i = rows_d, rows_i
+        self.knn_sq, self.k = knn_sq, k
+        self.dist, self.rank, self.world = dist, rank, world
+        self.transport = "gloo"
+
+    def forward(self, cl, ch):
+        left, right = side_needs(self.own_xyz[:, 0], self.rows_d[:, self.k - 1], cl, ch)
+        sides = left.astype(np.uint8) * LEFT + right.astype(np.uint8) * RIGHT
+        u = np.nonzero(sides)[0].astype(np.uint32)
+        return u, sides[u]
+
+    def coords(self, u):
+        return self.own_xyz[u]
+
+    def exchange(self, right, left, send_r, send_l, n_fl, n_fr, row_shape, dtype, tags):
+        return _bytes_sendrecv(self.dist, right, left, send_r, send_l, n_fl, n_fr, row_shape,
+                               dtype, tags)
+
+    def write(self, u, d2, ids):
+        self.rows_d[u] = np.sqrt(d2)
+        self.rows_i[u] = ids
+
+
+def second_round(be, rank, world, bounds, box, h, k, dist, log=None):
+    """Resolve every own row whose k-th distance reaches past the covered
+    x-range; all ranks call it together (it holds
+    collectives).  `be`: HostRows or DeviceRows.  Returns counters: the rows
+    forwarded at the first hop, the (query, hop) forwards, the hops run."""
+    import torch
+
+    st = {"rows_forwarded": 0, "forwards": 0, "hops": 0}
+    if world == 1:
+        return st
+    f32 = np.float32
+    cl0 = f32(f32(bounds[rank]) - f32(h))
+    ch0 = f32(f32(bounds[rank + 1]) + f32(h))
+    u, sides = be.forward(cl0, ch0)
+    t = torch.tensor([len(u)], dtype=torch.int64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    st["rows_forwarded"] = len(u)
+    if int(t[0]) == 0:
+        return st
+    qc = np.ascontiguousarray(be.coords(u), np.float32).reshape(-1, 3)
+    s_d2, s_id = be.knn_sq(qc)
+    s_d2 = np.array(s_d2, np.float32).reshape(len(u), k)
+    s_id = np.array(s_id, np.uint32).reshape(len(u), k)
+    rs = np.nonzero(sides & RIGHT)[0]
+    ls = np.nonzero(sides & LEFT)[0]
+    for j in range(1, world):
+        mine = torch.tensor([len(rs), len(ls)], dtype=torch.int64)
+        allc = [torch.zeros(2, dtype=torch.int64) for _ in range(world)]
+        dist.all_gather(allc, mine)
+        if sum(int(c.sum()) for c in allc) == 0:
+            break
+        st["hops"] = j
+        st["forwards"] += len(rs) + len(ls)
+        right, left = (rank + j) % world, (rank - j) % world
+        n_fl, n_fr = int(allc[left][0]), int(allc[right][1])
+        ql, qr = be.exchange(right, left, qc[rs], qc[ls], n_fl, n_fr, (3,), np.float32,
+                             (_TAG_Q_R, _TAG_Q_L))
+        a_d2, a_id = be.knn_sq(np.concatenate([ql.reshape(-1, 3), qr.reshape(-1, 3)]))
+        a_d2 = np.asarray(a_d2, np.float32).reshape(-1, k)
+        a_id = np.asarray(a_id, np.uint32).reshape(-1, k)
+        # answers go back the way their queries came: to the right for the
+        # queries that came from the right (their left-going rows), and so on
+        l_d2, r_d2 = be.exchange(right, left, a_d2[n_fl:], a_d2[:n_fl], len(ls), len(rs), (k,),
+                                 np.float32, (_TAG_A_R, _TAG_A_L))
+        l_id, r_id = be.exchange(right, left, a_id[n_fl:], a_id[:n_fl], len(ls), len(rs), (k,),
+                                 np.uint32, (_TAG_A_R + 10, _TAG_A_L + 10))
+        if len(rs):
+            s_d2[rs], s_id[rs] = merge_rows(s_d2[rs], s_id[rs], r_d2, r_id, k)
+        if len(ls):
+            s_d2[ls], s_id[ls] = merge_rows(s_d2[ls], s_id[ls], l_d2, l_id, k)
+        dk = np.sqrt(s_d2[:, k - 1])
+        ch = f32(f32(unwrapped_bound(bounds, rank + j + 1, box)) + f32(h))
+        cl = f32(f32(unwrapped_bound(bounds, rank - j, box)) - f32(h))
+        if len(rs):
+            rs = rs[side_needs(qc[rs, 0], dk[rs], cl, ch)[1]]
+        if len(ls):
+            ls = ls[side_needs(qc[ls, 0], dk[ls], cl, ch)[0]]
+    be.write(u, s_d2, s_id)
+    if log is not None and st["rows_forwarded"]:
+        log(f"rank {rank}: {st['rows_forwarded']} rows forwarded, {st['forwards']} forwards "
+            f"over {st['hops']} hop(s)")
+    return st
+
+
+class DeviceRows:
+    """Second-round backend over a DeviceSlab: the own queries are the first
+    n_own rows of ds.xyz, their rows (od, oi device pointers) or their k-th
+    distances only (kth device pointer) were written by the local tree, whose
+    ids are global (nbkd_set_ids).  The forward test runs on the device
+    (nbkd_slab_forward); the few forwarded rows travel over RCCL (device
+    buffers, grouped send/recv) when the slab has a communicator, else over
+    gloo; the neighbour's answer is its tree's NBKD_SQUARED kNN."""
+
+    def __init__(self, ds, tree, k, od_ptr=None, oi_ptr=None, kth_ptr=None, stream=None):
+        self.ds, self.tree, self.k = ds, tree, int(k)
+        self.od_ptr, self.oi_ptr, self.kth_ptr = od_ptr, oi_ptr, kth_ptr
+        self.stream = stream
+        self._cap = 0
+        self._list = self._sides = None
+        self.transport = "rccl" if ds.comm is not None else "gloo"
+
+    def forward(self, cl, ch):
+        from . import capi, hip
+
+        ds = self.ds
+        dptr, kk = (self.kth_ptr, 1) if self.kth_ptr is not None else (self.od_ptr, self.k)
+        for _ in range(2):
+            n = capi.slab_forward(ds.xyz.ptr, dptr, ds.n_own, kk, cl, ch,
+                                  self._list.ptr if self._cap else None,
+                                  self._sides.ptr if self._cap else None, self._cap,
+                                  device=ds.device, stream=self.stream)
+            if n <= self._cap:
+                break
+            self._cap = max(n, 2 * self._cap, 1024)
+            self._list = hip.DeviceArray((self._cap,), np.uint32)
+            self._sides = hip.DeviceArray((self._cap,), np.uint8)
+        if n == 0:
+            return np.zeros(0, np.uint32), np.zeros(0, np.uint8)
+        u = self._list.numpy_head(n)
+        sides = self._sides.numpy_head(n)
+        o = np.argsort(u, kind="stable")  # the device list is in completion order
+        return u[o], sides[o]
+
+    def coords(self, u):
+        from . import capi, hip
+
+        if len(u) == 0:
+            return np.zeros((0, 3), np.float32)
+        du = hip.DeviceArray.from_numpy(np.ascontiguousarray(u, np.uint32))
+        dq = hip.DeviceArray((len(u), 3), np.float32)
+        capi.rows_gather(self.ds.xyz.ptr, 12, du.ptr, len(u), dq.ptr, self.ds.device,
+                         self.stream)
+        hip.synchronize()
+        return dq.numpy()
+
+    def knn_sq(self, q):
+        q = np.ascontiguousarray(q, np.float32).reshape(-1, 3)
+        if len(q) == 0:
+            return np.zeros((0, self.k), np.float32), np.zeros((0, self.k), np.uint32)
+        return self.tree.query(q, self.k, squared=True)
+
+    def exchange(self, right, left, send_r, send_l, n_fl, n_fr, row_shape, dtype, tags):
+        if self.ds.comm is None:
+            return _bytes_sendrecv(self.ds.dist, right, left, send_r, send_l, n_fl, n_fr,
+                                   row_shape, dtype, tags)
+        from . import hip
+
+        rb = int(np.prod(row_shape)) * np.dtype(dtype).itemsize
+        sr = np.ascontiguousarray(send_r, dtype)
+        sl = np.ascontiguousarray(send_l, dtype)
+        bufs = [hip.DeviceArray((max(a.nbytes, 4),), np.uint8) for a in (sr, sl)]
+        for b, a in zip(bufs, (sr, sl)):
+            hip.memcpy(b.ptr, a.ctypes.data, a.nbytes, hip.H2D)
+        rl = hip.DeviceArray((max(n_fl * rb, 4),), np.uint8)
+        rr = hip.DeviceArray((max(n_fr * rb, 4),), np.uint8)
+        pairs = [(bufs[0].ptr, sr.nbytes, right, rl.ptr, n_fl * rb, left),
+                 (bufs[1].ptr, sl.nbytes, left, rr.ptr, n_fr * rb, right)]
+        err = _enqueue_agreed(self.ds.dist, self.ds.rank, "second-round exchange",
+                              lambda: self.ds.comm.exchange(pairs, stream=self.stream))
+        if err is not None:
+            # every rank failed to enqueue: the buffers may still be touched
+            _ABANDONED.extend(bufs + [rl, rr])
+            self.transport = "gloo"
+            return _bytes_sendrecv(self.ds.dist, right, left, send_r, send_l, n_fl, n_fr,
+                                   row_shape, dtype, tags)
+        hip.synchronize()
+        shape = lambda n: (n,) + tuple(row_shape)
+        out_l = rl.numpy_head(n_fl * rb).view(dtype).reshape(shape(n_fl))
+        out_r = rr.numpy_head(n_fr * rb).view(dtype).reshape(shape(n_fr))
+        return out_l, out_r
+
+    def write(self, u, d2, ids):
+        from . import capi, hip
+
+        if len(u) == 0:
+            return
+        du = hip.DeviceArray.from_numpy(np.ascontiguousarray(u, np.uint32))
+        dev, s = self.ds.device, self.stream
+        if self.kth_ptr is not None:
+            col = hip.DeviceArray.from_numpy(np.sqrt(np.ascontiguousarray(d2[:, self.k - 1])))
+            capi.rows_scatter(col.ptr, 4, du.ptr, len(u), self.kth_ptr, dev, s)
+        else:
+            dd = hip.DeviceArray.from_numpy(np.sqrt(np.asarray(d2, np.float32)))
+            di = hip.DeviceArray.from_numpy(np.ascontiguousarray(ids, np.uint32))
+            capi.rows_scatter(dd.ptr, 4 * self.k, du.ptr, len(u), self.od_ptr, dev, s)
+            capi.rows_scatter(di.ptr, 4 * self.k, du.ptr, len(u), self.oi_ptr, dev, s)
+        hip.synchronize()

@@ -7,6 +7,7 @@ export TMPDIR=/tmp
 TAG=${TAG:-r01}
 O=gpurun_out/$TAG
 mkdir -p $O
+sha256sum nbodyhpc_amd/lib/libnbkd.so > $O/lib.sha256
 B="python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-parity"
 echo "[round] gpu tests"; date
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $O/tests.log 2>&1 \

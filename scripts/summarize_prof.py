@@ -84,7 +84,12 @@ def main():
         w_kib = sum(wv) / len(wv)
         hbm = 2.0 * 1024.0 * f_kib + 1024.0 * w_kib
         cfg = (b or {}).get("config", {})
+        shaf = os.path.join(src, "lib.sha256")
+        lib_sha = open(shaf).read().split()[0] if os.path.exists(shaf) else None
         out = {
+            # the libnbkd.so these counters were measured with (bench.py uses the
+            # file only when the loaded library has the same SHA-256)
+            "lib_sha256": lib_sha,
             "kernel": (b or {}).get("roofline", {}).get("kernel", regex),
             "command": f"rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE --kernel-include-regex {regex} -- "
                        "python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-parity",

@@ -86,3 +86,44 @@ def test_deposit_arguments_rejected_before_any_device_call():
     assert L.nbkd_deposit(None, None, None, 4, 8, 8, 8, 1.0, None, 4, 0, 0, 8, None, -1, 0,
                           None) == capi.NBKD_EINVAL
     assert b"NULL" in L.nbkd_last_error()
+
+
+def test_production_library_reads_no_environment():
+    """Algorithm choices cannot change with the caller's environment: the
+    production libnbkd.so imports no getenv (the A/B overrides exist only in
+    the -DNBKD_EXPERIMENTS build, lib/exp/, loaded through NBKD_LIB)."""
+    import subprocess
+
+    out = subprocess.run(["nm", "-D", "--undefined-only", capi.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    assert "getenv" not in out
+
+
+def test_tuning_knobs_validated():
+    old = capi.get_tuning("knn_seed_margin")
+    assert old > 0
+    try:
+        capi.set_tuning("knn_seed_margin", 2.0)
+        assert capi.get_tuning("knn_seed_margin") == 2.0
+        for bad in (0.0, -1.0, float("nan"), float("inf")):
+            with pytest.raises(capi.NbkdError, match="out of range"):
+                capi.set_tuning("knn_seed_margin", bad)
+        with pytest.raises(capi.NbkdError, match="unknown knob"):
+            capi.set_tuning("no_such_knob", 1.0)
+        with pytest.raises(capi.NbkdError, match="out of range"):
+            capi.set_tuning("candidate_bytes", -5.0)
+    finally:
+        capi.set_tuning("knn_seed_margin", old)
+
+
+def test_row_and_forward_arguments_rejected():
+    L = capi.lib()
+    c = ctypes.c_uint64()
+    assert L.nbkd_slab_forward(None, None, 5, 4, 0.0, 1.0, None, None, 0, ctypes.byref(c), 0,
+                               None) == capi.NBKD_EINVAL
+    assert L.nbkd_slab_forward(None, None, 0, 0, 0.0, 1.0, None, None, 0, ctypes.byref(c), 0,
+                               None) == capi.NBKD_EINVAL
+    assert L.nbkd_rows_gather(None, 6, None, 0, None, 0, None) == capi.NBKD_EINVAL  # 6 % 4 != 0
+    assert L.nbkd_rows_scatter(None, 8, None, 3, None, 0, None) == capi.NBKD_EINVAL
+    # zero rows: nothing to do, no device touched
+    assert L.nbkd_rows_gather(None, 8, None, 0, None, 0, None) == capi.NBKD_OK

@@ -230,14 +230,22 @@ def test_device_pointer_path(gpu):
 
 
 # ---------------------------------------------------------------- seed ball retries
-@pytest.mark.parametrize("seed_param", ["0.05", "0"])
+@pytest.fixture
+def tuning(gpu):
+    """nbkd_set_tuning knobs, restored after the test."""
+    saved = {n: gpu.get_tuning(n) for n in ("knn_seed_margin", "candidate_bytes")}
+    yield gpu.set_tuning
+    for n, v in saved.items():
+        gpu.set_tuning(n, v)
+
+
 @pytest.mark.parametrize("box", [None, 1.0])
-def test_knn_seed_retry_and_no_seed(gpu, oracle, monkeypatch, seed_param, box):
-    """A tiny seed ball (NBKD_KNN_SEED=0.05) makes most queries fail the collect
-    pass: they go through the adaptive-seed retry, its second round (one query
-    per wave, 64x column) and, failing those, the exact kernel.
-    NBKD_KNN_SEED=0 switches the seed off (register top-k packet kernel)."""
-    monkeypatch.setenv("NBKD_KNN_SEED", seed_param)
+def test_knn_seed_retry(gpu, oracle, tuning, box):
+    """A tiny seed ball (knn_seed_margin 0.05) makes most queries fail the
+    collect pass: they go through the adaptive-seed retry, its second round
+    (one query per wave, 64x column) and, failing those, the exact kernel.
+    A candidate budget of a few packets cuts the first pass into many batches."""
+    tuning("knn_seed_margin", 0.05)
     pts = uniform(60_000, 31, L=box or 1.0)
     rng = np.random.Generator(np.random.PCG64(32))
     q = np.concatenate([pts[:3000], rng.uniform(0, box or 1.0, (2000, 3)).astype(np.float32)])
@@ -247,6 +255,27 @@ def test_knn_seed_retry_and_no_seed(gpu, oracle, monkeypatch, seed_param, box):
         d, i = t.query(q, k)
         dr, ir = o.query(q, k)
         assert_knn_equal(d, i, dr, ir, pts, q, box)
+    tuning("knn_seed_margin", 3.5)
+    tuning("candidate_bytes", 64 * 112 * 8 * 3)  # three 64-query packets per batch
+    d, i = t.query(q, 32)
+    dr, ir = o.query(q, 32)
+    assert_knn_equal(d, i, dr, ir, pts, q, box)
+
+
+def test_squared_output(gpu, oracle):
+    """NBKD_SQUARED: the d2 the rows are sorted by (kdtree.cpp:149-151), whose
+    sqrtf is the plain output, bit for bit (collect/select, exact and k > 64)."""
+    pts = uniform(40_000, 61)
+    rng = np.random.Generator(np.random.PCG64(62))
+    q = np.concatenate([pts[:1000], rng.uniform(-0.2, 1.2, (500, 3)).astype(np.float32)])
+    t = gpu.Tree(pts, leafsize=32, boxsize=None)
+    tp = gpu.Tree(np.clip(pts, 0, 1), leafsize=32, boxsize=1.0)
+    for tree in (t, tp):
+        for k in (8, 32, 100):
+            d, i = tree.query(q, k)
+            d2, i2 = tree.query(q, k, squared=True)
+            assert np.array_equal(np.sqrt(d2), d)
+            assert np.array_equal(i2, i)
 
 
 @pytest.mark.parametrize("box", [None, 1.0])
@@ -308,7 +337,7 @@ def test_knn_degenerate_planar_points(gpu, oracle, box):
 
 
 @pytest.mark.parametrize("box", [None, 1.0])
-def test_kth_distance_equals_row_column(gpu, monkeypatch, box):
+def test_kth_distance_equals_row_column(gpu, tuning, box):
     """nbkd_query_kth == column k-1 of nbkd_query_knn, bit for bit: the
     collect/select k-th-only output, the exact-kernel fallback (out-of-box
     periodic queries, forced seed failures) and the k > 64 row path."""
@@ -321,7 +350,7 @@ def test_kth_distance_equals_row_column(gpu, monkeypatch, box):
     for k in (1, 8, 32, 64, 100):
         d, _ = t.query(q, k)
         assert np.array_equal(t.query_kth(q, k), d[:, k - 1]), k
-    monkeypatch.setenv("NBKD_KNN_SEED", "0.05")  # most queries retried / exact
+    tuning("knn_seed_margin", 0.05)  # most queries retried / exact
     for k in (16, 32):
         d, _ = t.query(q, k)
         assert np.array_equal(t.query_kth(q, k), d[:, k - 1]), k

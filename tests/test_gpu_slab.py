@@ -98,7 +98,7 @@ def _rank_points(n_per, rank, world):
     return xyz, ids
 
 
-def _worker(rank, world, port, n_per, k, outdir, rccl=False):
+def _worker(rank, world, port, n_per, k, outdir, rccl=False, hscale=1.0):
     from nbodyhpc_amd import capi, hip
 
     hip.preload()  # the ROCm 7.2 runtime must load before torch's bundled one
@@ -115,7 +115,7 @@ def _worker(rank, world, port, n_per, k, outdir, rccl=False):
         if rccl and comm is None:
             raise RuntimeError("RCCL communicator did not start")
         ds = slab.DeviceSlab(xyz, ids, rank, world, 1.0, dev, dist, comm=comm)
-        h = slab.halo_width(n_per * world, k, 1.0)
+        h = slab.halo_width(n_per * world, k, 1.0) * hscale
         ds.exchange(h)
         t = capi.Tree(n=ds.n_local, dev_ptr=ds.xyz.ptr, leafsize=32, boxsize=1.0, device=dev)
         t.set_ids(dev_ptr=ds.ids.ptr)
@@ -124,8 +124,19 @@ def _worker(rank, world, port, n_per, k, outdir, rccl=False):
         t.query_device(ds.xyz.ptr, n_per, k, od.ptr, oi.ptr)
         hip.synchronize()
         v = ds.violations(od.ptr, k)
+        # second-round exchange (device forward test, gather / scatter, RCCL or gloo)
+        rows = slab.DeviceRows(ds, t, k, od.ptr, oi.ptr)
+        st = slab.second_round(rows, rank, world, ds.bounds, 1.0, ds.h, k, dist)
+        hip.synchronize()
+        # and the k-th-distance-only form of the same resolution
+        rk = hip.DeviceArray((n_per,), np.float32)
+        t.query_kth_device(ds.xyz.ptr, n_per, k, rk.ptr)
+        slab.second_round(slab.DeviceRows(ds, t, k, kth_ptr=rk.ptr), rank, world, ds.bounds,
+                          1.0, ds.h, k, dist)
+        hip.synchronize()
         np.savez(os.path.join(outdir, f"r{rank}.npz"), d=od.numpy(), i=oi.numpy(), v=v,
-                 nloc=ds.n_local, transport=ds.transport)
+                 nloc=ds.n_local, transport=ds.transport, fwd=st["rows_forwarded"],
+                 sr_transport=rows.transport, rk=rk.numpy())
         t.close()
         if comm is not None:
             comm.close()
@@ -133,14 +144,15 @@ def _worker(rank, world, port, n_per, k, outdir, rccl=False):
         dist.destroy_process_group()
 
 
-def _run_two_ranks(tmp_path, oracle, rccl):
+def _run_two_ranks(tmp_path, oracle, rccl, hscale=1.0):
     import multiprocessing as mp
 
     from tests.parity import assert_knn_equal
     world, n_per, k = 2, 60_000, 32
     ctx = mp.get_context("spawn")  # plain multiprocessing: torch must not load first
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, n_per, k, str(tmp_path), rccl))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n_per, k, str(tmp_path), rccl,
+                                               hscale))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -153,12 +165,18 @@ def _run_two_ranks(tmp_path, oracle, rccl):
     parts = [_rank_points(n_per, r, world)[0] for r in range(world)]
     allp = np.concatenate(parts)
     gd, gi = oracle.tree(allp, 32, 1.0).query(allp, k, workers=8)
+    fwd = 0
     for r in range(world):
         res = np.load(os.path.join(tmp_path, f"r{r}.npz"))
-        assert int(res["v"]) == 0 and res["nloc"] > n_per
+        assert res["nloc"] > n_per
+        assert int(res["fwd"]) == int(res["v"])
+        fwd += int(res["fwd"])
         assert str(res["transport"]) == ("rccl" if rccl else "gloo-staged")
+        assert str(res["sr_transport"]) == ("rccl" if rccl else "gloo")
         sl = slice(r * n_per, (r + 1) * n_per)
         assert_knn_equal(res["d"], res["i"], gd[sl], gi[sl], allp, parts[r], 1.0)
+        assert np.array_equal(res["rk"], gd[sl][:, -1])
+    assert (fwd > 0) == (hscale < 1.0)  # a thin halo leaves rows to the second round
     # the x = L particles of the last rank are rank 0's neighbours at x = 0
     assert np.isin(np.arange((world - 1) * n_per, (world - 1) * n_per + 32),
                    np.load(os.path.join(tmp_path, "r0.npz"))["i"]).any()
@@ -168,12 +186,56 @@ def test_two_rank_slab_knn_on_one_gpu(gpu, oracle, tmp_path):
     _run_two_ranks(tmp_path, oracle, rccl=False)
 
 
+def test_two_rank_second_round_on_one_gpu(gpu, oracle, tmp_path):
+    """SURVEY.md §8(e)(3) on the device path: a halo a tenth of the usual width
+    leaves thousands of rows reaching past it; the second-round exchange
+    (nbkd_slab_forward, the neighbour's NBKD_SQUARED kNN, merge, row scatter)
+    makes every row and every k-th distance equal the single-tree result."""
+    _run_two_ranks(tmp_path, oracle, rccl=False, hscale=0.1)
+
+
 def test_two_rank_slab_knn_rccl(gpu, oracle, tmp_path):
     """The RCCL halo path proper: one GPU per rank, grouped ncclSend/ncclRecv
-    with both ring neighbours being the same peer (W = 2).  Needs two GPUs."""
+    with both ring neighbours being the same peer (W = 2), and the second round
+    over RCCL.  Needs two GPUs."""
     if gpu.device_count() < 2:
         pytest.skip("the RCCL halo path needs two GPUs (one per rank)")
     _run_two_ranks(tmp_path, oracle, rccl=True)
+    _run_two_ranks(tmp_path, oracle, rccl=True, hscale=0.1)
+
+
+def test_forward_and_row_kernels_match_host(gpu):
+    """nbkd_slab_forward == slab.side_needs (per side, f32); row gather / scatter."""
+    from nbodyhpc_amd import hip
+    rng = np.random.default_rng(9)
+    m, k = 30_000, 8
+    q = rng.uniform(0, 1, (m, 3)).astype(np.float32)
+    q[:, 0] = rng.uniform(0.25, 0.5, m).astype(np.float32)
+    dist = rng.uniform(0, 0.03, (m, k)).astype(np.float32)
+    cl, ch = np.float32(0.24), np.float32(0.51)
+    left, right = slab.side_needs(q[:, 0], dist[:, -1], cl, ch)
+    want = np.nonzero(left | right)[0]
+    dq, dd = hip.DeviceArray.from_numpy(q), hip.DeviceArray.from_numpy(dist)
+    assert gpu.slab_forward(dq.ptr, dd.ptr, m, k, cl, ch) == len(want) > 0
+    lst = hip.DeviceArray((len(want),), np.uint32)
+    sides = hip.DeviceArray((len(want),), np.uint8)
+    assert gpu.slab_forward(dq.ptr, dd.ptr, m, k, cl, ch, lst.ptr, sides.ptr, len(want)) == len(want)
+    got, gs = lst.numpy(), sides.numpy()
+    o = np.argsort(got)
+    assert np.array_equal(got[o], want)
+    assert np.array_equal(gs[o], (left[want] * 1 + right[want] * 2).astype(np.uint8))
+    idx = rng.permutation(m)[:5000].astype(np.uint32)
+    di = hip.DeviceArray.from_numpy(idx)
+    g = hip.DeviceArray((5000, k), np.float32)
+    gpu.rows_gather(dd.ptr, 4 * k, di.ptr, 5000, g.ptr)
+    hip.synchronize()
+    assert np.array_equal(g.numpy(), dist[idx])
+    z = hip.DeviceArray.from_numpy(np.zeros((m, k), np.float32))
+    gpu.rows_scatter(g.ptr, 4 * k, di.ptr, 5000, z.ptr)
+    hip.synchronize()
+    want_z = np.zeros((m, k), np.float32)
+    want_z[idx] = dist[idx]
+    assert np.array_equal(z.numpy(), want_z)
 
 
 def test_bench_c5_line_small(gpu, oracle, monkeypatch, capsys):
@@ -192,7 +254,7 @@ def test_bench_c5_line_small(gpu, oracle, monkeypatch, capsys):
                                       "--k", str(k), "--leafsize", "32", "--steps", "1",
                                       "--warmup", "0"])
     args = bench.parse()
-    bench.run_c5(args, 0, 1, 0, None, False, lambda: None, lambda v: v)
+    bench.run_c5(args, 0, 1, 0, None, False, lambda: None, lambda v: v, lambda v: v)
     line = json.loads(capsys.readouterr().out.strip().splitlines()[-1])
     assert line["n_gpus"] == 1 and line["config"]["n_particles"] == n
     pts, _, _ = synth.lognormal_slab(n, 0, 1, grid=grid)

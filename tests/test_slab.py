@@ -349,7 +349,7 @@ def test_deposit_slabs_tile_the_single_deposit(world, tmp_path, oracle):
     assert abs(got.sum() - w.sum()) < 0.01 * w.sum()
 
 
-def _comm_worker(rank, world, port, fail_rank, outdir):
+def _comm_worker(rank, world, port, fail_rank, fail_uid, outdir):
     import torch.distributed as dist
 
     from nbodyhpc_amd import capi
@@ -357,11 +357,16 @@ def _comm_worker(rank, world, port, fail_rank, outdir):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    calls = []
+    calls, uids = [], []
     try:
-        def uid():
+        def probe():
             if rank == fail_rank:
                 raise RuntimeError("cannot load librccl.so.1 (test)")
+
+        def uid():
+            uids.append(rank)
+            if fail_uid:
+                raise RuntimeError("ncclGetUniqueId failed (test)")
             return bytes(capi.COMM_ID_BYTES)
 
         class NoInit:  # must never be reached when some rank lacks RCCL
@@ -369,22 +374,124 @@ def _comm_worker(rank, world, port, fail_rank, outdir):
                 calls.append(a)
                 raise AssertionError("ncclCommInitRank entered")
 
-        capi.comm_unique_id, capi.Comm = uid, NoInit
+        capi.comm_probe, capi.comm_unique_id, capi.Comm = probe, uid, NoInit
         c = slab.init_comm(dist, rank, world, 0)
-        np.savez(os.path.join(outdir, f"c{rank}.npz"), none=c is None, init_calls=len(calls))
+        np.savez(os.path.join(outdir, f"c{rank}.npz"), none=c is None, init_calls=len(calls),
+                 uid_calls=len(uids))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,fail_rank", [(2, 1), (3, 0)])
-def test_init_comm_agrees_before_rccl_init(world, fail_rank, tmp_path):
+@pytest.mark.parametrize("world,fail_rank,fail_uid", [(2, 1, False), (3, 0, False), (3, -1, True)])
+def test_init_comm_agrees_before_rccl_init(world, fail_rank, fail_uid, tmp_path):
     """slab.init_comm: ncclCommInitRank blocks until every rank joins, so a rank
-    that cannot load RCCL must stop all ranks before any enters it (gloo, CPU)."""
+    that cannot load RCCL (or a failed unique id on rank 0) must stop all ranks
+    before any enters it (gloo, CPU).  Only rank 0 creates the unique id: each
+    ncclGetUniqueId starts a bootstrap listener that only rank 0's id uses."""
     import torch.multiprocessing as mp
 
     port = _free_port()
-    mp.start_processes(_comm_worker, args=(world, port, fail_rank, str(tmp_path)), nprocs=world,
-                       join=True, start_method="spawn")
+    mp.start_processes(_comm_worker, args=(world, port, fail_rank, fail_uid, str(tmp_path)),
+                       nprocs=world, join=True, start_method="spawn")
     for r in range(world):
         res = np.load(os.path.join(tmp_path, f"c{r}.npz"))
         assert bool(res["none"]) and int(res["init_calls"]) == 0, r
+        assert int(res["uid_calls"]) == (1 if (r == 0 and fail_rank < 0) else 0), r
+
+
+# ------------------------------------------------ second-round exchange (§8(e)(3))
+def _sr_worker(rank, world, port, n, k, hscale, kind, outdir):
+    """A deliberately thin halo (h << the k-th neighbour radius): the slab-local
+    rows reaching past the covered x-range are forwarded to the neighbours and
+    merged (slab.second_round, gloo transport, the oracle as the local kNN)."""
+    import torch.distributed as dist
+
+    from nbodyhpc_amd import synth
+    from oracle.oracle import Oracle
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        if kind == "lognormal":
+            xyz, ids, bounds = synth.lognormal_slab(n, rank, world, grid=16)
+        else:
+            xyz, ids = _slab_points(n // world, 17, rank, world)
+            bounds = slab.bounds_list(world, 1.0)
+        h = slab.halo_width(n, k, 1.0) * hscale
+        lx, li = slab.exchange_host(xyz, ids, rank, world, 1.0, h, dist, bounds=bounds)
+        tree = Oracle().tree(lx, 16, 1.0)
+
+        def gids(i):
+            return np.where(i == 0xFFFFFFFF, np.uint32(0xFFFFFFFF),
+                            li[np.minimum(i, len(li) - 1)]).astype(np.uint32)
+
+        def knn_sq(q):
+            d2, i = tree.query(q, k, sqrt=False)
+            return d2, gids(i)
+
+        d, i = tree.query(xyz, k)
+        gi = gids(i)
+        v0 = slab.violations_host(xyz, d[:, -1], rank, world, 1.0, h, bounds=bounds)
+        be = slab.HostRows(xyz, d, gi, knn_sq, k, dist, rank, world)
+        st = slab.second_round(be, rank, world, bounds, 1.0, h, k, dist)
+        np.savez(os.path.join(outdir, f"sr{rank}.npz"), d=d, i=gi, xyz=xyz, ids=ids, v0=v0,
+                 nloc=len(lx), fwd=st["rows_forwarded"], hops=st["hops"])
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n,k,hscale,kind", [
+    (2, 8000, 8, 0.05, "uniform"), (3, 9000, 8, 0.05, "uniform"),
+    (4, 400, 48, 0.02, "uniform"),  # k-th radii wider than a slab: hops to the 2nd neighbour
+    (2, 12_000, 8, 0.1, "lognormal"), (3, 12_000, 16, 0.1, "lognormal")])
+def test_second_round_exchange_equals_single_tree(world, n, k, hscale, kind, tmp_path, oracle):
+    """SURVEY.md §8(e)(3): with a thin halo many slab-local rows are not exact;
+    after the second-round exchange every row equals the single-tree oracle
+    over all particles (tie-aware, bit-exact distances) - no rebuild, no
+    halo widening."""
+    import torch.multiprocessing as mp
+
+    from tests.parity import assert_knn_equal
+
+    port = _free_port()
+    mp.start_processes(_sr_worker, args=(world, port, n, k, hscale, kind, str(tmp_path)),
+                       nprocs=world, join=True, start_method="spawn")
+    res = [np.load(os.path.join(tmp_path, f"sr{r}.npz")) for r in range(world)]
+    allp = np.concatenate([x["xyz"] for x in res])
+    ids = np.concatenate([x["ids"] for x in res])
+    pts = np.empty_like(allp)
+    pts[ids] = allp  # global id order
+    gd, gi = oracle.tree(pts, 16, 1.0).query(pts, k, workers=4)
+    assert sum(int(x["v0"]) for x in res) > 0  # the thin halo did leave rows inexact
+    assert sum(int(x["fwd"]) for x in res) == sum(int(x["v0"]) for x in res)
+    if world == 4:
+        assert max(int(x["hops"]) for x in res) >= 2
+    for x in res:
+        assert_knn_equal(x["d"], x["i"], gd[x["ids"]], gi[x["ids"]], pts, x["xyz"], 1.0)
+
+
+def test_merge_rows_dedups_and_pads():
+    f = np.float32
+    a_d = np.array([[0.0, 1.0, 4.0, f(np.finfo(f).max)]], f)
+    a_i = np.array([[5, 7, 9, 0xFFFFFFFF]], np.uint32)
+    b_d = np.array([[1.0, 2.0, 4.0, 9.0]], f)
+    b_i = np.array([[7, 3, 8, 11]], np.uint32)  # 7 is the same particle as in a
+    d, i = slab.merge_rows(a_d, a_i, b_d, b_i, 4)
+    assert d.tolist() == [[0.0, 1.0, 2.0, 4.0]]
+    assert i.tolist() == [[5, 7, 3, 8]]  # equal d2 4.0: the smaller id first
+    d, i = slab.merge_rows(a_d[:, :2], a_i[:, :2], a_d[:, :1], a_i[:, :1], 4)
+    assert i.tolist() == [[5, 7, 0xFFFFFFFF, 0xFFFFFFFF]]
+    assert d[0, 2] == np.finfo(f).max
+
+
+def test_side_needs_matches_violations_host():
+    rng = np.random.default_rng(3)
+    world, rank, box, h = 3, 1, 1.0, 0.02
+    lo, hi = slab.slab_bounds(rank, world, box)
+    x = rng.uniform(lo, hi, 5000).astype(np.float32)
+    q = np.stack([x, x, x], 1)
+    dk = rng.uniform(0, 0.1, 5000).astype(np.float32)
+    f32 = np.float32
+    left, right = slab.side_needs(x, dk, f32(f32(lo) - f32(h)), f32(f32(hi) + f32(h)))
+    assert int((left | right).sum()) == slab.violations_host(q, dk, rank, world, box, h)
