@@ -134,6 +134,43 @@ static void deposit_image(float x, float y, float z, float w, float r, int gx, i
     }
 }
 
+/* per-axis image lists of one ball, augment_vertices_periodic
+ * (rasterization/src/cpp/vertex_utilities.cpp:13-42): for each axis in turn
+ * every vertex made so far gains a copy shifted by -P if x + r > P and one by
+ * +P if x - r < 0, i.e. the cartesian product of these per-axis lists */
+static void images(const float *p3, float r, const float *period, float sh[3][3], int ns[3]) {
+    for (int d = 0; d < 3; ++d) {
+        const float p = p3[d];
+        ns[d] = 1;
+        sh[d][0] = p;
+        if (period[d] > 0.0f) {
+            if (p + r > period[d]) sh[d][ns[d]++] = p - period[d];
+            if (p - r < 0.0f) sh[d][ns[d]++] = p + period[d];
+        }
+    }
+}
+
+/* the periodic images of each ball (test hook): out[27 * i + j] (x, y, z) for
+ * j < counts[i] */
+ORC_API void orc_deposit_images(const float *xyz, const float *radius, int64_t n,
+                                const float *period, float *out, int32_t *counts) {
+    for (int64_t i = 0; i < n; ++i) {
+        float sh[3][3];
+        int ns[3];
+        images(xyz + 3 * i, radius[i], period, sh, ns);
+        int j = 0;
+        for (int a = 0; a < ns[0]; ++a)
+            for (int b = 0; b < ns[1]; ++b)
+                for (int c = 0; c < ns[2]; ++c, ++j) {
+                    float *o = out + 3 * (27 * i + j);
+                    o[0] = sh[0][a];
+                    o[1] = sh[1][b];
+                    o[2] = sh[2][c];
+                }
+        counts[i] = j;
+    }
+}
+
 /*
  * Deposit n particles (xyz row-major (n, 3), weight[n], radius[n]) into
  * grid[gx * gy * nz] (zeroed by the caller; index px + gx * (py + gy * s)).
@@ -150,17 +187,14 @@ ORC_API int orc_deposit(const float *xyz, const float *weight, const float *radi
     orc_deposit_overlap_table(S, tbl);
     for (int64_t i = 0; i < n; ++i) {
         const float r = radius[i], w = weight[i];
+        /* w / (4/3 pi R^3) is 0 for R = inf (and a NaN vertex is not
+         * rasterised): such a ball contributes nothing */
+        if (!isfinite(r) || !isfinite(xyz[3 * i]) || !isfinite(xyz[3 * i + 1]) ||
+            !isfinite(xyz[3 * i + 2]))
+            continue;
         float sh[3][3];
         int ns[3];
-        for (int d = 0; d < 3; ++d) {
-            const float p = xyz[3 * i + d];
-            ns[d] = 1;
-            sh[d][0] = p;
-            if (period[d] > 0.0f) {
-                if (p + r > period[d]) sh[d][ns[d]++] = p - period[d];
-                if (p - r < 0.0f) sh[d][ns[d]++] = p + period[d];
-            }
-        }
+        images(xyz + 3 * i, r, period, sh, ns);
         for (int a = 0; a < ns[0]; ++a)
             for (int b = 0; b < ns[1]; ++b)
                 for (int c = 0; c < ns[2]; ++c)

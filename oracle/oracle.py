@@ -22,6 +22,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 ORC_PATH = os.path.join(HERE, "liborc.so")
 REF_PATH = os.path.join(HERE, "_ref", "libnbkd_ref.so")
+VERTEX_REF_PATH = os.path.join(HERE, "_ref", "libvertex_ref.so")
 
 NODE_DTYPE = np.dtype([("dim", "<i4"), ("split", "<f4"), ("left", "<u4"), ("right", "<u4")])
 
@@ -164,6 +165,20 @@ class Oracle(_Lib):
                                   ctypes.c_int32, ctypes.c_float, _fp, ctypes.c_int32,
                                   ctypes.c_int32, ctypes.POINTER(ctypes.c_double)]
         L.orc_deposit.restype = ctypes.c_int
+        L.orc_deposit_images.argtypes = [_fp, _fp, ctypes.c_int64, _fp, _fp,
+                                         ctypes.POINTER(ctypes.c_int32)]
+
+    def deposit_images(self, xyz, radius, period):
+        """Periodic images of each ball as the restated rasteriser makes them:
+        a list of (k_i, 3) float32 arrays."""
+        p, r = _f32(xyz), _f32(radius)
+        per = np.asarray(period, np.float32)
+        n = p.shape[0]
+        out = np.empty((n, 27, 3), np.float32)
+        cnt = np.empty(n, np.int32)
+        self.lib.orc_deposit_images(_ptr(p, _fp), _ptr(r, _fp), n, _ptr(per, _fp),
+                                    _ptr(out, _fp), cnt.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)))
+        return [out[i, :cnt[i]] for i in range(n)]
 
     def deposit(self, xyz, weight, radius, grid, ppu, period=(-1.0, -1.0, -1.0), subsample=4,
                 mode=0):
@@ -242,6 +257,36 @@ class Reference(_Lib):
 
     def tree(self, points, leafsize=128, boxsize=None):
         return Tree(self, points, leafsize, boxsize)
+
+
+class VertexReference:
+    """The reference rasteriser's own augment_vertices_periodic
+    (rasterization/src/cpp/vertex_utilities.cpp:13-42), compiled from its
+    sources into oracle/_ref/libvertex_ref.so (oracle/Makefile `ref`)."""
+
+    def __init__(self, path=None):
+        path = path or VERTEX_REF_PATH
+        if not os.path.exists(path):
+            if os.path.isdir("/root/reference/rasterization"):
+                subprocess.check_call(["make", "-s", "-C", HERE, "ref"])
+            else:
+                raise FileNotFoundError("oracle/_ref/libvertex_ref.so not built")
+        self.lib = ctypes.CDLL(path)
+        f = self.lib.ref_augment_vertices_periodic
+        f.argtypes = [_fp, _fp, _fp, ctypes.c_int64, _fp, _fp, ctypes.c_int64]
+        f.restype = ctypes.c_int64
+
+    def augment(self, xyz, weight, radius, box):
+        """(m, 5) float32 vertices (x, y, z, weight, radius) after augmentation,
+        in the reference's order."""
+        p, w, r = _f32(xyz), _f32(weight), _f32(radius)
+        b = np.asarray(box, np.float32)
+        n = p.shape[0]
+        cap = 27 * n
+        out = np.empty((cap, 5), np.float32)
+        m = self.lib.ref_augment_vertices_periodic(_ptr(p, _fp), _ptr(w, _fp), _ptr(r, _fp), n,
+                                                   _ptr(b, _fp), _ptr(out, _fp), cap)
+        return out[:m]
 
 
 def reference_available() -> bool:

@@ -178,3 +178,38 @@ def test_rasterizer_argument_errors():
     assert _normalize_period((1.0, 2.0, 3.0), False) == (-1.0, -1.0, -1.0)
     assert _normalize_period((1.0, 2.0, 3.0), 5.0) == (5.0, 5.0, 5.0)
     assert _normalize_period((1.0, 2.0, 3.0), (4.0, 5.0)) == (4.0, 5.0, -1.0)
+
+
+def test_periodic_images_pinned_to_reference_augment():
+    """The deposit oracle's periodic images (and so nbkd_deposit's, which is
+    checked against that oracle) equal the reference's own
+    augment_vertices_periodic (rasterization/src/cpp/vertex_utilities.cpp:13-42,
+    compiled from its sources into oracle/_ref) ball by ball, as multisets:
+    balls straddling one, two or three faces, radii wider than half the box,
+    zero, negative and infinite radii, points exactly on the faces, a
+    non-periodic axis (box <= 0)."""
+    import os
+
+    from oracle.oracle import VERTEX_REF_PATH, Oracle, VertexReference
+
+    if not os.path.exists(VERTEX_REF_PATH) and not os.path.isdir("/root/reference/rasterization"):
+        pytest.skip("oracle/_ref/libvertex_ref.so not built here")
+    ref = VertexReference()
+    orc = Oracle()
+    rng = np.random.default_rng(12)
+    n = 3000
+    for box in ((1.0, 1.0, 1.0), (2.0, 1.5, -1.0), (1.0, -1.0, 0.5)):
+        per = np.asarray(box, np.float32)
+        ext = np.where(per > 0, per, 1.0)
+        xyz = (rng.uniform(-0.05, 1.05, (n, 3)) * ext).astype(np.float32)
+        xyz[:50] = np.where(per > 0, per, 1.0) * rng.integers(0, 2, (50, 3))  # on the faces
+        r = rng.choice(np.array([0.0, 0.01, 0.1, 0.3, 0.7, -0.1, np.inf], np.float32), n)
+        w = np.arange(n, dtype=np.float32)  # the ball index travels as the weight
+        aug = ref.augment(xyz, w, r, box)
+        mine = orc.deposit_images(xyz, r, box)
+        by_ball = [[] for _ in range(n)]
+        for v in aug:
+            by_ball[int(v[3])].append(tuple(v[:3].tolist()))
+        for i in range(n):
+            got = sorted(tuple(x) for x in mine[i].tolist())
+            assert got == sorted(by_ball[i]), (i, xyz[i], r[i])

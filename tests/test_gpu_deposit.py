@@ -146,3 +146,47 @@ def test_knn_smoothing_lengths_feed_the_deposit(gpu, oracle):
     np.testing.assert_array_equal(radii[:500], ref_d[:, -1])
     _close(grid, oracle.deposit(pts, w, radii, (32, 32, 32), 32.0, (1.0, 1.0, 1.0), 4, 0))
     assert abs(float(grid.sum(dtype=np.float64)) - 1.0) < 0.02
+
+
+def test_non_finite_radii_and_centres_contribute_nothing(gpu, oracle):
+    """kth_distance pads with inf when k > n; w / (4/3 pi R^3) is then 0 in the
+    reference's shader, and a NaN vertex is not rasterised: such balls add
+    nothing (and are not expanded into 27 images over the whole grid)."""
+    from nbodyhpc_amd import capi
+    rng = np.random.default_rng(71)
+    grid, ppu = (32, 32, 32), 8.0
+    box = (4.0, 4.0, 4.0)
+    xyz, w, r = _particles(rng, 300, box, [0.05, 0.3, 0.8])
+    r[:40] = np.inf
+    xyz[40:50, 1] = np.nan
+    r[50:60] = np.nan
+    got = capi.deposit(xyz, w, r, grid, ppu, period=box, device=0)
+    keep = np.arange(300) >= 60
+    ref = oracle.deposit(xyz[keep], w[keep], r[keep], grid, ppu, box, 4, 0)
+    _close(got, ref)
+    assert np.all(np.isfinite(got))
+
+
+def test_device_deposits_on_two_streams(gpu, oracle):
+    """Two device-output deposits enqueued back to back on two streams share the
+    device's deposit workspace: the second call waits for the first's kernels
+    (stream-ordered reuse), so both grids equal the oracle's."""
+    from nbodyhpc_amd import capi, hip
+    rng = np.random.default_rng(72)
+    grid, ppu = (48, 48, 48), 6.0
+    box = tuple(np.array(grid) / ppu)
+    sets = [_particles(rng, 3000, box, [0.1, 0.4, 1.0]) for _ in range(2)]
+    streams = [hip.Stream(), hip.Stream()]
+    outs = []
+    keep = []
+    for (xyz, w, r), s in zip(sets, streams):
+        dx, dw, dr = (hip.DeviceArray.from_numpy(a) for a in (xyz, w, r))
+        g = hip.DeviceArray(grid[::-1], np.float32)
+        capi.deposit_device(dx.ptr, dw.ptr, dr.ptr, len(r), grid, ppu, g.ptr, period=box,
+                            device=0, stream=s.handle)
+        outs.append(g)
+        keep.append((dx, dw, dr))
+    hip.synchronize()
+    for (xyz, w, r), g in zip(sets, outs):
+        got = g.numpy().reshape(grid[::-1]).transpose(2, 1, 0)
+        _close(np.asfortranarray(got), oracle.deposit(xyz, w, r, grid, ppu, box, 4, 0))

@@ -467,3 +467,28 @@ def test_build_caches_alternating_sizes_and_threads(gpu, oracle):
     for x in th:
         x.join()
     assert not errors, errors
+
+
+def test_device_queries_on_two_streams(gpu, oracle):
+    """Two device-output queries of one tree on two streams: the tree's scratch
+    is reused, so the second call waits on the device for the first's kernels
+    (Workspace::enter); both results are exact."""
+    from nbodyhpc_amd import hip
+    pts = uniform(200_000, 81)
+    qa, qb = uniform(150_000, 82), uniform(90_000, 83)
+    t = gpu.Tree(pts, leafsize=64, boxsize=1.0)
+    k = 32
+    outs = []
+    keep = []
+    for q, s in ((qa, hip.Stream()), (qb, hip.Stream())):
+        dq = hip.DeviceArray.from_numpy(q)
+        od = hip.DeviceArray((len(q), k), np.float32)
+        oi = hip.DeviceArray((len(q), k), np.uint32)
+        t.query_device(dq.ptr, len(q), k, od.ptr, oi.ptr, s.handle)
+        outs.append((q, od, oi))
+        keep.append((dq, s))
+    hip.synchronize()
+    o = oracle.tree(pts, 64, 1.0)
+    for q, od, oi in outs:
+        dr, ir = o.query(q, k, workers=8)
+        assert_knn_equal(od.numpy(), oi.numpy(), dr, ir, pts, q, 1.0)
