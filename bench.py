@@ -207,6 +207,28 @@ def suite(args, capi, hip, tree, dev_pts, n, k, L, stream, od, oi):
     out["knn_independent_queries"] = {"queries_per_s": n / sec, "ms": sec * 1e3, "k": k,
                                       "queries": n, "query_seed": synth.SEED_QUERIES}
     log(f"suite: independent queries {n / sec:.3e} q/s")
+    # kNN with k = 100 (scipy-style callers): the wave-per-query select path
+    k2 = 100
+    od2 = hip.DeviceArray((n, k2), np.float32)
+    oi2 = hip.DeviceArray((n, k2), np.uint32)
+    tree.query_device(dev_pts.ptr, n, k2, od2.ptr, oi2.ptr, stream.handle)
+    capi.timing_reset()
+    capi.timing_enable(True)
+    sec = timed(lambda: tree.query_device(dev_pts.ptr, n, k2, od2.ptr, oi2.ptr, stream.handle),
+                steps, hip)
+    br = {nm: capi.timing_read(nm)[0] / steps for nm in
+          ("leaf_key", "sort", "knn_collect", "knn_select", "knn_retry", "knn_fallback")}
+    capi.timing_enable(False)
+    out["knn_k100"] = {"queries_per_s": n / sec, "ms": sec * 1e3, "k": k2, "queries": n,
+                       "breakdown_ms": br}
+    if not args.no_parity:
+        rows = min(200_000, n)
+        _, parity = cpu_baseline(dev_pts.numpy_head(n), k2, args.leafsize, L, rows,
+                                 od2.numpy_head(rows), oi2.numpy_head(rows))
+        out["knn_k100"]["parity_vs_cpu"] = parity
+    od2.free()
+    oi2.free()
+    log(f"suite: k=100 {n / sec:.3e} q/s")
     # k-th neighbour distance only (densities / smoothing radii): same search,
     # m floats out instead of the (m, k) rows
     rk = hip.DeviceArray((n,), np.float32)

@@ -26,6 +26,8 @@
 //
 // A query whose ball holds fewer than k points (seed too small) or more than
 // the column capacity is listed for the reference-exact kernel (query.hip).
+#include <algorithm>
+
 #include "internal.hpp"
 #include "metric.hpp"
 #include "packet.hpp"
@@ -866,6 +868,163 @@ knn_select_kernel(DevTree t, const float *__restrict__ q, const uint32_t *__rest
     }
 }
 
+// ---------------------------------------------------------------- k > 64: one wave per query
+// The top-K (K = pow2 >= k, 128..1024) of ONE query spread over the wave's 64
+// lanes: R = K/64 registers per lane, element e = r*64 + lane.  The query's
+// column is read in chunks of K slots (16 consecutive slots are one 128-B
+// line), each chunk bitonic-sorted across the wave (exchanges between
+// registers for strides >= 64, lane shuffles below) and merged into the top-K:
+// min(top[e], chunk[K-1-e]) holds the K smallest of both as a bitonic
+// sequence, which log2(K) half-cleaner stages sort.  A chunk with nothing
+// below the current k-th is skipped.  The rows leave as 64-wide contiguous
+// stores.  Same result rows as the lane-per-query select (the k smallest d2
+// of the column, ascending; ties in any order): find_closest,
+// kdtree/src/cpp/kdtree.cpp:133-159; tournament_tree.hpp:42-105 (any k).
+// compare-exchange of element pairs (e, e ^ STRIDE), ascending where (e & SIZE) == 0
+template <int R, int SIZE, int STRIDE>
+__device__ __forceinline__ void wave_cx(float (&d)[R], uint32_t (&p)[R], int lane) {
+    if constexpr (STRIDE >= 64) {
+        constexpr int rs = STRIDE / 64;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            if (r & rs) continue;
+            const int r2 = r | rs;
+            // e & SIZE for SIZE >= 128 depends on the register only
+            const bool asc = ((r * 64) & SIZE) == 0;
+            const bool sw = asc ? (d[r2] < d[r]) : (d[r2] > d[r]);
+            const float a = d[r], b = d[r2];
+            const uint32_t pa = p[r], pb = p[r2];
+            d[r] = sw ? b : a;
+            d[r2] = sw ? a : b;
+            p[r] = sw ? pb : pa;
+            p[r2] = sw ? pa : pb;
+        }
+    } else {
+        const bool lower = (lane & STRIDE) == 0;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const bool asc = (SIZE >= 128 ? ((r * 64) & SIZE) : (lane & SIZE)) == 0;
+            const float od = __shfl_xor(d[r], STRIDE, 64);
+            const uint32_t op = (uint32_t)__shfl_xor((int)p[r], STRIDE, 64);
+            // equal keys: neither partner takes the other's (the pair stays consistent)
+            const bool take = (lower == asc) ? (od < d[r]) : (od > d[r]);
+            d[r] = take ? od : d[r];
+            p[r] = take ? op : p[r];
+        }
+    }
+}
+
+template <int R, int SIZE, int STRIDE>
+__device__ __forceinline__ void wave_merge_stages(float (&d)[R], uint32_t (&p)[R], int lane) {
+    wave_cx<R, SIZE, STRIDE>(d, p, lane);
+    if constexpr (STRIDE > 1) wave_merge_stages<R, SIZE, STRIDE / 2>(d, p, lane);
+}
+
+template <int R, int SIZE>
+__device__ __forceinline__ void wave_sort_stages(float (&d)[R], uint32_t (&p)[R], int lane) {
+    wave_merge_stages<R, SIZE, SIZE / 2>(d, p, lane);
+    if constexpr (SIZE < 64 * R) wave_sort_stages<R, SIZE * 2>(d, p, lane);
+}
+
+template <int R, bool PER, bool WHOLE>
+__global__ void __launch_bounds__(TB)
+knn_select_wave_kernel(DevTree t, const float *__restrict__ q, const uint32_t *__restrict__ order,
+                       uint32_t m, int k, const uint2 *__restrict__ cand, uint32_t capg,
+                       const uint32_t *__restrict__ ccount, float *__restrict__ out_d,
+                       uint32_t *__restrict__ out_i, uint32_t *__restrict__ fail_list,
+                       uint32_t *__restrict__ fail_count, uint32_t pos_base,
+                       float *__restrict__ tg_fix, float mu, bool sq) {
+    constexpr int K = 64 * R;
+    const int lane = threadIdx.x & 63;
+    const uint32_t nwaves = gridDim.x * WPB;
+    for (uint32_t gq = blockIdx.x * WPB + (threadIdx.x >> 6); gq < m; gq += nwaves) {
+        const uint32_t qo = order[gq];
+        const uint32_t n = ccount[gq];
+        if (!(n >= (uint32_t)k && n <= capg)) {
+            if (lane == 0) {
+                const float qx = q[3 * (size_t)qo], qy = q[3 * (size_t)qo + 1],
+                            qz = q[3 * (size_t)qo + 2];
+                knn_fail_check<PER>(true, true, 0xFFFFFFFFu, qx, qy, qz, t.box,
+                                    pos_base == 0xFFFFFFFFu ? qo : pos_base + gq, fail_list,
+                                    fail_count);
+                if (tg_fix) { // the retry's seed, as knn_select_kernel
+                    float fv;
+                    if (n < (uint32_t)k)
+                        fv = fminf(8.0f, fmaxf(2.0f, 1.5f * mu / fmaxf((float)n, 0.5f)));
+                    else
+                        fv = fminf(1.0f, 4.0f * (float)capg / (float)n);
+                    tg_fix[qo] = fminf(tg_fix[qo] * cbrtf(fv * fv), FLT_MAX);
+                }
+            }
+            continue;
+        }
+        const uint2 *col = WHOLE ? cand + (size_t)(gq >> 6) * 64u * capg : cand + (size_t)gq * capg;
+        const uint32_t row = gq & 63u;
+        float td[R], cd[R];
+        uint32_t tp[R], cp[R];
+        const int kr = (k - 1) >> 6, kl = (k - 1) & 63; // element k-1: register kr, lane kl
+        for (uint32_t c0 = 0; c0 < n; c0 += K) {
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const uint32_t s = c0 + (uint32_t)(r * 64 + lane);
+                if (s < n) {
+                    const uint2 e = WHOLE ? col[((s >> 4) * 64u + row) * 16u + (s & 15u)] : col[s];
+                    cd[r] = __uint_as_float(e.x);
+                    cp[r] = e.y;
+                } else {
+                    cd[r] = INFINITY;
+                    cp[r] = 0xFFFFFFFFu;
+                }
+            }
+            if (c0 > 0) {
+                // nothing below the current k-th: the chunk changes nothing
+                float kth = 0.0f;
+#pragma unroll
+                for (int r = 0; r < R; ++r)
+                    if (r == kr) kth = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(td[r]), kl));
+                bool useful = false;
+#pragma unroll
+                for (int r = 0; r < R; ++r) useful |= cd[r] < kth;
+                if (!__any(useful)) continue;
+            }
+            wave_sort_stages<R, 2>(cd, cp, lane);
+            if (c0 == 0) {
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    td[r] = cd[r];
+                    tp[r] = cp[r];
+                }
+            } else {
+                // K smallest of both: top ascending vs the chunk reversed (a bitonic sequence)
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const float rd = __shfl(cd[R - 1 - r], 63 - lane, 64);
+                    const uint32_t rp = (uint32_t)__shfl((int)cp[R - 1 - r], 63 - lane, 64);
+                    const bool take = rd < td[r];
+                    td[r] = take ? rd : td[r];
+                    tp[r] = take ? rp : tp[r];
+                }
+                wave_merge_stages<R, 2 * K, K / 2>(td, tp, lane);
+            }
+        }
+        if (out_i == nullptr) { // k-th distance only
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+                if (r == kr && lane == kl) out_d[qo] = sq ? td[r] : sqrtf(td[r]);
+            continue;
+        }
+        const size_t base = (size_t)qo * (size_t)k;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int e = r * 64 + lane;
+            if (e < k) {
+                out_d[base + e] = sq ? td[r] : sqrtf(td[r]);
+                out_i[base + e] = tp[r] == 0xFFFFFFFFu ? tp[r] : t.idx[tp[r]];
+            }
+        }
+    }
+}
+
 #ifdef NBKD_EXPERIMENTS
 int dense_min() {
     const char *e = knob("NBKD_DENSE_MIN"); // tuning experiments only
@@ -888,6 +1047,10 @@ void launch_collect(const Tree &t, const float *q, const uint32_t *order, uint32
                     uint32_t *ccount, unsigned long long *stats, bool retry, hipStream_t s) {
     const char *const name = retry ? "knn_retry" : "knn_collect";
     const unsigned blocks = (unsigned)(((uint64_t)m + qpp - 1) / qpp + WPB - 1) / WPB;
+    // the bound histogram's 8-bit bucket counts are exact while the cumulative
+    // count below the k-th's bucket is < 256, i.e. for k <= 255 (a wrapped or
+    // carried byte can only make a larger cumulative count); above, no tightening
+    if (k > 255) k = 0x7FFFFFFF;
     if (t.ginfo && groups_enabled()) {
         // NBKD_XCD_MAP=0: hardware block order (A/B of the XCD-contiguous packet ranges)
         static const bool xcd = [] {
@@ -947,6 +1110,24 @@ void launch_collect(const Tree &t, const float *q, const uint32_t *order, uint32
 #else
     (void)stats;
 #endif
+}
+
+template <int R>
+void launch_select_wave(const Tree &t, const float *q, const uint32_t *order, uint32_t m, int k,
+                        uint32_t qpp, const uint2 *cand, uint32_t capg, const uint32_t *ccount,
+                        float *od, uint32_t *oi, uint32_t *fail_list, uint32_t *fail_count,
+                        uint32_t pos_base, float *tg_fix, float mu, bool sq, hipStream_t s) {
+    const unsigned blocks = (unsigned)std::min<uint64_t>(((uint64_t)m + WPB - 1) / WPB, 32768);
+#define NBKD_SELW(PER, WH)                                                                         \
+    knn_select_wave_kernel<R, PER, WH><<<blocks, TB, 0, s>>>(view(t), q, order, m, k, cand, capg,  \
+                                                            ccount, od, oi, fail_list, fail_count, \
+                                                            pos_base, tg_fix, mu, sq)
+    if (t.periodic) {
+        if (qpp == 64) NBKD_SELW(true, true); else NBKD_SELW(true, false);
+    } else {
+        if (qpp == 64) NBKD_SELW(false, true); else NBKD_SELW(false, false);
+    }
+#undef NBKD_SELW
 }
 
 template <int KC>
@@ -1014,9 +1195,21 @@ nbkd_status launch_knn_collect(const Tree &t, const float *q, const uint32_t *or
         else if (k <= 32)
             launch_select<32>(t, q, order, m, k, qpp, cand, capg, ccount, od, oi, fail_list,
                               fail_count, pos_base, tg_fix, mu, sq, s);
-        else
+        else if (k <= 64)
             launch_select<64>(t, q, order, m, k, qpp, cand, capg, ccount, od, oi, fail_list,
                               fail_count, pos_base, tg_fix, mu, sq, s);
+        else if (k <= 128)
+            launch_select_wave<2>(t, q, order, m, k, qpp, cand, capg, ccount, od, oi, fail_list,
+                                  fail_count, pos_base, tg_fix, mu, sq, s);
+        else if (k <= 256)
+            launch_select_wave<4>(t, q, order, m, k, qpp, cand, capg, ccount, od, oi, fail_list,
+                                  fail_count, pos_base, tg_fix, mu, sq, s);
+        else if (k <= 512)
+            launch_select_wave<8>(t, q, order, m, k, qpp, cand, capg, ccount, od, oi, fail_list,
+                                  fail_count, pos_base, tg_fix, mu, sq, s);
+        else
+            launch_select_wave<16>(t, q, order, m, k, qpp, cand, capg, ccount, od, oi, fail_list,
+                                   fail_count, pos_base, tg_fix, mu, sq, s);
         NBKD_HIP(hipGetLastError());
     }
     return NBKD_OK;

@@ -751,6 +751,10 @@ int key_bits(const Tree &t) {
 // Seed radius (guess_r2) parameters: mu = k + a sqrt(k) + b expected points in
 // the seed sphere, density from the first subtree of <= anchor points on the
 // query's descent.  NBKD_KNN_SEED=0 disables the seed (every bound starts +inf).
+// the collect / select path serves k <= 1024 (knn_select_kernel for k <= 64,
+// knn_select_wave_kernel above); larger k replays the reference per lane
+constexpr int KNN_PACKET_KMAX = 1024;
+
 struct SeedParams {
     bool on;
     float mu_c;
@@ -883,8 +887,8 @@ nbkd_status knn_locked(const Tree &t, const float *q, uint64_t m, int k, float *
     nbkd_status rc = stage_queries(t, q, m, flags, dq, s);
     if (rc) return rc;
     // the collect / select path needs the sub-leaf groups (every non-empty
-    // tree has them); k > 64 and the empty tree take the exact kernel
-    const bool packet = k <= 64 && t.ginfo != nullptr;
+    // tree has them); k > 1024 and the empty tree take the exact kernel
+    const bool packet = k <= KNN_PACKET_KMAX && t.ginfo != nullptr;
     const SeedParams sp = seed_params(t, k);
     float *tg = nullptr;
     if (packet && sp.on) {
@@ -1046,6 +1050,10 @@ nbkd_status knn_locked(const Tree &t, const float *q, uint64_t m, int k, float *
             }
         } else {
 #ifdef NBKD_EXPERIMENTS
+            if (k > 64) {
+                set_error("experiments build: the no-seed packet kernel serves k <= 64 only");
+                return NBKD_EINVAL;
+            }
             TimedScope ts("knn", s);
             launch_knn_packet(t, dq, ord, mm, k, tg, dd, di, list, count, stats, s);
             NBKD_HIP(hipGetLastError());
@@ -1122,7 +1130,7 @@ nbkd_status query_kth(const Tree &t, const float *q, uint64_t m, int k, float *o
     NBKD_HIP(call.err);
     // the collect/select path writes the k-th distance alone; elsewhere the
     // rows go to scratch and column k-1 is copied out
-    if (k <= 64 && t.ginfo && seed_params(t, k).on && !collect_disabled())
+    if (k <= KNN_PACKET_KMAX && t.ginfo && seed_params(t, k).on && !collect_disabled())
         return knn_locked(t, q, m, k, out_d, nullptr, flags, s);
     float *rd = (float *)t.ws.get(WS_KTHD, m * (size_t)k * 4, s);
     uint32_t *ri = (uint32_t *)t.ws.get(WS_KTHI, m * (size_t)k * 4, s);

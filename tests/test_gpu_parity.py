@@ -102,7 +102,8 @@ def test_edge_cases_golden(gpu, golden):
     (10, 16, 4, None), (100, 16, 4, 2.0), (1000, 32, 4, None), (4096, 16, 1, 1.0),
     (10_000, 64, 7, None), (33_333, 16, 16, 1.0), (100_000, 128, 20, None),
     (100_000, 32, 33, 1.0), (250_000, 24, 64, None), (250_000, 200, 5, 3.0),
-    (50_000, 32, 100, 1.0), (20_000, 16, 200, None),
+    (50_000, 32, 100, 1.0), (20_000, 16, 200, None), (30_000, 64, 300, 1.0),
+    (12_000, 32, 700, None), (3_000, 16, 1500, 1.0),
 ])
 def test_knn_vs_oracle(gpu, oracle, n, leaf, k, box):
     pts = uniform(n, n + leaf, L=box or 1.0)
@@ -251,7 +252,7 @@ def test_knn_seed_retry(gpu, oracle, tuning, box):
     q = np.concatenate([pts[:3000], rng.uniform(0, box or 1.0, (2000, 3)).astype(np.float32)])
     t = gpu.Tree(pts, leafsize=32, boxsize=box)
     o = oracle.tree(pts, 32, box)
-    for k in (1, 16, 32, 50):
+    for k in (1, 16, 32, 50, 100, 150):
         d, i = t.query(q, k)
         dr, ir = o.query(q, k)
         assert_knn_equal(d, i, dr, ir, pts, q, box)
