@@ -207,6 +207,28 @@ def suite(args, capi, hip, tree, dev_pts, n, k, L, stream, od, oi):
     out["knn_independent_queries"] = {"queries_per_s": n / sec, "ms": sec * 1e3, "k": k,
                                       "queries": n, "query_seed": synth.SEED_QUERIES}
     log(f"suite: independent queries {n / sec:.3e} q/s")
+    # the same self-queries over a leafsize-128 tree (the reference wrapper's
+    # default, kdtree/src/python/nbodyhpc/kdtree/__init__.py:17): 65..128-point
+    # leaves are staged as two halves with their own tight boxes
+    if args.leafsize != 128:
+        t128 = capi.Tree(n=n, dev_ptr=dev_pts.ptr, leafsize=128, boxsize=L, stream=stream.handle)
+        t128.query_device(dev_pts.ptr, n, k, od.ptr, oi.ptr, stream.handle)
+        capi.timing_reset()
+        capi.timing_enable(True)
+        sec = timed(lambda: t128.query_device(dev_pts.ptr, n, k, od.ptr, oi.ptr, stream.handle),
+                    steps, hip)
+        br = {nm: capi.timing_read(nm)[0] / steps for nm in
+              ("leaf_key", "sort", "knn_collect", "knn_select", "knn_retry")}
+        capi.timing_enable(False)
+        out["knn_leafsize128"] = {"queries_per_s": n / sec, "ms": sec * 1e3, "k": k,
+                                  "queries": n, "breakdown_ms": br}
+        if not args.no_parity:
+            rows = min(1_000_000, n)
+            _, parity = cpu_baseline(dev_pts.numpy_head(n), k, 128, L, rows,
+                                     od.numpy_head(rows), oi.numpy_head(rows))
+            out["knn_leafsize128"]["parity_vs_cpu"] = parity
+        t128.close()
+        log(f"suite: leafsize 128 {n / sec:.3e} q/s")
     # kNN with k = 100 (scipy-style callers): the wave-per-query select path
     k2 = 100
     od2 = hip.DeviceArray((n, k2), np.float32)
