@@ -903,7 +903,8 @@ __device__ __forceinline__ void wave_cx(float (&d)[R], uint32_t (&p)[R], int lan
         const bool lower = (lane & STRIDE) == 0;
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-            const bool asc = (SIZE >= 128 ? ((r * 64) & SIZE) : (lane & SIZE)) == 0;
+            // e & SIZE: from the register bits for SIZE >= 64, from the lane below
+            const bool asc = (SIZE >= 64 ? ((r * 64) & SIZE) : (lane & SIZE)) == 0;
             const float od = __shfl_xor(d[r], STRIDE, 64);
             const uint32_t op = (uint32_t)__shfl_xor((int)p[r], STRIDE, 64);
             // equal keys: neither partner takes the other's (the pair stays consistent)
