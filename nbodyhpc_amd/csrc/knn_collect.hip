@@ -873,15 +873,42 @@ knn_select_kernel(DevTree t, const float *__restrict__ q, const uint32_t *__rest
 // lanes: R = K/64 registers per lane, element e = r*64 + lane.  The query's
 // column is read in chunks of K slots (16 consecutive slots are one 128-B
 // line), each chunk bitonic-sorted across the wave (exchanges between
-// registers for strides >= 64, lane shuffles below) and merged into the top-K:
-// min(top[e], chunk[K-1-e]) holds the K smallest of both as a bitonic
-// sequence, which log2(K) half-cleaner stages sort.  A chunk with nothing
+// registers for strides >= 64, DPP / permlane lane exchanges below) and merged
+// into the top-K: with the chunk sorted descending, min(top[e], chunk[e])
+// holds the K smallest of both as a bitonic sequence, which log2(K)
+// half-cleaner stages sort.  A chunk with nothing
 // below the current k-th is skipped.  The rows leave as 64-wide contiguous
 // stores.  Same result rows as the lane-per-query select (the k smallest d2
 // of the column, ascending; ties in any order): find_closest,
 // kdtree/src/cpp/kdtree.cpp:133-159; tournament_tree.hpp:42-105 (any k).
-// compare-exchange of element pairs (e, e ^ STRIDE), ascending where (e & SIZE) == 0
-template <int R, int SIZE, int STRIDE>
+// the value of lane (lane ^ S), as VALU data movement where gfx950 has it:
+// DPP quad permutes (S = 1, 2), DPP row shifts (S = 4, 8: the lower half of
+// each 2S-group reads lane + S, the upper lane - S), v_permlane32_swap
+// (S = 32: lanes 0-31 of one copy trade places with lanes 32-63 of the
+// other); S = 16 by ds_swizzle (xor within 32-lane groups).  ds_bpermute
+// (__shfl_xor) ran the sort through the LDS crossbar: 196 ms for the k = 100
+// select at 1e8 (r03d).
+template <int S> __device__ __forceinline__ int lane_xor(int x, int lane) {
+    if constexpr (S == 1) {
+        return __builtin_amdgcn_update_dpp(0, x, 0xB1, 0xF, 0xF, true); // quad_perm [1,0,3,2]
+    } else if constexpr (S == 2) {
+        return __builtin_amdgcn_update_dpp(0, x, 0x4E, 0xF, 0xF, true); // quad_perm [2,3,0,1]
+    } else if constexpr (S == 4 || S == 8) {
+        const int up = __builtin_amdgcn_update_dpp(0, x, 0x100 + S, 0xF, 0xF, true); // row_shl:S
+        const int dn = __builtin_amdgcn_update_dpp(0, x, 0x110 + S, 0xF, 0xF, true); // row_shr:S
+        return (lane & S) ? dn : up;
+    } else if constexpr (S == 16) {
+        return __builtin_amdgcn_ds_swizzle(x, 0x401F); // bit mode: and 0x1F, xor 0x10
+    } else {
+        static_assert(S == 32, "lane_xor: stride");
+        const auto pr = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+        return (lane & 32) ? (int)pr[0] : (int)pr[1];
+    }
+}
+
+// compare-exchange of element pairs (e, e ^ STRIDE), ascending where
+// ((e & SIZE) == 0) != DESC
+template <int R, int SIZE, int STRIDE, bool DESC>
 __device__ __forceinline__ void wave_cx(float (&d)[R], uint32_t (&p)[R], int lane) {
     if constexpr (STRIDE >= 64) {
         constexpr int rs = STRIDE / 64;
@@ -890,7 +917,7 @@ __device__ __forceinline__ void wave_cx(float (&d)[R], uint32_t (&p)[R], int lan
             if (r & rs) continue;
             const int r2 = r | rs;
             // e & SIZE for SIZE >= 128 depends on the register only
-            const bool asc = ((r * 64) & SIZE) == 0;
+            const bool asc = ((((r * 64) & SIZE) == 0)) != DESC;
             const bool sw = asc ? (d[r2] < d[r]) : (d[r2] > d[r]);
             const float a = d[r], b = d[r2];
             const uint32_t pa = p[r], pb = p[r2];
@@ -904,9 +931,9 @@ __device__ __forceinline__ void wave_cx(float (&d)[R], uint32_t (&p)[R], int lan
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             // e & SIZE: from the register bits for SIZE >= 64, from the lane below
-            const bool asc = (SIZE >= 64 ? ((r * 64) & SIZE) : (lane & SIZE)) == 0;
-            const float od = __shfl_xor(d[r], STRIDE, 64);
-            const uint32_t op = (uint32_t)__shfl_xor((int)p[r], STRIDE, 64);
+            const bool asc = ((SIZE >= 64 ? ((r * 64) & SIZE) : (lane & SIZE)) == 0) != DESC;
+            const float od = __int_as_float(lane_xor<STRIDE>(__float_as_int(d[r]), lane));
+            const uint32_t op = (uint32_t)lane_xor<STRIDE>((int)p[r], lane);
             // equal keys: neither partner takes the other's (the pair stays consistent)
             const bool take = (lower == asc) ? (od < d[r]) : (od > d[r]);
             d[r] = take ? od : d[r];
@@ -915,16 +942,16 @@ __device__ __forceinline__ void wave_cx(float (&d)[R], uint32_t (&p)[R], int lan
     }
 }
 
-template <int R, int SIZE, int STRIDE>
+template <int R, int SIZE, int STRIDE, bool DESC>
 __device__ __forceinline__ void wave_merge_stages(float (&d)[R], uint32_t (&p)[R], int lane) {
-    wave_cx<R, SIZE, STRIDE>(d, p, lane);
-    if constexpr (STRIDE > 1) wave_merge_stages<R, SIZE, STRIDE / 2>(d, p, lane);
+    wave_cx<R, SIZE, STRIDE, DESC>(d, p, lane);
+    if constexpr (STRIDE > 1) wave_merge_stages<R, SIZE, STRIDE / 2, DESC>(d, p, lane);
 }
 
-template <int R, int SIZE>
+template <int R, int SIZE, bool DESC>
 __device__ __forceinline__ void wave_sort_stages(float (&d)[R], uint32_t (&p)[R], int lane) {
-    wave_merge_stages<R, SIZE, SIZE / 2>(d, p, lane);
-    if constexpr (SIZE < 64 * R) wave_sort_stages<R, SIZE * 2>(d, p, lane);
+    wave_merge_stages<R, SIZE, SIZE / 2, DESC>(d, p, lane);
+    if constexpr (SIZE < 64 * R) wave_sort_stages<R, SIZE * 2, DESC>(d, p, lane);
 }
 
 template <int R, bool PER, bool WHOLE>
@@ -988,24 +1015,24 @@ knn_select_wave_kernel(DevTree t, const float *__restrict__ q, const uint32_t *_
                 for (int r = 0; r < R; ++r) useful |= cd[r] < kth;
                 if (!__any(useful)) continue;
             }
-            wave_sort_stages<R, 2>(cd, cp, lane);
             if (c0 == 0) {
+                wave_sort_stages<R, 2, false>(cd, cp, lane);
 #pragma unroll
                 for (int r = 0; r < R; ++r) {
                     td[r] = cd[r];
                     tp[r] = cp[r];
                 }
             } else {
-                // K smallest of both: top ascending vs the chunk reversed (a bitonic sequence)
+                // the chunk sorted DESCENDING: min(top[e], chunk[e]) holds the K
+                // smallest of both as a bitonic sequence
+                wave_sort_stages<R, 2, true>(cd, cp, lane);
 #pragma unroll
                 for (int r = 0; r < R; ++r) {
-                    const float rd = __shfl(cd[R - 1 - r], 63 - lane, 64);
-                    const uint32_t rp = (uint32_t)__shfl((int)cp[R - 1 - r], 63 - lane, 64);
-                    const bool take = rd < td[r];
-                    td[r] = take ? rd : td[r];
-                    tp[r] = take ? rp : tp[r];
+                    const bool take = cd[r] < td[r];
+                    td[r] = take ? cd[r] : td[r];
+                    tp[r] = take ? cp[r] : tp[r];
                 }
-                wave_merge_stages<R, 2 * K, K / 2>(td, tp, lane);
+                wave_merge_stages<R, 2 * K, K / 2, false>(td, tp, lane);
             }
         }
         if (out_i == nullptr) { // k-th distance only
