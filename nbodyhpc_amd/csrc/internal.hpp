@@ -19,7 +19,7 @@ namespace nbkd {
 enum WsSlot {
     WS_Q = 0, WS_KEYS, WS_KEYS2, WS_ORDER, WS_TMP, WS_HIST, WS_SUMS, WS_OUTD, WS_OUTI,
     WS_COUNT, WS_OFF, WS_IDX, WS_STATS, WS_LIST, WS_LT, WS_TG, WS_CAND, WS_CCOUNT,
-    WS_LIST2, WS_RSORT, WS_KTHD, WS_KTHI, WS_NSLOTS
+    WS_LIST2, WS_RSORT, WS_KTHD, WS_KTHI, WS_KB, WS_NSLOTS
 };
 struct Workspace {
     std::mutex mu;
@@ -208,8 +208,8 @@ nbkd_status launch_knn_collect(const Tree &t, const float *q, const uint32_t *or
                                int k, const float *tg, float seed_mul, uint32_t qpp, uint2 *cand,
                                uint32_t capg, uint32_t *ccount, float *od, uint32_t *oi,
                                uint32_t *fail_list, uint32_t *fail_count, uint32_t pos_base,
-                               bool retry, bool fix_seed, bool sq, unsigned long long *stats,
-                               hipStream_t s);
+                               bool retry, bool fix_seed, bool sq, float *kb,
+                               unsigned long long *stats, hipStream_t s);
 
 // ball.hip: radius count (out_idx == nullptr) or CSR fill over m kd-ordered
 // queries (periodic queries outside [0, L]^3 are skipped: query.hip answers them)

@@ -477,7 +477,7 @@ __device__ __forceinline__ void grp_packet(const DevTree &t, const float *__rest
                                            const uint32_t *__restrict__ linfo,
                                            const float *__restrict__ hinfo,
                                            CollectLdsG &W, const int lane, const float qx,
-                                           const float qy, const float qz, float kth,
+                                           const float qy, const float qz, float &kth,
                                            const float s_over_nb, const float nb_over_s,
                                            uint2 *__restrict__ col, const uint32_t qpp,
                                            const uint32_t capg, const int kq, uint32_t &cnt,
@@ -662,7 +662,7 @@ knn_collect_grp_kernel(DevTree t, const float *__restrict__ ginfo,
                        const float *__restrict__ tg, float seed_mul, uint32_t qpp,
                        uint2 *__restrict__ cand, uint32_t capg,
                        uint32_t *__restrict__ ccount, unsigned long long *__restrict__ stats,
-                       bool xcd) {
+                       bool xcd, float *__restrict__ kbound) {
     __shared__ CollectLdsG Wl[WPB];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     CollectLdsG &W = Wl[wave];
@@ -683,9 +683,13 @@ knn_collect_grp_kernel(DevTree t, const float *__restrict__ ginfo,
     uint2 *const col = cand + (size_t)pk * qpp * capg;
     uint32_t cnt = 0;
     uint64_t st[13] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-    grp_packet<PER, PER, STATS>(t, ginfo, linfo, hinfo, W, lane, qx, qy, qz, seed, s_over_nb, nb_over_s,
+    float kth = seed;
+    grp_packet<PER, PER, STATS>(t, ginfo, linfo, hinfo, W, lane, qx, qy, qz, kth, s_over_nb, nb_over_s,
                                 col, qpp, capg, kq, cnt, st);
     if (valid) ccount[gq] = cnt;
+    // the final bound: at least k candidates lie strictly below it (bound
+    // histogram), so none at or above it is among the k smallest
+    if (valid && kbound) kbound[gq] = kth;
     if (STATS && lane == 0) {
         atomicAdd(&stats[0], (unsigned long long)st[0]);
         atomicAdd(&stats[1], (unsigned long long)st[5]);
@@ -961,9 +965,13 @@ knn_select_wave_kernel(DevTree t, const float *__restrict__ q, const uint32_t *_
                        const uint32_t *__restrict__ ccount, float *__restrict__ out_d,
                        uint32_t *__restrict__ out_i, uint32_t *__restrict__ fail_list,
                        uint32_t *__restrict__ fail_count, uint32_t pos_base,
-                       float *__restrict__ tg_fix, float mu, bool sq) {
+                       float *__restrict__ tg_fix, float mu, bool sq,
+                       const float *__restrict__ kbound) {
     constexpr int K = 64 * R;
+    // per wave: the query's candidates below its final bound, compacted
+    __shared__ uint2 cl_all[WPB][2 * K];
     const int lane = threadIdx.x & 63;
+    uint2 *const cl = cl_all[threadIdx.x >> 6];
     const uint32_t nwaves = gridDim.x * WPB;
     for (uint32_t gq = blockIdx.x * WPB + (threadIdx.x >> 6); gq < m; gq += nwaves) {
         const uint32_t qo = order[gq];
@@ -988,43 +996,48 @@ knn_select_wave_kernel(DevTree t, const float *__restrict__ q, const uint32_t *_
         }
         const uint2 *col = WHOLE ? cand + (size_t)(gq >> 6) * 64u * capg : cand + (size_t)gq * capg;
         const uint32_t row = gq & 63u;
+        // at least k candidates lie strictly below the collect kernel's final
+        // bound, so the k smallest are all below it
+        const float bnd = kbound ? kbound[gq] : INFINITY;
         float td[R], cd[R];
         uint32_t tp[R], cp[R];
         const int kr = (k - 1) >> 6, kl = (k - 1) & 63; // element k-1: register kr, lane kl
-        for (uint32_t c0 = 0; c0 < n; c0 += K) {
+        if (n <= (uint32_t)(2 * K)) {
+            // one pass: all 2K slots loaded at once, the candidates below the
+            // bound compacted into LDS (typically k + a bucket's worth), then
+            // one sort of K (or a sort + merge when more than K survive)
+            uint2 e[2 * R];
+#pragma unroll
+            for (int j = 0; j < 2 * R; ++j) {
+                const uint32_t sl = (uint32_t)(j * 64 + lane);
+                e[j] = sl < n ? (WHOLE ? col[((sl >> 4) * 64u + row) * 16u + (sl & 15u)] : col[sl])
+                              : make_uint2(0x7F800000u, 0xFFFFFFFFu);
+            }
+            uint32_t c = 0;
+#pragma unroll
+            for (int j = 0; j < 2 * R; ++j) {
+                const bool v = __uint_as_float(e[j].x) < bnd;
+                const uint64_t bal = __ballot(v);
+                if (v) cl[c + mbcnt64(bal)] = e[j];
+                c += (uint32_t)__popcll(bal);
+            }
+            wave_sync();
 #pragma unroll
             for (int r = 0; r < R; ++r) {
-                const uint32_t s = c0 + (uint32_t)(r * 64 + lane);
-                if (s < n) {
-                    const uint2 e = WHOLE ? col[((s >> 4) * 64u + row) * 16u + (s & 15u)] : col[s];
-                    cd[r] = __uint_as_float(e.x);
-                    cp[r] = e.y;
-                } else {
-                    cd[r] = INFINITY;
-                    cp[r] = 0xFFFFFFFFu;
-                }
+                const uint32_t x = (uint32_t)(r * 64 + lane);
+                const uint2 v = x < c ? cl[x] : make_uint2(0x7F800000u, 0xFFFFFFFFu);
+                td[r] = __uint_as_float(v.x);
+                tp[r] = v.y;
             }
-            if (c0 > 0) {
-                // nothing below the current k-th: the chunk changes nothing
-                float kth = 0.0f;
-#pragma unroll
-                for (int r = 0; r < R; ++r)
-                    if (r == kr) kth = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(td[r]), kl));
-                bool useful = false;
-#pragma unroll
-                for (int r = 0; r < R; ++r) useful |= cd[r] < kth;
-                if (!__any(useful)) continue;
-            }
-            if (c0 == 0) {
-                wave_sort_stages<R, 2, false>(cd, cp, lane);
+            wave_sort_stages<R, 2, false>(td, tp, lane);
+            if (c > (uint32_t)K) {
 #pragma unroll
                 for (int r = 0; r < R; ++r) {
-                    td[r] = cd[r];
-                    tp[r] = cp[r];
+                    const uint32_t x = (uint32_t)(K + r * 64 + lane);
+                    const uint2 v = x < c ? cl[x] : make_uint2(0x7F800000u, 0xFFFFFFFFu);
+                    cd[r] = __uint_as_float(v.x);
+                    cp[r] = v.y;
                 }
-            } else {
-                // the chunk sorted DESCENDING: min(top[e], chunk[e]) holds the K
-                // smallest of both as a bitonic sequence
                 wave_sort_stages<R, 2, true>(cd, cp, lane);
 #pragma unroll
                 for (int r = 0; r < R; ++r) {
@@ -1033,6 +1046,51 @@ knn_select_wave_kernel(DevTree t, const float *__restrict__ q, const uint32_t *_
                     tp[r] = take ? cp[r] : tp[r];
                 }
                 wave_merge_stages<R, 2 * K, K / 2, false>(td, tp, lane);
+            }
+            wave_sync(); // the LDS reads are done before the next query's writes
+        } else {
+            // long columns (retry rounds): chunks of K from global memory
+            for (uint32_t c0 = 0; c0 < n; c0 += K) {
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const uint32_t sl = c0 + (uint32_t)(r * 64 + lane);
+                    const uint2 e = sl < n ? (WHOLE ? col[((sl >> 4) * 64u + row) * 16u + (sl & 15u)]
+                                                    : col[sl])
+                                           : make_uint2(0x7F800000u, 0xFFFFFFFFu);
+                    const float d = __uint_as_float(e.x);
+                    cd[r] = d < bnd ? d : INFINITY;
+                    cp[r] = d < bnd ? e.y : 0xFFFFFFFFu;
+                }
+                if (c0 > 0) {
+                    // nothing below the current k-th: the chunk changes nothing
+                    float kth = 0.0f;
+#pragma unroll
+                    for (int r = 0; r < R; ++r)
+                        if (r == kr) kth = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(td[r]), kl));
+                    bool useful = false;
+#pragma unroll
+                    for (int r = 0; r < R; ++r) useful |= cd[r] < kth;
+                    if (!__any(useful)) continue;
+                }
+                if (c0 == 0) {
+                    wave_sort_stages<R, 2, false>(cd, cp, lane);
+#pragma unroll
+                    for (int r = 0; r < R; ++r) {
+                        td[r] = cd[r];
+                        tp[r] = cp[r];
+                    }
+                } else {
+                    // the chunk sorted DESCENDING: min(top[e], chunk[e]) holds the K
+                    // smallest of both as a bitonic sequence
+                    wave_sort_stages<R, 2, true>(cd, cp, lane);
+#pragma unroll
+                    for (int r = 0; r < R; ++r) {
+                        const bool take = cd[r] < td[r];
+                        td[r] = take ? cd[r] : td[r];
+                        tp[r] = take ? cp[r] : tp[r];
+                    }
+                    wave_merge_stages<R, 2 * K, K / 2, false>(td, tp, lane);
+                }
             }
         }
         if (out_i == nullptr) { // k-th distance only
@@ -1072,7 +1130,8 @@ bool groups_enabled() {
 template <bool PER>
 void launch_collect(const Tree &t, const float *q, const uint32_t *order, uint32_t m, int k,
                     const float *tg, float seed_mul, uint32_t qpp, uint2 *cand, uint32_t capg,
-                    uint32_t *ccount, unsigned long long *stats, bool retry, hipStream_t s) {
+                    uint32_t *ccount, unsigned long long *stats, bool retry, float *kbound,
+                    hipStream_t s) {
     const char *const name = retry ? "knn_retry" : "knn_collect";
     const unsigned blocks = (unsigned)(((uint64_t)m + qpp - 1) / qpp + WPB - 1) / WPB;
     // the bound histogram's 8-bit bucket counts are exact while the cumulative
@@ -1089,11 +1148,11 @@ void launch_collect(const Tree &t, const float *q, const uint32_t *order, uint32
         if (stats)
             knn_collect_grp_kernel<PER, 8, true><<<blocks, TB, 0, s>>>(
                 view(t), t.ginfo, t.leafinfo, t.hinfo, q, order, m, k, tg, seed_mul, qpp, cand, capg,
-                ccount, stats, xcd);
+                ccount, stats, xcd, kbound);
         else
             knn_collect_grp_kernel<PER, 8, false><<<blocks, TB, 0, s>>>(
                 view(t), t.ginfo, t.leafinfo, t.hinfo, q, order, m, k, tg, seed_mul, qpp, cand, capg,
-                ccount, nullptr, xcd);
+                ccount, nullptr, xcd, kbound);
         return;
     }
 #ifdef NBKD_EXPERIMENTS
@@ -1144,12 +1203,13 @@ template <int R>
 void launch_select_wave(const Tree &t, const float *q, const uint32_t *order, uint32_t m, int k,
                         uint32_t qpp, const uint2 *cand, uint32_t capg, const uint32_t *ccount,
                         float *od, uint32_t *oi, uint32_t *fail_list, uint32_t *fail_count,
-                        uint32_t pos_base, float *tg_fix, float mu, bool sq, hipStream_t s) {
+                        uint32_t pos_base, float *tg_fix, float mu, bool sq, const float *kbound,
+                        hipStream_t s) {
     const unsigned blocks = (unsigned)std::min<uint64_t>(((uint64_t)m + WPB - 1) / WPB, 32768);
 #define NBKD_SELW(PER, WH)                                                                         \
     knn_select_wave_kernel<R, PER, WH><<<blocks, TB, 0, s>>>(view(t), q, order, m, k, cand, capg,  \
                                                             ccount, od, oi, fail_list, fail_count, \
-                                                            pos_base, tg_fix, mu, sq)
+                                                            pos_base, tg_fix, mu, sq, kbound)
     if (t.periodic) {
         if (qpp == 64) NBKD_SELW(true, true); else NBKD_SELW(true, false);
     } else {
@@ -1202,15 +1262,17 @@ nbkd_status launch_knn_collect(const Tree &t, const float *q, const uint32_t *or
                                int k, const float *tg, float seed_mul, uint32_t qpp, uint2 *cand,
                                uint32_t capg, uint32_t *ccount, float *od, uint32_t *oi,
                                uint32_t *fail_list, uint32_t *fail_count, uint32_t pos_base,
-                               bool retry, bool fix_seed, bool sq, unsigned long long *stats,
-                               hipStream_t s) {
+                               bool retry, bool fix_seed, bool sq, float *kb,
+                               unsigned long long *stats, hipStream_t s) {
     if (m == 0) return NBKD_OK;
+    // k > 64: the collect kernel hands each query's final bound to the wave select
+    float *kbound = k > 64 ? kb : nullptr;
     if (t.periodic)
         launch_collect<true>(t, q, order, m, k, tg, seed_mul, qpp, cand, capg, ccount, stats,
-                             retry, s);
+                             retry, kbound, s);
     else
         launch_collect<false>(t, q, order, m, k, tg, seed_mul, qpp, cand, capg, ccount, stats,
-                              retry, s);
+                              retry, kbound, s);
     NBKD_HIP(hipGetLastError());
     {
         TimedScope ts(retry ? "knn_retry" : "knn_select", s);
@@ -1228,16 +1290,16 @@ nbkd_status launch_knn_collect(const Tree &t, const float *q, const uint32_t *or
                               fail_count, pos_base, tg_fix, mu, sq, s);
         else if (k <= 128)
             launch_select_wave<2>(t, q, order, m, k, qpp, cand, capg, ccount, od, oi, fail_list,
-                                  fail_count, pos_base, tg_fix, mu, sq, s);
+                                  fail_count, pos_base, tg_fix, mu, sq, kbound, s);
         else if (k <= 256)
             launch_select_wave<4>(t, q, order, m, k, qpp, cand, capg, ccount, od, oi, fail_list,
-                                  fail_count, pos_base, tg_fix, mu, sq, s);
+                                  fail_count, pos_base, tg_fix, mu, sq, kbound, s);
         else if (k <= 512)
             launch_select_wave<8>(t, q, order, m, k, qpp, cand, capg, ccount, od, oi, fail_list,
-                                  fail_count, pos_base, tg_fix, mu, sq, s);
+                                  fail_count, pos_base, tg_fix, mu, sq, kbound, s);
         else
             launch_select_wave<16>(t, q, order, m, k, qpp, cand, capg, ccount, od, oi, fail_list,
-                                   fail_count, pos_base, tg_fix, mu, sq, s);
+                                   fail_count, pos_base, tg_fix, mu, sq, kbound, s);
         NBKD_HIP(hipGetLastError());
     }
     return NBKD_OK;

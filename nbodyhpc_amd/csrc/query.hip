@@ -951,6 +951,13 @@ nbkd_status knn_locked(const Tree &t, const float *q, uint64_t m, int k, float *
             batch = std::min<uint64_t>(batch, ((uint64_t)mm + 63) / 64 * 64);
             uint2 *cand = (uint2 *)t.ws.get(WS_CAND, batch * capg * 8u, s);
             uint32_t *ccount = (uint32_t *)t.ws.get(WS_CCOUNT, batch * 4u, s);
+            // k > 64: per-query final bounds, collect -> wave select (any batch
+            // of any round holds at most max(batch, mm) queries)
+            float *kb = nullptr;
+            if (k > 64) {
+                kb = (float *)t.ws.get(WS_KB, std::max<uint64_t>(batch, (uint64_t)mm) * 4u, s);
+                if (!kb) return NBKD_ENOMEM;
+            }
             // seed failures (fewer than k points in the seed ball, or more than
             // the column holds) are retried with a 4x seed (2x radius): listed
             // by sorted position, put back in kd order, and walked as packets
@@ -966,7 +973,7 @@ nbkd_status knn_locked(const Tree &t, const float *q, uint64_t m, int k, float *
                     const uint32_t nb = (uint32_t)std::min<uint64_t>(batch, mm - b0);
                     rc = launch_knn_collect(t, dq, ord + b0, nb, k, tg, 1.0f, 64u, cand, capg,
                                             ccount, dd, di, rlist, rcount, (uint32_t)b0, false,
-                                            retry_adaptive(), sq, stats, s);
+                                            retry_adaptive(), sq, kb, stats, s);
                     if (rc) return rc;
                 }
             }
@@ -1020,7 +1027,7 @@ nbkd_status knn_locked(const Tree &t, const float *q, uint64_t m, int k, float *
                     rc = launch_knn_collect(t, dq, rq + b0, nb, k, tg, second ? 1.0f : 4.0f,
                                             rqpp, rcand, capr, rcc, dd, di,
                                             second ? rlist : list, second ? rcount : count,
-                                            0xFFFFFFFFu, true, second, sq, nullptr, s);
+                                            0xFFFFFFFFu, true, second, sq, kb, nullptr, s);
                     if (rc) return rc;
                 }
                 uint32_t nr2 = 0;
@@ -1043,7 +1050,7 @@ nbkd_status knn_locked(const Tree &t, const float *q, uint64_t m, int k, float *
                         const uint32_t nb = (uint32_t)std::min<uint64_t>(rb2, nr2 - b0);
                         rc = launch_knn_collect(t, dq, rlist + b0, nb, k, tg, 1.0f, 1u, rcand2,
                                                 capr2, rcc2, dd, di, list, count, 0xFFFFFFFFu,
-                                                true, false, sq, nullptr, s);
+                                                true, false, sq, kb, nullptr, s);
                         if (rc) return rc;
                     }
                 }
