@@ -973,9 +973,35 @@ knn_select_wave_kernel(DevTree t, const float *__restrict__ q, const uint32_t *_
     const int lane = threadIdx.x & 63;
     uint2 *const cl = cl_all[threadIdx.x >> 6];
     const uint32_t nwaves = gridDim.x * WPB;
-    for (uint32_t gq = blockIdx.x * WPB + (threadIdx.x >> 6); gq < m; gq += nwaves) {
-        const uint32_t qo = order[gq];
-        const uint32_t n = ccount[gq];
+    // software pipeline: the next query's count, bound and first 2K slots are
+    // loaded before this query is sorted (their addresses depend on gq only;
+    // slots past the column are clamped to its last slot and masked by n)
+    auto slot_ptr = [&](uint32_t g, uint32_t sl) {
+        const uint32_t c = min(sl, capg - 1u);
+        return WHOLE ? cand + (size_t)(g >> 6) * 64u * capg + ((c >> 4) * 64u + (g & 63u)) * 16u + (c & 15u)
+                     : cand + (size_t)g * capg + c;
+    };
+    uint32_t gq = blockIdx.x * WPB + (threadIdx.x >> 6);
+    uint32_t n_nx = 0, qo_nx = 0;
+    float b_nx = INFINITY;
+    uint2 e_nx[2 * R];
+    auto prefetch = [&](uint32_t g) {
+        if (g >= m) return;
+        n_nx = ccount[g];
+        qo_nx = order[g];
+        b_nx = kbound ? kbound[g] : INFINITY;
+#pragma unroll
+        for (int j = 0; j < 2 * R; ++j) e_nx[j] = *slot_ptr(g, (uint32_t)(j * 64 + lane));
+    };
+    prefetch(gq);
+    for (; gq < m; gq += nwaves) {
+        const uint32_t qo = qo_nx;
+        const uint32_t n = n_nx;
+        const float bnd = b_nx;
+        uint2 e[2 * R];
+#pragma unroll
+        for (int j = 0; j < 2 * R; ++j) e[j] = e_nx[j];
+        prefetch(gq + nwaves);
         if (!(n >= (uint32_t)k && n <= capg)) {
             if (lane == 0) {
                 const float qx = q[3 * (size_t)qo], qy = q[3 * (size_t)qo + 1],
@@ -997,8 +1023,7 @@ knn_select_wave_kernel(DevTree t, const float *__restrict__ q, const uint32_t *_
         const uint2 *col = WHOLE ? cand + (size_t)(gq >> 6) * 64u * capg : cand + (size_t)gq * capg;
         const uint32_t row = gq & 63u;
         // at least k candidates lie strictly below the collect kernel's final
-        // bound, so the k smallest are all below it
-        const float bnd = kbound ? kbound[gq] : INFINITY;
+        // bound (bnd), so the k smallest are all below it
         float td[R], cd[R];
         uint32_t tp[R], cp[R];
         const int kr = (k - 1) >> 6, kl = (k - 1) & 63; // element k-1: register kr, lane kl
@@ -1006,17 +1031,10 @@ knn_select_wave_kernel(DevTree t, const float *__restrict__ q, const uint32_t *_
             // one pass: all 2K slots loaded at once, the candidates below the
             // bound compacted into LDS (typically k + a bucket's worth), then
             // one sort of K (or a sort + merge when more than K survive)
-            uint2 e[2 * R];
-#pragma unroll
-            for (int j = 0; j < 2 * R; ++j) {
-                const uint32_t sl = (uint32_t)(j * 64 + lane);
-                e[j] = sl < n ? (WHOLE ? col[((sl >> 4) * 64u + row) * 16u + (sl & 15u)] : col[sl])
-                              : make_uint2(0x7F800000u, 0xFFFFFFFFu);
-            }
             uint32_t c = 0;
 #pragma unroll
             for (int j = 0; j < 2 * R; ++j) {
-                const bool v = __uint_as_float(e[j].x) < bnd;
+                const bool v = (uint32_t)(j * 64 + lane) < n && __uint_as_float(e[j].x) < bnd;
                 const uint64_t bal = __ballot(v);
                 if (v) cl[c + mbcnt64(bal)] = e[j];
                 c += (uint32_t)__popcll(bal);
