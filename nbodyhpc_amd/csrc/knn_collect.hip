@@ -885,33 +885,47 @@ knn_select_kernel(DevTree t, const float *__restrict__ q, const uint32_t *__rest
 // stores.  Same result rows as the lane-per-query select (the k smallest d2
 // of the column, ascending; ties in any order): find_closest,
 // kdtree/src/cpp/kdtree.cpp:133-159; tournament_tree.hpp:42-105 (any k).
+// the lanes l with (l & b) == 0, as an exec-style mask (compile time)
+constexpr uint64_t lanes_bit_clear(int b) {
+    uint64_t m = 0;
+    for (int l = 0; l < 64; ++l)
+        if ((l & b) == 0) m |= 1ull << l;
+    return m;
+}
+
 // the value of lane (lane ^ S), as VALU data movement where gfx950 has it:
-// DPP quad permutes (S = 1, 2), DPP row shifts (S = 4, 8: the lower half of
-// each 2S-group reads lane + S, the upper lane - S), v_permlane32_swap
-// (S = 32: lanes 0-31 of one copy trade places with lanes 32-63 of the
-// other); S = 16 by ds_swizzle (xor within 32-lane groups).  ds_bpermute
-// (__shfl_xor) ran the sort through the LDS crossbar: 196 ms for the k = 100
-// select at 1e8 (r03d).
-template <int S> __device__ __forceinline__ int lane_xor(int x, int lane) {
+// DPP quad permutes (S = 1, 2); two DPP row shifts whose bank masks pick the
+// lanes each serves (S = 4, 8: the lower half of every 2S-lane group reads
+// lane + S, the upper half lane - S); v_permlane32_swap (S = 32: lanes 0-31 of
+// one copy trade places with lanes 32-63 of the other); S = 16 by ds_swizzle
+// (xor within 32-lane groups).  ds_bpermute (__shfl_xor) ran the k = 100
+// select through the LDS crossbar: 196 ms at 1e8 (r03d).
+template <int S> __device__ __forceinline__ int lane_xor(int x) {
     if constexpr (S == 1) {
         return __builtin_amdgcn_update_dpp(0, x, 0xB1, 0xF, 0xF, true); // quad_perm [1,0,3,2]
     } else if constexpr (S == 2) {
         return __builtin_amdgcn_update_dpp(0, x, 0x4E, 0xF, 0xF, true); // quad_perm [2,3,0,1]
-    } else if constexpr (S == 4 || S == 8) {
-        const int up = __builtin_amdgcn_update_dpp(0, x, 0x100 + S, 0xF, 0xF, true); // row_shl:S
-        const int dn = __builtin_amdgcn_update_dpp(0, x, 0x110 + S, 0xF, 0xF, true); // row_shr:S
-        return (lane & S) ? dn : up;
+    } else if constexpr (S == 4) {
+        // banks (4-lane groups of a 16-lane row) 0, 2 read lane + 4; 1, 3 lane - 4
+        const int t = __builtin_amdgcn_update_dpp(x, x, 0x104, 0xF, 0x5, false); // row_shl:4
+        return __builtin_amdgcn_update_dpp(t, x, 0x114, 0xF, 0xA, false);        // row_shr:4
+    } else if constexpr (S == 8) {
+        const int t = __builtin_amdgcn_update_dpp(x, x, 0x108, 0xF, 0x3, false); // row_shl:8
+        return __builtin_amdgcn_update_dpp(t, x, 0x118, 0xF, 0xC, false);        // row_shr:8
     } else if constexpr (S == 16) {
         return __builtin_amdgcn_ds_swizzle(x, 0x401F); // bit mode: and 0x1F, xor 0x10
     } else {
         static_assert(S == 32, "lane_xor: stride");
         const auto pr = __builtin_amdgcn_permlane32_swap(x, x, false, false);
-        return (lane & 32) ? (int)pr[0] : (int)pr[1];
+        return (int)lane_set((uint32_t)pr[1], (uint32_t)pr[0], ~lanes_bit_clear(32));
     }
 }
 
 // compare-exchange of element pairs (e, e ^ STRIDE), ascending where
-// ((e & SIZE) == 0) != DESC
+// ((e & SIZE) == 0) != DESC.  A lane keeps its partner's value iff
+// (lower == ascending) ? partner < own : partner > own; that choice is a
+// compile-time lane mask M, so take = (M & lt) | (~M & gt) is scalar work on
+// the two compare masks (equal keys: neither partner takes the other's)
 template <int R, int SIZE, int STRIDE, bool DESC>
 __device__ __forceinline__ void wave_cx(float (&d)[R], uint32_t (&p)[R], int lane) {
     if constexpr (STRIDE >= 64) {
@@ -931,19 +945,29 @@ __device__ __forceinline__ void wave_cx(float (&d)[R], uint32_t (&p)[R], int lan
             p[r2] = sw ? pa : pb;
         }
     } else {
-        const bool lower = (lane & STRIDE) == 0;
+        constexpr uint64_t lower = lanes_bit_clear(STRIDE);
+        float od[R];
+        uint32_t op[R];
+        // every exchange of the stage first: the DPP reads of a register then
+        // sit several instructions after its last write (fewer hazard nops)
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-            // e & SIZE: from the register bits for SIZE >= 64, from the lane below
-            const bool asc = ((SIZE >= 64 ? ((r * 64) & SIZE) : (lane & SIZE)) == 0) != DESC;
-            const float od = __int_as_float(lane_xor<STRIDE>(__float_as_int(d[r]), lane));
-            const uint32_t op = (uint32_t)lane_xor<STRIDE>((int)p[r], lane);
-            // equal keys: neither partner takes the other's (the pair stays consistent)
-            const bool take = (lower == asc) ? (od < d[r]) : (od > d[r]);
-            d[r] = take ? od : d[r];
-            p[r] = take ? op : p[r];
+            od[r] = __int_as_float(lane_xor<STRIDE>(__float_as_int(d[r])));
+            op[r] = (uint32_t)lane_xor<STRIDE>((int)p[r]);
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            constexpr uint64_t ones = ~0ull;
+            const uint64_t asc_m = SIZE >= 64 ? ((((r * 64) & SIZE) == 0) ? ones : 0ull)
+                                              : lanes_bit_clear(SIZE);
+            const uint64_t M = ~(lower ^ (DESC ? ~asc_m : asc_m)); // lower == ascending
+            const uint64_t lt = __ballot(od[r] < d[r]), gt = __ballot(od[r] > d[r]);
+            const uint64_t take = (M & lt) | (~M & gt);
+            d[r] = lane_set(d[r], od[r], take);
+            p[r] = lane_set(p[r], op[r], take);
         }
     }
+    (void)lane;
 }
 
 template <int R, int SIZE, int STRIDE, bool DESC>
