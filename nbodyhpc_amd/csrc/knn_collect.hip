@@ -1018,6 +1018,8 @@ knn_select_wave_kernel(DevTree t, const float *__restrict__ q, const uint32_t *_
         for (int j = 0; j < 2 * R; ++j) e_nx[j] = *slot_ptr(g, (uint32_t)(j * 64 + lane));
     };
     prefetch(gq);
+    uint32_t pend_q = 0xFFFFFFFFu; // the query whose ids are still to be stored
+    uint32_t pend_i[R];
     for (; gq < m; gq += nwaves) {
         const uint32_t qo = qo_nx;
         const uint32_t n = n_nx;
@@ -1142,14 +1144,28 @@ knn_select_wave_kernel(DevTree t, const float *__restrict__ q, const uint32_t *_
             continue;
         }
         const size_t base = (size_t)qo * (size_t)k;
+        // the original ids are gathered now and stored one query later, so the
+        // gathers' latency overlaps the next query's sort
+        uint32_t gi[R];
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             const int e = r * 64 + lane;
-            if (e < k) {
-                out_d[base + e] = sq ? td[r] : sqrtf(td[r]);
-                out_i[base + e] = tp[r] == 0xFFFFFFFFu ? tp[r] : t.idx[tp[r]];
-            }
+            gi[r] = (e < k && tp[r] != 0xFFFFFFFFu) ? t.idx[tp[r]] : 0xFFFFFFFFu;
+            if (e < k) out_d[base + e] = sq ? td[r] : sqrtf(td[r]);
         }
+        if (pend_q != 0xFFFFFFFFu) {
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+                if (r * 64 + lane < k) out_i[(size_t)pend_q * (size_t)k + r * 64 + lane] = pend_i[r];
+        }
+        pend_q = qo;
+#pragma unroll
+        for (int r = 0; r < R; ++r) pend_i[r] = gi[r];
+    }
+    if (pend_q != 0xFFFFFFFFu) {
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+            if (r * 64 + lane < k) out_i[(size_t)pend_q * (size_t)k + r * 64 + lane] = pend_i[r];
     }
 }
 
