@@ -61,11 +61,21 @@ def lib_sha256():
     return h.hexdigest()
 
 
-def pmc_traffic(n_particles, k, q_per_launch):
-    """(HBM bytes per collect launch, source file) from the PMC summary measured
-    with this very library build, or (None, None)."""
+def pmc_traffic(n_particles, k, q_per_launch, kind="knn"):
+    """(HBM bytes per launch, source file) from the PMC summary measured with
+    this very library build, or (None, None).  kind: "knn" (the collect
+    kernel) or "ball" (the C3 radius count, k ignored)."""
     import glob
     sha = lib_sha256()
+    if kind == "ball":
+        for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_ball.json"))):
+            try:
+                pm = json.load(open(path))
+            except Exception:
+                continue
+            if pm.get("lib_sha256") == sha and pm.get("n_particles") == n_particles:
+                return pm.get("hbm_bytes_per_launch"), os.path.relpath(path, ROOT)
+        return None, None
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_knn.json"))):
         try:
             pm = json.load(open(path))
@@ -308,9 +318,13 @@ def suite(args, capi, hip, tree, dev_pts, n, k, L, stream, od, oi):
         # re-read from cache (the kernel is VALU-bound: profiles/r01k_ball_pmc.txt)
         br = 16.0 * REF_BALL_NODES_1E8 + 12.0 * REF_BALL_POINTS_1E8 + 16.0
         ach = br * n / (kern_ms / steps * 1e-3) / 1e9
+        traffic, tsrc = pmc_traffic(n, k, n, kind="ball")
         out["radius_count"]["roofline"] = {
             "bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": ach / HBM_PEAK_GBS, "bytes_per_query": br,
+            "traffic": traffic, "traffic_source": tsrc,
+            "hbm_frac": (None if traffic is None else
+                         traffic / (kern_ms / steps * 1e-3) / (HBM_PEAK_GBS * 1e9)),
             "kernel": "ball_packet_kernel<periodic, count> (nbodyhpc_amd/csrc/ball.hip)"}
     log(f"suite: radius count {n / sec:.3e} q/s, mean {c.mean():.1f} (expect {expect:.1f})")
     # C3: CSR batch (host in / host out: PCIe-inclusive)

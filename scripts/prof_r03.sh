@@ -16,6 +16,8 @@ timeout -k 10 900 python3 bench.py --suite > $O/suite.json 2> $O/suite.err \
  && echo "[prof] trace" && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/trace -o run --output-format csv -- $B > $O/trace.log 2>&1 \
  && echo "[prof] fetch" && timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex knn_collect -d $O/fetch -o run --output-format csv -- $B > $O/fetch.log 2>&1 \
  && echo "[prof] write" && timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex knn_collect -d $O/write -o run --output-format csv -- $B > $O/write.log 2>&1 \
+ && echo "[prof] ball fetch" && timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex ball_packet -d $O/ball_fetch -o run --output-format csv -- python3 scripts/ball_run.py > $O/ball_fetch.log 2>&1 \
+ && echo "[prof] ball write" && timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex ball_packet -d $O/ball_write -o run --output-format csv -- python3 scripts/ball_run.py > $O/ball_write.log 2>&1 \
  && cp $O/suite.json $O/bench.json
 rc=$?
 date

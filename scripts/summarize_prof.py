@@ -105,6 +105,27 @@ def main():
         }
         json.dump(out, open(os.path.join(prof, f"{tag}_pmc_knn.json"), "w"), indent=1)
         print(json.dumps(out, indent=1))
+    # the C3 radius count's passes (scripts/ball_run.py under rocprofv3)
+    bf = find(os.path.join(src, "ball_fetch"), "*counter_collection.csv")
+    bw = find(os.path.join(src, "ball_write"), "*counter_collection.csv")
+    if bf and bw:
+        fv = per_dispatch(bf, "ball_packet")
+        wv = per_dispatch(bw, "ball_packet")
+        f_kib, w_kib = sum(fv) / len(fv), sum(wv) / len(wv)
+        shaf = os.path.join(src, "lib.sha256")
+        out = {
+            "lib_sha256": open(shaf).read().split()[0] if os.path.exists(shaf) else None,
+            "kernel": "ball_packet_kernel<periodic, count> (nbodyhpc_amd/csrc/ball.hip)",
+            "command": "rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE --kernel-include-regex "
+                       "ball_packet -- python3 scripts/ball_run.py",
+            "n_particles": 100_000_000, "r": 0.01, "queries_per_launch": 100_000_000,
+            "dispatches": [len(fv), len(wv)],
+            "FETCH_SIZE_KiB_per_launch": f_kib, "WRITE_SIZE_KiB_per_launch": w_kib,
+            "hbm_bytes_per_launch": 2.0 * 1024.0 * f_kib + 1024.0 * w_kib,
+            "note": "FETCH_SIZE doubled (gfx950 wide-read correction)",
+        }
+        json.dump(out, open(os.path.join(prof, f"{tag}_pmc_ball.json"), "w"), indent=1)
+        print(json.dumps(out, indent=1))
     if b:
         print(json.dumps(b)[:2000])
 
