@@ -55,10 +55,10 @@ __device__ __forceinline__ float box_ub2(float qx, float qy, float qz, const flo
 // occupancy per variant: the count kernels spilled to scratch at 8 waves per
 // SIMD (20 / 104 B per lane, periodic / not: WRITE_SIZE 4.7 GB per 1e8 count,
 // r03f); at 7 (periodic) and 6 (not) they fit their registers
-template <bool PER, bool FILL> constexpr int ball_occ() { return FILL ? 8 : (PER ? 7 : 6); }
+constexpr int BALL_OCC[2][2] = {{6, 8}, {7, 8}}; // [periodic][fill]
 
 template <bool PER, bool FILL>
-__global__ void __launch_bounds__(TB, ball_occ<PER, FILL>())
+__global__ void __launch_bounds__(TB, BALL_OCC[PER][FILL])
 ball_packet_kernel(DevTree t, const uint32_t *__restrict__ linfo, const float *__restrict__ q,
                    const uint32_t *__restrict__ order, uint32_t m, float r2, PadLeaves pad,
                    uint32_t *__restrict__ out_count, const uint64_t *__restrict__ row_offsets,
