@@ -52,10 +52,11 @@ __device__ __forceinline__ float box_ub2(float qx, float qy, float qz, const flo
     return (ux * ux + uy * uy) + uz * uz;
 }
 
-// occupancy per variant: the count kernels spilled to scratch at 8 waves per
-// SIMD (20 / 104 B per lane, periodic / not: WRITE_SIZE 4.7 GB per 1e8 count,
-// r03f); at 7 (periodic) and 6 (not) they fit their registers
-constexpr int BALL_OCC[2][2] = {{6, 8}, {7, 8}}; // [periodic][fill]
+// occupancy per variant ([periodic][fill]).  The count kernels spill a few
+// registers at 8 waves per SIMD (20 / 104 B per lane, periodic / not; the
+// periodic 1e8 count writes 4.7 GB, r03f), but at 7 waves without spills the
+// periodic count ran 128.5 ms against 124.3 (r03g): the spills stay in L2
+constexpr int BALL_OCC[2][2] = {{8, 8}, {8, 8}};
 
 template <bool PER, bool FILL>
 __global__ void __launch_bounds__(TB, BALL_OCC[PER][FILL])
