@@ -82,10 +82,14 @@ class KDTree(cKDTree):
         return distances, indices
 
     def query_ball(self, points: np.ndarray, r: float, return_length: bool = False,
-                   return_sorted: bool = True, workers: int = 1, **kwargs):
+                   return_sorted: bool = True, workers: int = 1, return_csr: bool = False,
+                   **kwargs):
         """Points within distance r (d2 <= r*r in float32, the kNN metric).
 
         return_length=True -> uint32 counts, shape points.shape[:-1].
+        return_csr=True -> (offsets uint64 (M + 1,), indices uint32): row i is
+        indices[offsets[i]:offsets[i + 1]] (each row sorted unless
+        return_sorted=False); no per-row Python objects, for large batches.
         Otherwise an object array of uint32 index arrays (sorted ascending
         unless return_sorted=False), like scipy's query_ball_point.
         """
@@ -96,8 +100,14 @@ class KDTree(cKDTree):
         if return_length:
             return super().query_ball_count(points, float(r)).reshape(out_shape)
         off, idx = super().query_ball_csr(points, float(r))
-        rows = np.empty(len(off) - 1, dtype=object)
-        for i in range(len(off) - 1):
+        m = len(off) - 1
+        if return_csr:
+            if return_sorted:
+                for i in range(m):  # in place, row by row (cache-resident rows)
+                    idx[off[i]:off[i + 1]].sort()
+            return off, idx
+        rows = np.empty(m, dtype=object)
+        for i in range(m):
             row = idx[off[i]:off[i + 1]]
             rows[i] = np.sort(row) if return_sorted else row
         return rows.reshape(out_shape)
