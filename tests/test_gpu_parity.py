@@ -200,6 +200,9 @@ def test_python_surface(gpu):
     rows = t.query_ball(pts[:5], 0.05)
     counts = t.query_ball(pts[:5], 0.05, return_length=True)
     assert [len(r) for r in rows] == counts.tolist()
+    off, idx = t.query_ball(pts[:5], 0.05, return_csr=True)
+    assert np.diff(off.astype(np.int64)).tolist() == counts.tolist()
+    assert all(np.array_equal(rows[i], idx[off[i]:off[i + 1]]) for i in range(5))
     dens = t.density(pts[:100], k=8)
     assert np.all(np.isfinite(dens)) and np.all(dens > 0)
     rk = t.kth_distance(pts[:12].reshape(3, 4, 3), 8)
