@@ -12,14 +12,15 @@
  * memory unless the matching NBKD_*_DEVICE flag is set, in which case they are
  * device pointers on the tree's device.  `stream` is a hipStream_t (NULL = the
  * null stream).  With host outputs a call returns after the results are
- * copied back.  With device outputs the results are complete when the work
- * enqueued on `stream` so far has completed; the call itself may wait on
- * `stream` once before it returns: nbkd_query_knn / nbkd_query_kth to size the
- * re-walk of the queries whose seed ball held fewer than k points (on uniform
- * inputs about 2e-4 of them), nbkd_query_ball_count on a periodic tree to
- * count the queries outside [0, L]^3.  Calls on one tree are serialised, and a
- * call on another stream first waits for the tree's previous call to finish
- * on the device (the tree's scratch memory is reused).
+ * copied back.  With device outputs nbkd_query_knn / nbkd_query_kth return once
+ * the work is enqueued (the re-walk of the queries whose seed ball held fewer
+ * than k points runs on grids that read the failure count on the device);
+ * nbkd_query_ball_count on a periodic tree waits on `stream` once, to count the
+ * queries outside [0, L]^3.  The first call of a tree, or one needing more
+ * scratch than any before it, may also wait while the scratch grows.  Calls on
+ * one tree are serialised, and a call on another stream first waits for the
+ * tree's previous call to finish on the device (the tree's scratch memory is
+ * reused).
  *
  * Every entry point returns an nbkd_status; on failure nbkd_last_error()
  * (thread-local) holds a message.  Statuses NBKD_EINVAL / NBKD_EBOX /

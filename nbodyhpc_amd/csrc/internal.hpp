@@ -194,6 +194,29 @@ void launch_knn_packet(const Tree &t, const float *q, const uint32_t *order, uin
                        const float *tg, float *od, uint32_t *oi, uint32_t *fail_list,
                        uint32_t *fail_count, unsigned long long *stats, hipStream_t s);
 
+// The queries one collect / select pass handles (order[0 .. m)): a count known
+// on the host (count == nullptr: m), or, for the retry rounds, a count the
+// previous round left in device memory: m = min(*count - base, cap), 0 when
+// *count <= base, and 0 unless the density mode matches (mode 1: only when the
+// failures are dense, *count * 512 >= total, walked as packets of 64; mode 2:
+// only when they are sparse, one query per wave).  A device-counted pass is
+// launched on a fixed grid that strides over its packets, so the host never
+// reads the count: the kNN call returns without waiting on the device.
+struct QSpan {
+    uint32_t m;            // the count, or the cap of a device-counted pass
+    const uint32_t *count; // device count, or nullptr
+    uint32_t base;         // this pass's first entry of the device-counted list
+    uint32_t total;        // queries of the call (density test)
+    int mode;              // 0: always; 1: only dense; 2: only sparse
+};
+__host__ __device__ inline QSpan static_span(uint32_t m) { return QSpan{m, nullptr, 0u, 0u, 0}; }
+__device__ __forceinline__ uint32_t span_m(const QSpan &s) {
+    if (!s.count) return s.m;
+    const uint32_t c = __builtin_amdgcn_readfirstlane(*s.count);
+    if (s.mode != 0 && (((uint64_t)c * 512u >= (uint64_t)s.total) != (s.mode == 1))) return 0u;
+    return c > s.base ? min(c - s.base, s.m) : 0u;
+}
+
 // (oi == nullptr: od receives only the k-th distance of each query, m floats)
 // knn_collect.hip: candidate column capacity for k, and one collect + select
 // pass over m queries (order[0..m) = query ids; tg = seed bounds, scaled by
@@ -204,11 +227,13 @@ uint32_t collect_capacity(int k);
 // seed-failure retry: adaptive per-query seeds written by the first select
 // pass (on by default) instead of a fixed 4x seed
 bool retry_adaptive();
-nbkd_status launch_knn_collect(const Tree &t, const float *q, const uint32_t *order, uint32_t m,
+// fail_bits != nullptr: failures are marked at bit pos_base + gq (first pass)
+// instead of appended to fail_list
+nbkd_status launch_knn_collect(const Tree &t, const float *q, const uint32_t *order, QSpan span,
                                int k, const float *tg, float seed_mul, uint32_t qpp, uint2 *cand,
                                uint32_t capg, uint32_t *ccount, float *od, uint32_t *oi,
-                               uint32_t *fail_list, uint32_t *fail_count, uint32_t pos_base,
-                               bool retry, bool fix_seed, bool sq, float *kb,
+                               uint32_t *fail_list, uint32_t *fail_count, uint32_t *fail_bits,
+                               uint32_t pos_base, bool retry, bool fix_seed, bool sq, float *kb,
                                unsigned long long *stats, hipStream_t s);
 
 // ball.hip: radius count (out_idx == nullptr) or CSR fill over m kd-ordered

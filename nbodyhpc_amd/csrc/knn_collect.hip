@@ -658,7 +658,7 @@ __global__ void __launch_bounds__(TB, OCC)
 knn_collect_grp_kernel(DevTree t, const float *__restrict__ ginfo,
                        const uint32_t *__restrict__ linfo, const float *__restrict__ hinfo,
                        const float *__restrict__ q,
-                       const uint32_t *__restrict__ order, uint32_t m, int kq,
+                       const uint32_t *__restrict__ order, QSpan span, int kq,
                        const float *__restrict__ tg, float seed_mul, uint32_t qpp,
                        uint2 *__restrict__ cand, uint32_t capg,
                        uint32_t *__restrict__ ccount, unsigned long long *__restrict__ stats,
@@ -666,48 +666,70 @@ knn_collect_grp_kernel(DevTree t, const float *__restrict__ ginfo,
     __shared__ CollectLdsG Wl[WPB];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     CollectLdsG &W = Wl[wave];
+    // packets pk < npk; a static pass launches one wave per packet, a device-
+    // counted pass (retry rounds) a fixed grid that strides over them
+    const uint32_t m = span_m(span);
+    const uint32_t npk = (m + qpp - 1) / qpp;
     const uint32_t bid = xcd ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
-    const uint32_t pk = bid * WPB + wave;
-    const uint32_t gq = pk * qpp + lane;
-    const bool valid = (uint32_t)lane < qpp && gq < m;
-    const uint32_t qo = valid ? order[gq] : 0u;
-    const float qx = valid ? q[3 * (size_t)qo] : 0.0f;
-    const float qy = valid ? q[3 * (size_t)qo + 1] : 0.0f;
-    const float qz = valid ? q[3 * (size_t)qo + 2] : 0.0f;
-    const float seed = valid ? fminf(tg[qo] * seed_mul, FLT_MAX) : -INFINITY;
-    const bool fin = seed < FLT_MAX && seed >= 1e-30f;
-    const float s_over_nb = fin ? seed * (1.0f / NB) : (seed > 0.0f ? INFINITY : 0.0f);
-    const float nb_over_s = fin ? (float)NB / seed * 1.00000095367431640625f : 0.0f;
+    for (uint32_t pk = bid * WPB + wave; pk < npk; pk += gridDim.x * WPB) {
+        const uint32_t gq = pk * qpp + lane;
+        const bool valid = (uint32_t)lane < qpp && gq < m;
+        const uint32_t qo = valid ? order[gq] : 0u;
+        const float qx = valid ? q[3 * (size_t)qo] : 0.0f;
+        const float qy = valid ? q[3 * (size_t)qo + 1] : 0.0f;
+        const float qz = valid ? q[3 * (size_t)qo + 2] : 0.0f;
+        const float seed = valid ? fminf(tg[qo] * seed_mul, FLT_MAX) : -INFINITY;
+        const bool fin = seed < FLT_MAX && seed >= 1e-30f;
+        const float s_over_nb = fin ? seed * (1.0f / NB) : (seed > 0.0f ? INFINITY : 0.0f);
+        const float nb_over_s = fin ? (float)NB / seed * 1.00000095367431640625f : 0.0f;
+        wave_sync(); // the previous packet's LDS reads are done
 #pragma unroll
-    for (int w = 0; w < NB / 4; ++w) W.hist[w][lane] = 0u;
-    uint2 *const col = cand + (size_t)pk * qpp * capg;
-    uint32_t cnt = 0;
-    uint64_t st[13] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-    float kth = seed;
-    grp_packet<PER, PER, STATS>(t, ginfo, linfo, hinfo, W, lane, qx, qy, qz, kth, s_over_nb, nb_over_s,
-                                col, qpp, capg, kq, cnt, st);
-    if (valid) ccount[gq] = cnt;
-    // the final bound: at least k candidates lie strictly below it (bound
-    // histogram), so none at or above it is among the k smallest
-    if (valid && kbound) kbound[gq] = kth;
-    if (STATS && lane == 0) {
-        atomicAdd(&stats[0], (unsigned long long)st[0]);
-        atomicAdd(&stats[1], (unsigned long long)st[5]);
-        atomicAdd(&stats[2], (unsigned long long)st[3]);
-        atomicAdd(&stats[3], (unsigned long long)st[4]);
-        atomicAdd(&stats[4], (unsigned long long)st[2]);
-        atomicAdd(&stats[5], 1ull);
-        atomicAdd(&stats[7], (unsigned long long)st[1]);
+        for (int w = 0; w < NB / 4; ++w) W.hist[w][lane] = 0u;
+        uint2 *const col = cand + (size_t)pk * qpp * capg;
+        uint32_t cnt = 0;
+        uint64_t st[13] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+        float kth = seed;
+        grp_packet<PER, PER, STATS>(t, ginfo, linfo, hinfo, W, lane, qx, qy, qz, kth, s_over_nb,
+                                    nb_over_s, col, qpp, capg, kq, cnt, st);
+        if (valid) ccount[gq] = cnt;
+        // the final bound: at least k candidates lie strictly below it (bound
+        // histogram), so none at or above it is among the k smallest
+        if (valid && kbound) kbound[gq] = kth;
+        if (STATS && lane == 0) {
+            atomicAdd(&stats[0], (unsigned long long)st[0]);
+            atomicAdd(&stats[1], (unsigned long long)st[5]);
+            atomicAdd(&stats[2], (unsigned long long)st[3]);
+            atomicAdd(&stats[3], (unsigned long long)st[4]);
+            atomicAdd(&stats[4], (unsigned long long)st[2]);
+            atomicAdd(&stats[5], 1ull);
+            atomicAdd(&stats[7], (unsigned long long)st[1]);
 #pragma unroll
-        for (int i = 0; i < 6; ++i) atomicAdd(&stats[10 + i], (unsigned long long)st[6 + i]);
-        atomicAdd(&stats[16], (unsigned long long)st[12]);
+            for (int i = 0; i < 6; ++i) atomicAdd(&stats[10 + i], (unsigned long long)st[6 + i]);
+            atomicAdd(&stats[16], (unsigned long long)st[12]);
+        }
+        if (STATS) {
+            uint32_t c = valid ? cnt : 0u;
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+            if (lane == 0) atomicAdd(&stats[6], (unsigned long long)c);
+        }
     }
-    if (STATS) {
-        uint32_t c = valid ? cnt : 0u;
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
-        if (lane == 0) atomicAdd(&stats[6], (unsigned long long)c);
-    }
+}
+
+// a query whose seed ball held fewer than k points (or more than the column):
+// marked in the failure bitmap at its sorted position (first pass: the next
+// round reads the bitmap in kd order), else appended by query id to the next
+// round's list.  Periodic queries outside [0, L]^3 are listed for the exact
+// kernel already (outside_box_kernel).
+template <bool PER>
+__device__ __forceinline__ void mark_failure(float qx, float qy, float qz, float L, uint32_t id,
+                                             uint32_t *fail_list, uint32_t *fail_count,
+                                             uint32_t *fail_bits) {
+    if (PER && !(qx >= 0.0f && qx <= L && qy >= 0.0f && qy <= L && qz >= 0.0f && qz <= L)) return;
+    if (fail_bits)
+        atomicOr(&fail_bits[id >> 5], 1u << (id & 31u));
+    else
+        fail_list[atomicAdd(fail_count, 1u)] = id;
 }
 
 // One 8-KB candidate block (64 rows x 8 pieces of 16 B, row-contiguous) into
@@ -731,11 +753,11 @@ __device__ __forceinline__ void issue_block(const uint4 *b4, uint4 *lds4, int la
 template <int KC, bool PER, bool WHOLE>
 __global__ void __launch_bounds__(TB, KC <= 32 ? 4 : 2)
 knn_select_kernel(DevTree t, const float *__restrict__ q, const uint32_t *__restrict__ order,
-                  uint32_t m, int k, uint32_t qpp, const uint2 *__restrict__ cand, uint32_t capg,
+                  QSpan span, int k, uint32_t qpp, const uint2 *__restrict__ cand, uint32_t capg,
                   const uint32_t *__restrict__ ccount, float *__restrict__ out_d,
                   uint32_t *__restrict__ out_i, uint32_t *__restrict__ fail_list,
                   uint32_t *__restrict__ fail_count, uint32_t pos_base, uint64_t all_rows,
-                  float *__restrict__ tg_fix, float mu, bool sq) {
+                  float *__restrict__ tg_fix, float mu, bool sq, uint32_t *__restrict__ fail_bits) {
     constexpr int NS = 16;                  // candidates merged per pass
     constexpr int CC = KC < 32 ? KC : 32;   // top-k registers staged per output pass
     constexpr int SW = CC < 32 ? 32 * 64 : CC * 64; // >= 8 KB: one candidate block
@@ -743,8 +765,13 @@ knn_select_kernel(DevTree t, const float *__restrict__ q, const uint32_t *__rest
     __shared__ uint32_t rowq_all[WPB][64];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     uint32_t *stage = stage_all[wave], *rowq = rowq_all[wave];
-    // lane = one query gq; its candidates: packet gq / qpp, row gq % qpp
-    const uint32_t gq = (blockIdx.x * WPB + wave) * 64u + lane;
+    const uint32_t m = span_m(span);
+    // lane = one query gq; its candidates: packet gq / qpp, row gq % qpp.  A
+    // device-counted pass (retry rounds) strides its fixed grid over the blocks
+    for (uint32_t wb = blockIdx.x * WPB + wave; wb * 64u < m; wb += gridDim.x * WPB) {
+    __builtin_amdgcn_s_waitcnt(0xC07F); // lgkmcnt(0): the previous block's LDS reads are done
+    wave_sync();
+    const uint32_t gq = wb * 64u + lane;
     const bool valid = gq < m;
     const uint32_t qo = valid ? order[gq] : 0u;
     const uint32_t n = valid ? ccount[gq] : 0u;
@@ -753,8 +780,8 @@ knn_select_kernel(DevTree t, const float *__restrict__ q, const uint32_t *__rest
         const float qx = q[3 * (size_t)qo], qy = q[3 * (size_t)qo + 1], qz = q[3 * (size_t)qo + 2];
         // outside-box periodic queries are listed already (outside_box_kernel);
         // pos_base != ~0: list the sorted position (pos_base + gq), not the id
-        knn_fail_check<PER>(true, true, 0xFFFFFFFFu, qx, qy, qz, t.box,
-                            pos_base == 0xFFFFFFFFu ? qo : pos_base + gq, fail_list, fail_count);
+        mark_failure<PER>(qx, qy, qz, t.box, pos_base == 0xFFFFFFFFu ? qo : pos_base + gq,
+                          fail_list, fail_count, fail_bits);
         // the retry's seed (tg_fix: first pass only); n counted every point
         // inside the seed ball, so it measured the local density.  n < k:
         // grow the volume to hold ~1.5 mu at that density (2x..8x).  An
@@ -843,7 +870,7 @@ knn_select_kernel(DevTree t, const float *__restrict__ q, const uint32_t *__rest
 
     if (out_i == nullptr) { // k-th distance only (nbkd_query_kth): column k-1
         if (valid) out_d[qo] = sq ? td[KC - 1] : sqrtf(td[KC - 1]);
-        return;
+        continue;
     }
     rowq[lane] = valid ? qo : 0xFFFFFFFFu;
 #pragma unroll
@@ -869,6 +896,7 @@ knn_select_kernel(DevTree t, const float *__restrict__ q, const uint32_t *__rest
         for (int j = 0; j < CC; ++j) stage[j * 64 + (lane ^ j)] = ti[j0 + j];
         wave_sync();
         store_rows<CC>(stage, rowq, out_i, k, j0 - (KC - k), lane);
+    }
     }
 }
 
@@ -985,17 +1013,18 @@ __device__ __forceinline__ void wave_sort_stages(float (&d)[R], uint32_t (&p)[R]
 template <int R, bool PER, bool WHOLE>
 __global__ void __launch_bounds__(TB)
 knn_select_wave_kernel(DevTree t, const float *__restrict__ q, const uint32_t *__restrict__ order,
-                       uint32_t m, int k, const uint2 *__restrict__ cand, uint32_t capg,
+                       QSpan span, int k, const uint2 *__restrict__ cand, uint32_t capg,
                        const uint32_t *__restrict__ ccount, float *__restrict__ out_d,
                        uint32_t *__restrict__ out_i, uint32_t *__restrict__ fail_list,
                        uint32_t *__restrict__ fail_count, uint32_t pos_base,
                        float *__restrict__ tg_fix, float mu, bool sq,
-                       const float *__restrict__ kbound) {
+                       const float *__restrict__ kbound, uint32_t *__restrict__ fail_bits) {
     constexpr int K = 64 * R;
     // per wave: the query's candidates below its final bound, compacted
     __shared__ uint2 cl_all[WPB][2 * K];
     const int lane = threadIdx.x & 63;
     uint2 *const cl = cl_all[threadIdx.x >> 6];
+    const uint32_t m = span_m(span);
     const uint32_t nwaves = gridDim.x * WPB;
     // software pipeline: the next query's count, bound and first 2K slots are
     // loaded before this query is sorted (their addresses depend on gq only;
@@ -1032,9 +1061,8 @@ knn_select_wave_kernel(DevTree t, const float *__restrict__ q, const uint32_t *_
             if (lane == 0) {
                 const float qx = q[3 * (size_t)qo], qy = q[3 * (size_t)qo + 1],
                             qz = q[3 * (size_t)qo + 2];
-                knn_fail_check<PER>(true, true, 0xFFFFFFFFu, qx, qy, qz, t.box,
-                                    pos_base == 0xFFFFFFFFu ? qo : pos_base + gq, fail_list,
-                                    fail_count);
+                mark_failure<PER>(qx, qy, qz, t.box, pos_base == 0xFFFFFFFFu ? qo : pos_base + gq,
+                                  fail_list, fail_count, fail_bits);
                 if (tg_fix) { // the retry's seed, as knn_select_kernel
                     float fv;
                     if (n < (uint32_t)k)
@@ -1185,13 +1213,30 @@ bool groups_enabled() {
     return on;
 }
 
+// a device-counted pass's fixed grid: 8 blocks of 4 waves per CU
+unsigned resident_blocks() {
+    static const unsigned b = [] {
+        int dev = 0, cus = 256;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            cus = 256;
+        (void)hipGetLastError();
+        return 8u * (unsigned)std::max(cus, 1);
+    }();
+    return b;
+}
+
 template <bool PER>
-void launch_collect(const Tree &t, const float *q, const uint32_t *order, uint32_t m, int k,
+void launch_collect(const Tree &t, const float *q, const uint32_t *order, QSpan span, int k,
                     const float *tg, float seed_mul, uint32_t qpp, uint2 *cand, uint32_t capg,
                     uint32_t *ccount, unsigned long long *stats, bool retry, float *kbound,
                     hipStream_t s) {
     const char *const name = retry ? "knn_retry" : "knn_collect";
-    const unsigned blocks = (unsigned)(((uint64_t)m + qpp - 1) / qpp + WPB - 1) / WPB;
+    const uint32_t m = span.m;
+    const unsigned blocks =
+        span.count ? std::min<unsigned>(resident_blocks(),
+                                        (unsigned)((((uint64_t)m + qpp - 1) / qpp + WPB - 1) / WPB))
+                   : (unsigned)((((uint64_t)m + qpp - 1) / qpp + WPB - 1) / WPB);
     // the bound histogram's 8-bit bucket counts are exact while the cumulative
     // count below the k-th's bucket is < 256, i.e. for k <= 255 (a wrapped or
     // carried byte can only make a larger cumulative count); above, no tightening
@@ -1205,12 +1250,12 @@ void launch_collect(const Tree &t, const float *q, const uint32_t *order, uint32
         TimedScope ts(name, s);
         if (stats)
             knn_collect_grp_kernel<PER, 8, true><<<blocks, TB, 0, s>>>(
-                view(t), t.ginfo, t.leafinfo, t.hinfo, q, order, m, k, tg, seed_mul, qpp, cand, capg,
-                ccount, stats, xcd, kbound);
+                view(t), t.ginfo, t.leafinfo, t.hinfo, q, order, span, k, tg, seed_mul, qpp, cand,
+                capg, ccount, stats, xcd && !span.count, kbound);
         else
             knn_collect_grp_kernel<PER, 8, false><<<blocks, TB, 0, s>>>(
-                view(t), t.ginfo, t.leafinfo, t.hinfo, q, order, m, k, tg, seed_mul, qpp, cand, capg,
-                ccount, nullptr, xcd, kbound);
+                view(t), t.ginfo, t.leafinfo, t.hinfo, q, order, span, k, tg, seed_mul, qpp, cand,
+                capg, ccount, nullptr, xcd && !span.count, kbound);
         return;
     }
 #ifdef NBKD_EXPERIMENTS
@@ -1258,16 +1303,18 @@ void launch_collect(const Tree &t, const float *q, const uint32_t *order, uint32
 }
 
 template <int R>
-void launch_select_wave(const Tree &t, const float *q, const uint32_t *order, uint32_t m, int k,
+void launch_select_wave(const Tree &t, const float *q, const uint32_t *order, QSpan span, int k,
                         uint32_t qpp, const uint2 *cand, uint32_t capg, const uint32_t *ccount,
                         float *od, uint32_t *oi, uint32_t *fail_list, uint32_t *fail_count,
-                        uint32_t pos_base, float *tg_fix, float mu, bool sq, const float *kbound,
-                        hipStream_t s) {
-    const unsigned blocks = (unsigned)std::min<uint64_t>(((uint64_t)m + WPB - 1) / WPB, 32768);
+                        uint32_t *fail_bits, uint32_t pos_base, float *tg_fix, float mu, bool sq,
+                        const float *kbound, hipStream_t s) {
+    const unsigned blocks = (unsigned)std::min<uint64_t>(((uint64_t)span.m + WPB - 1) / WPB,
+                                                         span.count ? resident_blocks() : 32768u);
 #define NBKD_SELW(PER, WH)                                                                         \
-    knn_select_wave_kernel<R, PER, WH><<<blocks, TB, 0, s>>>(view(t), q, order, m, k, cand, capg,  \
-                                                            ccount, od, oi, fail_list, fail_count, \
-                                                            pos_base, tg_fix, mu, sq, kbound)
+    knn_select_wave_kernel<R, PER, WH><<<blocks, TB, 0, s>>>(view(t), q, order, span, k, cand,     \
+                                                            capg, ccount, od, oi, fail_list,       \
+                                                            fail_count, pos_base, tg_fix, mu, sq,  \
+                                                            kbound, fail_bits)
     if (t.periodic) {
         if (qpp == 64) NBKD_SELW(true, true); else NBKD_SELW(true, false);
     } else {
@@ -1277,19 +1324,22 @@ void launch_select_wave(const Tree &t, const float *q, const uint32_t *order, ui
 }
 
 template <int KC>
-void launch_select(const Tree &t, const float *q, const uint32_t *order, uint32_t m, int k,
+void launch_select(const Tree &t, const float *q, const uint32_t *order, QSpan span, int k,
                    uint32_t qpp, const uint2 *cand, uint32_t capg, const uint32_t *ccount,
                    float *od, uint32_t *oi, uint32_t *fail_list, uint32_t *fail_count,
-                   uint32_t pos_base, float *tg_fix, float mu, bool sq, hipStream_t s) {
-    const unsigned blocks = (m + TB - 1) / TB;
+                   uint32_t *fail_bits, uint32_t pos_base, float *tg_fix, float mu, bool sq,
+                   hipStream_t s) {
+    const unsigned need = (span.m + TB - 1) / TB;
+    const unsigned blocks = span.count ? std::min(need, resident_blocks()) : need;
     static const uint64_t all_rows = [] { // NBKD_SELECT_ROWMASK=0: read whole blocks
         const char *e = knob("NBKD_SELECT_ROWMASK");
         return (e && atoi(e) == 0) ? ~0ull : 0ull;
     }();
 #define NBKD_SELECT(PER, WH)                                                                       \
-    knn_select_kernel<KC, PER, WH><<<blocks, TB, 0, s>>>(view(t), q, order, m, k, qpp, cand, capg, \
-                                                        ccount, od, oi, fail_list, fail_count,     \
-                                                        pos_base, all_rows, tg_fix, mu, sq)
+    knn_select_kernel<KC, PER, WH><<<blocks, TB, 0, s>>>(view(t), q, order, span, k, qpp, cand,    \
+                                                        capg, ccount, od, oi, fail_list,           \
+                                                        fail_count, pos_base, all_rows, tg_fix,    \
+                                                        mu, sq, fail_bits)
     if (t.periodic) {
         if (qpp == 64) NBKD_SELECT(true, true); else NBKD_SELECT(true, false);
     } else {
@@ -1316,20 +1366,20 @@ uint32_t collect_capacity(int k) {
     return (uint32_t)((c + 15.0) / 16.0) * 16u;
 }
 
-nbkd_status launch_knn_collect(const Tree &t, const float *q, const uint32_t *order, uint32_t m,
+nbkd_status launch_knn_collect(const Tree &t, const float *q, const uint32_t *order, QSpan span,
                                int k, const float *tg, float seed_mul, uint32_t qpp, uint2 *cand,
                                uint32_t capg, uint32_t *ccount, float *od, uint32_t *oi,
-                               uint32_t *fail_list, uint32_t *fail_count, uint32_t pos_base,
-                               bool retry, bool fix_seed, bool sq, float *kb,
+                               uint32_t *fail_list, uint32_t *fail_count, uint32_t *fail_bits,
+                               uint32_t pos_base, bool retry, bool fix_seed, bool sq, float *kb,
                                unsigned long long *stats, hipStream_t s) {
-    if (m == 0) return NBKD_OK;
+    if (span.m == 0) return NBKD_OK;
     // k > 64: the collect kernel hands each query's final bound to the wave select
     float *kbound = k > 64 ? kb : nullptr;
     if (t.periodic)
-        launch_collect<true>(t, q, order, m, k, tg, seed_mul, qpp, cand, capg, ccount, stats,
+        launch_collect<true>(t, q, order, span, k, tg, seed_mul, qpp, cand, capg, ccount, stats,
                              retry, kbound, s);
     else
-        launch_collect<false>(t, q, order, m, k, tg, seed_mul, qpp, cand, capg, ccount, stats,
+        launch_collect<false>(t, q, order, span, k, tg, seed_mul, qpp, cand, capg, ccount, stats,
                               retry, kbound, s);
     NBKD_HIP(hipGetLastError());
     {
@@ -1338,26 +1388,26 @@ nbkd_status launch_knn_collect(const Tree &t, const float *q, const uint32_t *or
         float *tg_fix = fix_seed ? const_cast<float *>(tg) : nullptr;
         const float mu = (float)k + 4.0f * sqrtf((float)k) + 4.0f;
         if (k <= 16)
-            launch_select<16>(t, q, order, m, k, qpp, cand, capg, ccount, od, oi, fail_list,
-                              fail_count, pos_base, tg_fix, mu, sq, s);
+            launch_select<16>(t, q, order, span, k, qpp, cand, capg, ccount, od, oi, fail_list,
+                              fail_count, fail_bits, pos_base, tg_fix, mu, sq, s);
         else if (k <= 32)
-            launch_select<32>(t, q, order, m, k, qpp, cand, capg, ccount, od, oi, fail_list,
-                              fail_count, pos_base, tg_fix, mu, sq, s);
+            launch_select<32>(t, q, order, span, k, qpp, cand, capg, ccount, od, oi, fail_list,
+                              fail_count, fail_bits, pos_base, tg_fix, mu, sq, s);
         else if (k <= 64)
-            launch_select<64>(t, q, order, m, k, qpp, cand, capg, ccount, od, oi, fail_list,
-                              fail_count, pos_base, tg_fix, mu, sq, s);
+            launch_select<64>(t, q, order, span, k, qpp, cand, capg, ccount, od, oi, fail_list,
+                              fail_count, fail_bits, pos_base, tg_fix, mu, sq, s);
         else if (k <= 128)
-            launch_select_wave<2>(t, q, order, m, k, qpp, cand, capg, ccount, od, oi, fail_list,
-                                  fail_count, pos_base, tg_fix, mu, sq, kbound, s);
+            launch_select_wave<2>(t, q, order, span, k, qpp, cand, capg, ccount, od, oi,
+                                  fail_list, fail_count, fail_bits, pos_base, tg_fix, mu, sq, kbound, s);
         else if (k <= 256)
-            launch_select_wave<4>(t, q, order, m, k, qpp, cand, capg, ccount, od, oi, fail_list,
-                                  fail_count, pos_base, tg_fix, mu, sq, kbound, s);
+            launch_select_wave<4>(t, q, order, span, k, qpp, cand, capg, ccount, od, oi,
+                                  fail_list, fail_count, fail_bits, pos_base, tg_fix, mu, sq, kbound, s);
         else if (k <= 512)
-            launch_select_wave<8>(t, q, order, m, k, qpp, cand, capg, ccount, od, oi, fail_list,
-                                  fail_count, pos_base, tg_fix, mu, sq, kbound, s);
+            launch_select_wave<8>(t, q, order, span, k, qpp, cand, capg, ccount, od, oi,
+                                  fail_list, fail_count, fail_bits, pos_base, tg_fix, mu, sq, kbound, s);
         else
-            launch_select_wave<16>(t, q, order, m, k, qpp, cand, capg, ccount, od, oi, fail_list,
-                                   fail_count, pos_base, tg_fix, mu, sq, kbound, s);
+            launch_select_wave<16>(t, q, order, span, k, qpp, cand, capg, ccount, od, oi,
+                                   fail_list, fail_count, fail_bits, pos_base, tg_fix, mu, sq, kbound, s);
         NBKD_HIP(hipGetLastError());
     }
     return NBKD_OK;

@@ -731,7 +731,57 @@ outside_box_kernel(const float *__restrict__ q, uint32_t m, float L, uint32_t *_
     if (!inside) list[atomicAdd(count, 1u)] = i;
 }
 
-// out[i] = ord[pos[i]]: sorted positions back to query ids
+// The failure bitmap over sorted positions -> query ids in kd order + count:
+// per-word popcounts, an exclusive scan of them, then each word's set bits in
+// order.  Every grid is sized by the call's query count, so nothing here needs
+// the failure count on the host.
+__global__ void __launch_bounds__(TB)
+bits_popc_kernel(const uint32_t *__restrict__ bits, uint64_t nwords, uint32_t *__restrict__ pc) {
+    const uint64_t w = (uint64_t)blockIdx.x * TB + threadIdx.x;
+    if (w < nwords) pc[w] = (uint32_t)__popc(bits[w]);
+}
+
+__global__ void __launch_bounds__(TB)
+bits_emit_kernel(const uint32_t *__restrict__ bits, const uint32_t *__restrict__ pc_excl,
+                 uint64_t nwords, const uint32_t *__restrict__ ord, uint32_t *__restrict__ out,
+                 uint32_t *__restrict__ count) {
+    const uint64_t w = (uint64_t)blockIdx.x * TB + threadIdx.x;
+    if (w >= nwords) return;
+    uint32_t b = bits[w], o = pc_excl[w];
+    if (w == nwords - 1) *count = o + (uint32_t)__popc(b);
+    while (b) {
+        const uint32_t j = (uint32_t)__builtin_ctz(b);
+        b &= b - 1u;
+        out[o++] = ord[w * 32 + j];
+    }
+}
+
+// the entries of a device-counted list past what the rounds handled: appended
+// to the next list (order irrelevant there: one query per wave, or the exact
+// kernel)
+__global__ void __launch_bounds__(TB)
+spill_kernel(const uint32_t *__restrict__ from, const uint32_t *__restrict__ from_count,
+             uint32_t handled, uint32_t *__restrict__ to, uint32_t *__restrict__ to_count) {
+    const uint32_t c = *from_count;
+    for (uint32_t i = handled + blockIdx.x * TB + threadIdx.x; i < c; i += gridDim.x * TB)
+        to[atomicAdd(to_count, 1u)] = from[i];
+}
+
+nbkd_status compact_failures(Workspace &ws, const uint32_t *bits, uint32_t mm, const uint32_t *ord,
+                             uint32_t *out, uint32_t *count, hipStream_t s) {
+    const uint64_t nwords = ((uint64_t)mm + 31) / 32;
+    uint32_t *pc = (uint32_t *)ws.get(WS_KEYS2, nwords * 4u + 16u, s);
+    if (!pc) return NBKD_ENOMEM;
+    const unsigned blocks = (unsigned)((nwords + TB - 1) / TB);
+    bits_popc_kernel<<<blocks, TB, 0, s>>>(bits, nwords, pc);
+    nbkd_status rc = device_excl_scan(ws, pc, nwords, s);
+    if (rc) return rc;
+    bits_emit_kernel<<<blocks, TB, 0, s>>>(bits, pc, nwords, ord, out, count);
+    NBKD_HIP(hipGetLastError());
+    return NBKD_OK;
+}
+
+// out[i] = ord[pos[i]]: sorted positions back to query ids// out[i] = ord[pos[i]]: sorted positions back to query ids
 __global__ void __launch_bounds__(TB)
 gather_kernel(const uint32_t *__restrict__ pos, uint32_t n, const uint32_t *__restrict__ ord,
               uint32_t *__restrict__ out) {
@@ -949,8 +999,19 @@ nbkd_status knn_locked(const Tree &t, const float *q, uint64_t m, int k, float *
             uint64_t batch = budget / ((uint64_t)capg * 8u) / 64u * 64u;
             batch = std::max<uint64_t>(batch, 64);
             batch = std::min<uint64_t>(batch, ((uint64_t)mm + 63) / 64 * 64);
-            uint2 *cand = (uint2 *)t.ws.get(WS_CAND, batch * capg * 8u, s);
-            uint32_t *ccount = (uint32_t *)t.ws.get(WS_CCOUNT, batch * 4u, s);
+            // the re-walk rounds' columns: 8 capg (packets of 64 or one query
+            // per wave), then 64 capg (one query per wave)
+            const uint32_t capr = capg * 8u, capr2 = capg * 64u;
+            const uint64_t rb = std::max<uint64_t>(budget / ((uint64_t)capr * 8u) / 64u * 64u, 64);
+            const uint64_t rb2 = std::max<uint64_t>(budget / ((uint64_t)capr2 * 8u), 64);
+            // a round's pass covers at most min(cap, mm) queries, in packets of 64
+            const uint64_t mm64 = ((uint64_t)mm + 63) / 64 * 64;
+            const uint64_t cap1 = std::min<uint64_t>(rb, mm64), cap2 = std::min<uint64_t>(rb2, mm);
+            const uint64_t cand_bytes =
+                std::max<uint64_t>({batch * capg * 8u, cap1 * capr * 8u, cap2 * capr2 * 8u});
+            const uint64_t cc_words = std::max<uint64_t>(batch, cap1);
+            uint2 *cand = (uint2 *)t.ws.get(WS_CAND, cand_bytes, s);
+            uint32_t *ccount = (uint32_t *)t.ws.get(WS_CCOUNT, cc_words * 4u, s);
             // k > 64: per-query final bounds, collect -> wave select (any batch
             // of any round holds at most max(batch, mm) queries)
             float *kb = nullptr;
@@ -958,102 +1019,82 @@ nbkd_status knn_locked(const Tree &t, const float *q, uint64_t m, int k, float *
                 kb = (float *)t.ws.get(WS_KB, std::max<uint64_t>(batch, (uint64_t)mm) * 4u, s);
                 if (!kb) return NBKD_ENOMEM;
             }
-            // seed failures (fewer than k points in the seed ball, or more than
-            // the column holds) are retried with a 4x seed (2x radius): listed
-            // by sorted position, put back in kd order, and walked as packets
-            // of 64 (one query per wave when there are few); what still fails
-            // joins the exact kernel's list
-            uint32_t *rlist = (uint32_t *)t.ws.get(WS_LIST2, (size_t)mm * 4 + 16, s);
-            if (!cand || !ccount || !rlist) return NBKD_ENOMEM;
-            uint32_t *rcount = rlist + mm;
-            NBKD_HIP(hipMemsetAsync(rcount, 0, 4, s));
+            // Seed failures (fewer than k points in the seed ball, or more than
+            // the column holds) are re-walked without the host reading how many
+            // there are: the first pass marks them in a bitmap over the sorted
+            // positions; an ordered compaction turns it into query ids in kd
+            // order plus a count in device memory; the rounds below run on
+            // fixed grids that read that count (QSpan), and what a round does
+            // not resolve goes to the next one, the last to the exact kernel.
+            const uint64_t nwords = ((uint64_t)mm + 31) / 32;
+            uint32_t *bits = (uint32_t *)t.ws.get(WS_RSORT, nwords * 4u + 64u, s);
+            uint32_t *rq = (uint32_t *)t.ws.get(WS_LIST2, (size_t)mm * 8 + 256, s);
+            if (!cand || !ccount || !bits || !rq) return NBKD_ENOMEM;
+            uint32_t *rq_count = rq + (size_t)mm;      // round-1 queries (compaction)
+            uint32_t *r2 = rq_count + 16;               // round-2 list (ids)
+            uint32_t *r2_count = r2 + (size_t)mm;
+            NBKD_HIP(hipMemsetAsync(bits, 0, nwords * 4u, s));
+            NBKD_HIP(hipMemsetAsync(rq_count, 0, 4, s));
+            NBKD_HIP(hipMemsetAsync(r2_count, 0, 4, s));
+            const bool adaptive = retry_adaptive();
             {
                 TimedScope ts("knn", s);
                 for (uint64_t b0 = 0; b0 < mm; b0 += batch) {
                     const uint32_t nb = (uint32_t)std::min<uint64_t>(batch, mm - b0);
-                    rc = launch_knn_collect(t, dq, ord + b0, nb, k, tg, 1.0f, 64u, cand, capg,
-                                            ccount, dd, di, rlist, rcount, (uint32_t)b0, false,
-                                            retry_adaptive(), sq, kb, stats, s);
+                    rc = launch_knn_collect(t, dq, ord + b0, static_span(nb), k, tg, 1.0f, 64u, cand,
+                                            capg, ccount, dd, di, nullptr, nullptr, bits,
+                                            (uint32_t)b0, false, adaptive, sq, kb, stats, s);
                     if (rc) return rc;
                 }
             }
-            uint32_t nr = 0;
-            NBKD_HIP(hipMemcpyAsync(&nr, rcount, 4, hipMemcpyDeviceToHost, s));
-            NBKD_HIP(hipStreamSynchronize(s));
-            if (stats) NBKD_HIP(hipMemcpyAsync(stats + 9, rcount, 4, hipMemcpyDeviceToDevice, s));
-            if (nr > 0) {
-                // positions -> kd order -> query ids
-                uint32_t *rs = (uint32_t *)t.ws.get(WS_RSORT, (size_t)nr * 12, s);
-                if (!rs) return NBKD_ENOMEM;
-                int pbits = 1;
-                while (pbits < 32 && (1ull << pbits) < (uint64_t)mm) ++pbits;
-                const bool odd = nr > 1 && (((pbits + 7) / 8) & 1); // sorted keys in k1
-                uint32_t *rq = odd ? rs : rs + nr;
-                {
-                    TimedScope ts2("knn_retry_order", s);
-                    uint32_t *vdummy = nullptr;
-                    rc = radix_sort(t.ws, rlist, rs, rs + nr, rs + 2 * (size_t)nr, nr, pbits, s,
-                                    &vdummy);
-                    if (rc) return rc;
-                    gather_kernel<<<(nr + TB - 1) / TB, TB, 0, s>>>(odd ? rs + nr : rlist, nr, ord,
-                                                                   rq);
-                    NBKD_HIP(hipGetLastError());
-                }
-                // packets pay off only where failures are dense enough to be
-                // coherent (clustered inputs: ~4% of queries; uniform: ~0.02%,
-                // 2.3 ms as packets of 64 vs 0.4 ms one per wave).  Crossover
-                // at 1e8 uniform (r02bi): 82 k failures 1.1 ms one per wave vs
-                // 1.9 as packets, 307 k 3.0 vs 2.0: packets from 1/512.
-                static const int force_qpp = [] { // NBKD_RETRY_QPP=1|64: A/B only
-                    const char *e = knob("NBKD_RETRY_QPP");
-                    return e ? atoi(e) : 0;
-                }();
-                const uint32_t rqpp = force_qpp == 1 || force_qpp == 64
-                                          ? (uint32_t)force_qpp
-                                          : ((uint64_t)nr * 512u >= (uint64_t)mm ? 64u : 1u);
-                const uint32_t capr = collect_capacity(k) * 8u;
-                uint64_t rb = budget / ((uint64_t)capr * 8u) / 64u * 64u;
-                rb = std::max<uint64_t>(std::min<uint64_t>(rb, ((uint64_t)nr + 63) / 64 * 64), 64);
-                uint2 *rcand = (uint2 *)t.ws.get(WS_CAND, rb * capr * 8u, s);
-                uint32_t *rcc = (uint32_t *)t.ws.get(WS_CCOUNT, rb * 4u, s);
-                if (!rcand || !rcc) return NBKD_ENOMEM;
-                // adaptive: the retry's failures (query ids) go to rlist for a
-                // second round; rlist's sorted positions were consumed by the
-                // gather above (stream order)
-                const bool second = retry_adaptive();
-                if (second) NBKD_HIP(hipMemsetAsync(rcount, 0, 4, s));
-                for (uint64_t b0 = 0; b0 < nr; b0 += rb) {
-                    const uint32_t nb = (uint32_t)std::min<uint64_t>(rb, nr - b0);
-                    rc = launch_knn_collect(t, dq, rq + b0, nb, k, tg, second ? 1.0f : 4.0f,
-                                            rqpp, rcand, capr, rcc, dd, di,
-                                            second ? rlist : list, second ? rcount : count,
-                                            0xFFFFFFFFu, true, second, sq, kb, nullptr, s);
+            {
+                TimedScope ts2("knn_retry_order", s);
+                rc = compact_failures(t.ws, bits, mm, ord, rq, rq_count, s);
+                if (rc) return rc;
+            }
+            if (stats) NBKD_HIP(hipMemcpyAsync(stats + 9, rq_count, 4, hipMemcpyDeviceToDevice, s));
+            // round 1: the failures in kd order, as packets of 64 where they
+            // are dense (>= 1/512 of the queries, as on clustered inputs: a
+            // coherent walk) and one query per wave where they are sparse
+            // (uniform 1e8, r02bi: 82 k failures 1.1 ms one per wave vs 1.9 ms
+            // as packets); batches of rb up to ~10 % of the queries, the rest
+            // (never reached on the benchmark sets) straight to round 2
+            const uint32_t nb1 =
+                (uint32_t)std::min<uint64_t>(8, std::max<uint64_t>(1, ((uint64_t)mm / 10 + rb - 1) / rb));
+            for (uint32_t bi = 0; bi < nb1; ++bi) {
+                for (int mode = 1; mode <= 2; ++mode) {
+                    const QSpan sp{(uint32_t)cap1, rq_count, (uint32_t)(bi * rb), mm, mode};
+                    rc = launch_knn_collect(t, dq, rq + bi * rb, sp, k, tg, adaptive ? 1.0f : 4.0f,
+                                            mode == 1 ? 64u : 1u, cand, capr, ccount, dd, di,
+                                            adaptive ? r2 : list, adaptive ? r2_count : count,
+                                            nullptr, 0xFFFFFFFFu, true, adaptive, sq, kb, nullptr, s);
                     if (rc) return rc;
                 }
-                uint32_t nr2 = 0;
-                if (second) {
-                    NBKD_HIP(hipMemcpyAsync(&nr2, rcount, 4, hipMemcpyDeviceToHost, s));
-                    NBKD_HIP(hipStreamSynchronize(s));
+            }
+            {
+                TimedScope ts3("knn_retry", s);
+                spill_kernel<<<64, TB, 0, s>>>(rq, rq_count, (uint32_t)std::min<uint64_t>(nb1 * rb, mm64),
+                                               adaptive ? r2 : list, adaptive ? r2_count : count);
+                NBKD_HIP(hipGetLastError());
+            }
+            if (adaptive) {
+                // round 2, one query per wave: the seed each failure rewrote
+                // (2x..8x volume when short, the same seed when the 8x column
+                // overflowed) and a 64x column; what still fails joins the
+                // exact kernel's list
+                const uint32_t nb2 = (uint32_t)std::min<uint64_t>(
+                    4, std::max<uint64_t>(1, ((uint64_t)mm / 100 + rb2 - 1) / rb2));
+                for (uint32_t bi = 0; bi < nb2; ++bi) {
+                    const QSpan sp{(uint32_t)cap2, r2_count, (uint32_t)(bi * rb2), mm, 0};
+                    rc = launch_knn_collect(t, dq, r2 + bi * rb2, sp, k, tg, 1.0f, 1u, cand, capr2,
+                                            ccount, dd, di, list, count, nullptr, 0xFFFFFFFFu, true,
+                                            false, sq, kb, nullptr, s);
+                    if (rc) return rc;
                 }
-                if (nr2 > 0) {
-                    // second round, one query per wave: the seed each failure
-                    // rewrote (2x..8x volume when short, same seed when the 8x
-                    // column overflowed) and a 64x column; what still fails
-                    // joins the exact kernel's list
-                    const uint32_t capr2 = collect_capacity(k) * 64u;
-                    uint64_t rb2 = std::max<uint64_t>(budget / ((uint64_t)capr2 * 8u), 64);
-                    rb2 = std::min<uint64_t>(rb2, nr2);
-                    uint2 *rcand2 = (uint2 *)t.ws.get(WS_CAND, rb2 * capr2 * 8u, s);
-                    uint32_t *rcc2 = (uint32_t *)t.ws.get(WS_CCOUNT, rb2 * 4u, s);
-                    if (!rcand2 || !rcc2) return NBKD_ENOMEM;
-                    for (uint64_t b0 = 0; b0 < nr2; b0 += rb2) {
-                        const uint32_t nb = (uint32_t)std::min<uint64_t>(rb2, nr2 - b0);
-                        rc = launch_knn_collect(t, dq, rlist + b0, nb, k, tg, 1.0f, 1u, rcand2,
-                                                capr2, rcc2, dd, di, list, count, 0xFFFFFFFFu,
-                                                true, false, sq, kb, nullptr, s);
-                        if (rc) return rc;
-                    }
-                }
+                TimedScope ts4("knn_retry", s);
+                spill_kernel<<<64, TB, 0, s>>>(r2, r2_count, (uint32_t)std::min<uint64_t>(nb2 * rb2, mm),
+                                               list, count);
+                NBKD_HIP(hipGetLastError());
             }
         } else {
 #ifdef NBKD_EXPERIMENTS

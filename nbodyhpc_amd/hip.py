@@ -35,6 +35,7 @@ def _hip():
         L.hipStreamCreate.argtypes = [ctypes.POINTER(vp)]
         L.hipStreamDestroy.argtypes = [vp]
         L.hipStreamSynchronize.argtypes = [vp]
+        L.hipStreamQuery.argtypes = [vp]
         L.hipEventCreate.argtypes = [ctypes.POINTER(vp)]
         L.hipEventDestroy.argtypes = [vp]
         L.hipEventRecord.argtypes = [vp, vp]
@@ -132,6 +133,14 @@ class Stream:
 
     def synchronize(self):
         _ok(_hip().hipStreamSynchronize(self.handle), "hipStreamSynchronize")
+
+    def busy(self) -> bool:
+        """hipStreamQuery: True while work enqueued on the stream is pending."""
+        rc = _hip().hipStreamQuery(self.handle)
+        if rc == 600:  # hipErrorNotReady
+            return True
+        _ok(rc, "hipStreamQuery")
+        return False
 
 
 class Event:

@@ -496,3 +496,41 @@ def test_device_queries_on_two_streams(gpu, oracle):
     for q, od, oi in outs:
         dr, ir = o.query(q, k, workers=8)
         assert_knn_equal(od.numpy(), oi.numpy(), dr, ir, pts, q, 1.0)
+
+
+def test_device_output_queries_are_asynchronous(gpu, oracle):
+    """NBKD_OUTPUT_DEVICE kNN calls only enqueue (nbkd.h): the seed-failure
+    re-walk runs on device-counted grids, so no call waits for the device.
+    Two calls on one stream both return while the stream is still busy, and
+    both results are exact (a tiny seed margin makes most queries take the
+    re-walk rounds too)."""
+    from nbodyhpc_amd import hip
+    pts = uniform(2_000_000, 91)
+    q2 = uniform(2_000_000, 92)
+    t = gpu.Tree(pts, leafsize=64, boxsize=1.0)
+    k = 32
+    s = hip.Stream()
+    dp, dq = hip.DeviceArray.from_numpy(pts), hip.DeviceArray.from_numpy(q2)
+    outs = [(hip.DeviceArray((len(pts), k), np.float32), hip.DeviceArray((len(pts), k), np.uint32))
+            for _ in range(2)]
+    saved = gpu.get_tuning("knn_seed_margin")
+    try:
+        for margin in (3.5, 0.05):
+            gpu.set_tuning("knn_seed_margin", margin)
+            t.query_device(dp.ptr, len(pts), k, outs[0][0].ptr, outs[0][1].ptr, s.handle)  # warm
+            s.synchronize()
+            busy = []
+            for (od, oi), src in zip(outs, (dp, dq)):
+                t.query_device(src.ptr, len(pts), k, od.ptr, oi.ptr, s.handle)
+                busy.append(s.busy())
+            s.synchronize()
+            assert all(busy), busy
+            o = oracle.tree(pts, 64, 1.0)
+            rng = np.random.Generator(np.random.PCG64(93))
+            sel = np.sort(rng.choice(len(pts), 20_000, replace=False))
+            for (od, oi), host_q in zip(outs, (pts, q2)):
+                d, i = od.numpy()[sel], oi.numpy()[sel]
+                dr, ir = o.query(host_q[sel], k, workers=8)
+                assert_knn_equal(d, i, dr, ir, pts, host_q[sel], 1.0)
+    finally:
+        gpu.set_tuning("knn_seed_margin", saved)
