@@ -653,7 +653,61 @@ __device__ __forceinline__ void grp_packet(const DevTree &t, const float *__rest
 #undef NBKD_PH
 }
 
-template <bool PER, int OCC, bool STATS>
+// one packet of the collect pass
+template <bool PER, bool STATS>
+__device__ __forceinline__ void collect_packet(
+    const DevTree &t, const float *__restrict__ ginfo, const uint32_t *__restrict__ linfo,
+    const float *__restrict__ hinfo, const float *__restrict__ q, const uint32_t *__restrict__ order,
+    uint32_t m, int kq, const float *__restrict__ tg, float seed_mul, uint32_t qpp,
+    uint2 *__restrict__ cand, uint32_t capg, uint32_t *__restrict__ ccount,
+    unsigned long long *__restrict__ stats, float *__restrict__ kbound, CollectLdsG &W, int lane,
+    uint32_t pk) {
+    const uint32_t gq = pk * qpp + lane;
+    const bool valid = (uint32_t)lane < qpp && gq < m;
+    const uint32_t qo = valid ? order[gq] : 0u;
+    const float qx = valid ? q[3 * (size_t)qo] : 0.0f;
+    const float qy = valid ? q[3 * (size_t)qo + 1] : 0.0f;
+    const float qz = valid ? q[3 * (size_t)qo + 2] : 0.0f;
+    const float seed = valid ? fminf(tg[qo] * seed_mul, FLT_MAX) : -INFINITY;
+    const bool fin = seed < FLT_MAX && seed >= 1e-30f;
+    const float s_over_nb = fin ? seed * (1.0f / NB) : (seed > 0.0f ? INFINITY : 0.0f);
+    const float nb_over_s = fin ? (float)NB / seed * 1.00000095367431640625f : 0.0f;
+#pragma unroll
+    for (int w = 0; w < NB / 4; ++w) W.hist[w][lane] = 0u;
+    uint2 *const col = cand + (size_t)pk * qpp * capg;
+    uint32_t cnt = 0;
+    uint64_t st[13] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    float kth = seed;
+    grp_packet<PER, PER, STATS>(t, ginfo, linfo, hinfo, W, lane, qx, qy, qz, kth, s_over_nb,
+                                nb_over_s, col, qpp, capg, kq, cnt, st);
+    if (valid) ccount[gq] = cnt;
+    // the final bound: at least k candidates lie strictly below it (bound
+    // histogram), so none at or above it is among the k smallest
+    if (valid && kbound) kbound[gq] = kth;
+    if (STATS && lane == 0) {
+        atomicAdd(&stats[0], (unsigned long long)st[0]);
+        atomicAdd(&stats[1], (unsigned long long)st[5]);
+        atomicAdd(&stats[2], (unsigned long long)st[3]);
+        atomicAdd(&stats[3], (unsigned long long)st[4]);
+        atomicAdd(&stats[4], (unsigned long long)st[2]);
+        atomicAdd(&stats[5], 1ull);
+        atomicAdd(&stats[7], (unsigned long long)st[1]);
+#pragma unroll
+        for (int i = 0; i < 6; ++i) atomicAdd(&stats[10 + i], (unsigned long long)st[6 + i]);
+        atomicAdd(&stats[16], (unsigned long long)st[12]);
+    }
+    if (STATS) {
+        uint32_t c = valid ? cnt : 0u;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+        if (lane == 0) atomicAdd(&stats[6], (unsigned long long)c);
+    }
+}
+
+// A static pass launches one wave per packet; a device-counted pass (the
+// retry rounds: LOOP) a fixed grid that strides over its packets.  Only the
+// LOOP instance carries the loop (in the first pass it cost a 12-28 B spill).
+template <bool PER, int OCC, bool STATS, bool LOOP>
 __global__ void __launch_bounds__(TB, OCC)
 knn_collect_grp_kernel(DevTree t, const float *__restrict__ ginfo,
                        const uint32_t *__restrict__ linfo, const float *__restrict__ hinfo,
@@ -666,53 +720,20 @@ knn_collect_grp_kernel(DevTree t, const float *__restrict__ ginfo,
     __shared__ CollectLdsG Wl[WPB];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     CollectLdsG &W = Wl[wave];
-    // packets pk < npk; a static pass launches one wave per packet, a device-
-    // counted pass (retry rounds) a fixed grid that strides over them
     const uint32_t m = span_m(span);
     const uint32_t npk = (m + qpp - 1) / qpp;
     const uint32_t bid = xcd ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
-    for (uint32_t pk = bid * WPB + wave; pk < npk; pk += gridDim.x * WPB) {
-        const uint32_t gq = pk * qpp + lane;
-        const bool valid = (uint32_t)lane < qpp && gq < m;
-        const uint32_t qo = valid ? order[gq] : 0u;
-        const float qx = valid ? q[3 * (size_t)qo] : 0.0f;
-        const float qy = valid ? q[3 * (size_t)qo + 1] : 0.0f;
-        const float qz = valid ? q[3 * (size_t)qo + 2] : 0.0f;
-        const float seed = valid ? fminf(tg[qo] * seed_mul, FLT_MAX) : -INFINITY;
-        const bool fin = seed < FLT_MAX && seed >= 1e-30f;
-        const float s_over_nb = fin ? seed * (1.0f / NB) : (seed > 0.0f ? INFINITY : 0.0f);
-        const float nb_over_s = fin ? (float)NB / seed * 1.00000095367431640625f : 0.0f;
-        wave_sync(); // the previous packet's LDS reads are done
-#pragma unroll
-        for (int w = 0; w < NB / 4; ++w) W.hist[w][lane] = 0u;
-        uint2 *const col = cand + (size_t)pk * qpp * capg;
-        uint32_t cnt = 0;
-        uint64_t st[13] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-        float kth = seed;
-        grp_packet<PER, PER, STATS>(t, ginfo, linfo, hinfo, W, lane, qx, qy, qz, kth, s_over_nb,
-                                    nb_over_s, col, qpp, capg, kq, cnt, st);
-        if (valid) ccount[gq] = cnt;
-        // the final bound: at least k candidates lie strictly below it (bound
-        // histogram), so none at or above it is among the k smallest
-        if (valid && kbound) kbound[gq] = kth;
-        if (STATS && lane == 0) {
-            atomicAdd(&stats[0], (unsigned long long)st[0]);
-            atomicAdd(&stats[1], (unsigned long long)st[5]);
-            atomicAdd(&stats[2], (unsigned long long)st[3]);
-            atomicAdd(&stats[3], (unsigned long long)st[4]);
-            atomicAdd(&stats[4], (unsigned long long)st[2]);
-            atomicAdd(&stats[5], 1ull);
-            atomicAdd(&stats[7], (unsigned long long)st[1]);
-#pragma unroll
-            for (int i = 0; i < 6; ++i) atomicAdd(&stats[10 + i], (unsigned long long)st[6 + i]);
-            atomicAdd(&stats[16], (unsigned long long)st[12]);
+    if constexpr (LOOP) {
+        for (uint32_t pk = bid * WPB + wave; pk < npk; pk += gridDim.x * WPB) {
+            wave_sync(); // the previous packet's LDS reads are done
+            collect_packet<PER, STATS>(t, ginfo, linfo, hinfo, q, order, m, kq, tg, seed_mul, qpp,
+                                       cand, capg, ccount, stats, kbound, W, lane, pk);
         }
-        if (STATS) {
-            uint32_t c = valid ? cnt : 0u;
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
-            if (lane == 0) atomicAdd(&stats[6], (unsigned long long)c);
-        }
+    } else {
+        const uint32_t pk = bid * WPB + wave;
+        if (pk < npk)
+            collect_packet<PER, STATS>(t, ginfo, linfo, hinfo, q, order, m, kq, tg, seed_mul, qpp,
+                                       cand, capg, ccount, stats, kbound, W, lane, pk);
     }
 }
 
@@ -765,12 +786,12 @@ knn_select_kernel(DevTree t, const float *__restrict__ q, const uint32_t *__rest
     __shared__ uint32_t rowq_all[WPB][64];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     uint32_t *stage = stage_all[wave], *rowq = rowq_all[wave];
+    // a device-counted pass (retry rounds) is launched for its cap and reads
+    // its count here (a loop over blocks made the compiler spill td / ti)
     const uint32_t m = span_m(span);
-    // lane = one query gq; its candidates: packet gq / qpp, row gq % qpp.  A
-    // device-counted pass (retry rounds) strides its fixed grid over the blocks
-    for (uint32_t wb = blockIdx.x * WPB + wave; wb * 64u < m; wb += gridDim.x * WPB) {
-    __builtin_amdgcn_s_waitcnt(0xC07F); // lgkmcnt(0): the previous block's LDS reads are done
-    wave_sync();
+    const uint32_t wb = blockIdx.x * WPB + wave;
+    if (wb * 64u >= m) return;
+    // lane = one query gq; its candidates: packet gq / qpp, row gq % qpp
     const uint32_t gq = wb * 64u + lane;
     const bool valid = gq < m;
     const uint32_t qo = valid ? order[gq] : 0u;
@@ -870,7 +891,7 @@ knn_select_kernel(DevTree t, const float *__restrict__ q, const uint32_t *__rest
 
     if (out_i == nullptr) { // k-th distance only (nbkd_query_kth): column k-1
         if (valid) out_d[qo] = sq ? td[KC - 1] : sqrtf(td[KC - 1]);
-        continue;
+        return;
     }
     rowq[lane] = valid ? qo : 0xFFFFFFFFu;
 #pragma unroll
@@ -896,7 +917,6 @@ knn_select_kernel(DevTree t, const float *__restrict__ q, const uint32_t *__rest
         for (int j = 0; j < CC; ++j) stage[j * 64 + (lane ^ j)] = ti[j0 + j];
         wave_sync();
         store_rows<CC>(stage, rowq, out_i, k, j0 - (KC - k), lane);
-    }
     }
 }
 
@@ -1248,12 +1268,16 @@ void launch_collect(const Tree &t, const float *q, const uint32_t *order, QSpan 
             return !(e && atoi(e) == 0);
         }();
         TimedScope ts(name, s);
-        if (stats)
-            knn_collect_grp_kernel<PER, 8, true><<<blocks, TB, 0, s>>>(
+        if (span.count)
+            knn_collect_grp_kernel<PER, 8, false, true><<<blocks, TB, 0, s>>>(
+                view(t), t.ginfo, t.leafinfo, t.hinfo, q, order, span, k, tg, seed_mul, qpp, cand,
+                capg, ccount, nullptr, false, kbound);
+        else if (stats)
+            knn_collect_grp_kernel<PER, 8, true, false><<<blocks, TB, 0, s>>>(
                 view(t), t.ginfo, t.leafinfo, t.hinfo, q, order, span, k, tg, seed_mul, qpp, cand,
                 capg, ccount, stats, xcd && !span.count, kbound);
         else
-            knn_collect_grp_kernel<PER, 8, false><<<blocks, TB, 0, s>>>(
+            knn_collect_grp_kernel<PER, 8, false, false><<<blocks, TB, 0, s>>>(
                 view(t), t.ginfo, t.leafinfo, t.hinfo, q, order, span, k, tg, seed_mul, qpp, cand,
                 capg, ccount, nullptr, xcd && !span.count, kbound);
         return;
@@ -1329,8 +1353,7 @@ void launch_select(const Tree &t, const float *q, const uint32_t *order, QSpan s
                    float *od, uint32_t *oi, uint32_t *fail_list, uint32_t *fail_count,
                    uint32_t *fail_bits, uint32_t pos_base, float *tg_fix, float mu, bool sq,
                    hipStream_t s) {
-    const unsigned need = (span.m + TB - 1) / TB;
-    const unsigned blocks = span.count ? std::min(need, resident_blocks()) : need;
+    const unsigned blocks = (span.m + TB - 1) / TB; // device-counted: sized by the cap
     static const uint64_t all_rows = [] { // NBKD_SELECT_ROWMASK=0: read whole blocks
         const char *e = knob("NBKD_SELECT_ROWMASK");
         return (e && atoi(e) == 0) ? ~0ull : 0ull;
