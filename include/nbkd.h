@@ -14,10 +14,10 @@
  * null stream).  With host outputs a call returns after the results are
  * copied back.  With device outputs nbkd_query_knn / nbkd_query_kth return once
  * the work is enqueued (the re-walk of the queries whose seed ball held fewer
- * than k points runs on grids that read the failure count on the device);
- * nbkd_query_ball_count on a periodic tree waits on `stream` once, to count the
- * queries outside [0, L]^3.  The first call of a tree, or one needing more
- * scratch than any before it, may also wait while the scratch grows.  Calls on
+ * than k points runs on grids that read the failure count on the device), and
+ * so does nbkd_query_ball_count.  nbkd_query_ball_csr waits (its offsets are
+ * host memory), and the first call of a tree, or one needing more scratch than
+ * any before it, may also wait while the scratch grows.  Calls on
  * one tree are serialised, and a call on another stream first waits for the
  * tree's previous call to finish on the device (the tree's scratch memory is
  * reused).

@@ -233,7 +233,47 @@ __global__ void ball_zero_kernel(const uint32_t *__restrict__ list, uint32_t nou
     if (fill) fill[j] = 0;
 }
 
+// the same for a list whose length is in device memory (count mode): fixed
+// grids that stride over (query, point tile) pairs, so the host never reads it
+__global__ void __launch_bounds__(TB)
+ball_zero_dev_kernel(const uint32_t *__restrict__ list, const uint32_t *__restrict__ nout,
+                     uint32_t *__restrict__ out_count) {
+    const uint32_t c = *nout;
+    for (uint32_t j = blockIdx.x * TB + threadIdx.x; j < c; j += gridDim.x * TB)
+        out_count[list[j]] = 0;
+}
+
+__global__ void __launch_bounds__(TB)
+ball_brute_dev_kernel(DevTree t, const float *__restrict__ q, const uint32_t *__restrict__ list,
+                      const uint32_t *__restrict__ nout, uint32_t ntiles, float r2,
+                      uint32_t *__restrict__ out_count) {
+    const uint64_t total = (uint64_t)__builtin_amdgcn_readfirstlane(*nout) * ntiles;
+    const float L = t.box;
+    for (uint64_t w = blockIdx.x; w < total; w += gridDim.x) {
+        const uint32_t j = (uint32_t)(w / ntiles), tile = (uint32_t)(w - (uint64_t)j * ntiles);
+        const uint32_t qo = list[j];
+        const float qx = q[3 * (size_t)qo], qy = q[3 * (size_t)qo + 1], qz = q[3 * (size_t)qo + 2];
+        uint32_t c = 0;
+        const uint32_t base = tile * (uint32_t)(TB * BR_ITEMS) + threadIdx.x;
+#pragma unroll
+        for (int u = 0; u < BR_ITEMS; ++u) {
+            const uint32_t p = base + u * TB;
+            if (p < t.n8 && point_d2<true>(qx, qy, qz, t.x[p], t.y[p], t.z[p], L) <= r2) ++c;
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+        if ((threadIdx.x & 63) == 0 && c) atomicAdd(&out_count[qo], c);
+    }
+}
+
 } // namespace
+
+void launch_ball_outside_dev(const Tree &t, const float *q, const uint32_t *list,
+                             const uint32_t *nout, float r2, uint32_t *out_count, hipStream_t s) {
+    const uint32_t ntiles = (uint32_t)((t.n8 + TB * BR_ITEMS - 1) / (TB * BR_ITEMS));
+    ball_zero_dev_kernel<<<64, TB, 0, s>>>(list, nout, out_count);
+    ball_brute_dev_kernel<<<2048, TB, 0, s>>>(view(t), q, list, nout, ntiles, r2, out_count);
+}
 
 void launch_ball_outside(const Tree &t, const float *q, const uint32_t *list, uint32_t nout,
                          float r2, uint32_t *out_count, uint32_t *fill,

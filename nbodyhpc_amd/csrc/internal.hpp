@@ -243,6 +243,9 @@ void launch_ball_packet(const Tree &t, const float *q, const uint32_t *order, ui
                         hipStream_t s);
 // the listed periodic queries outside [0, L]^3, every point tested (fill: nout
 // zeroed scratch words when out_idx is set)
+// count mode with the list's length in device memory (no host read)
+void launch_ball_outside_dev(const Tree &t, const float *q, const uint32_t *list,
+                             const uint32_t *nout, float r2, uint32_t *out_count, hipStream_t s);
 void launch_ball_outside(const Tree &t, const float *q, const uint32_t *list, uint32_t nout,
                          float r2, uint32_t *out_count, uint32_t *fill,
                          const uint64_t *row_offsets, uint32_t *out_idx, hipStream_t s);

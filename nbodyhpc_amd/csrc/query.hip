@@ -1220,19 +1220,27 @@ static nbkd_status ball_common(const Tree &t, const float *q, uint64_t m, float 
     rc = sort_queries(t, dq, mm, ord, s);
     if (rc) return rc;
     const float r2 = r * r;
-    // periodic queries outside [0, L]^3: listed, every point tested for them
+    // periodic queries outside [0, L]^3: listed, every point tested for them.
+    // Count mode reads the list's length on the device; the CSR fill (host
+    // offsets anyway) reads it here
     uint32_t *list = nullptr, nout = 0;
+    const bool count_only = offsets == nullptr;
     if (t.periodic) {
         list = (uint32_t *)t.ws.get(WS_LIST, (size_t)mm * 8 + 16, s);
         if (!list) return NBKD_ENOMEM;
         NBKD_HIP(hipMemsetAsync(list + mm, 0, 4, s));
         outside_box_kernel<<<(mm + TB - 1) / TB, TB, 0, s>>>(dq, mm, t.box, list, list + mm);
-        NBKD_HIP(hipMemcpyAsync(&nout, list + mm, 4, hipMemcpyDeviceToHost, s));
-        NBKD_HIP(hipStreamSynchronize(s));
+        if (!count_only) {
+            NBKD_HIP(hipMemcpyAsync(&nout, list + mm, 4, hipMemcpyDeviceToHost, s));
+            NBKD_HIP(hipStreamSynchronize(s));
+        }
     }
     auto run = [&](uint32_t *c, const uint64_t *off, uint32_t *idx) -> nbkd_status {
         launch_ball_packet(t, dq, ord, mm, r2, c, off, idx, s);
-        launch_ball_outside(t, dq, list, nout, r2, c, list + mm + 4, off, idx, s);
+        if (count_only && list)
+            launch_ball_outside_dev(t, dq, list, list + mm, r2, c, s);
+        else
+            launch_ball_outside(t, dq, list, nout, r2, c, list + mm + 4, off, idx, s);
         NBKD_HIP(hipGetLastError());
         return NBKD_OK;
     };
