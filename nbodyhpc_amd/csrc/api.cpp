@@ -96,14 +96,71 @@ void release_idle_blocks(int dev) {
     }
 }
 
+namespace {
+thread_local std::vector<const void *> t_held;
+struct WsList {
+    std::mutex mu;
+    std::vector<Workspace *> all;
+};
+WsList &ws_list() {
+    static WsList *l = new WsList(); // never destroyed: workspaces outlive statics
+    return *l;
+}
+} // namespace
+
+void hold_mark(const void *p) { t_held.push_back(p); }
+void hold_unmark(const void *p) {
+    for (size_t i = t_held.size(); i-- > 0;)
+        if (t_held[i] == p) {
+            t_held.erase(t_held.begin() + (std::ptrdiff_t)i);
+            return;
+        }
+}
+bool held_here(const void *p) {
+    for (const void *h : t_held)
+        if (h == p) return true;
+    return false;
+}
+
+Workspace::Workspace() {
+    WsList &l = ws_list();
+    std::lock_guard<std::mutex> g(l.mu);
+    l.all.push_back(this);
+}
+
+Workspace::~Workspace() {
+    WsList &l = ws_list();
+    std::lock_guard<std::mutex> g(l.mu);
+    for (size_t i = 0; i < l.all.size(); ++i)
+        if (l.all[i] == this) {
+            l.all[i] = l.all.back();
+            l.all.pop_back();
+            break;
+        }
+}
+
+// the idle workspaces of `dev` (no call holds them) give their slots back;
+// try_lock only, so a call in flight on another thread is never waited for
+static void trim_idle_workspaces(int dev) {
+    WsList &l = ws_list();
+    std::lock_guard<std::mutex> g(l.mu);
+    for (Workspace *w : l.all) {
+        if (w->dev != dev || held_here(w) || !w->mu.try_lock()) continue;
+        w->trim();
+        w->mu.unlock();
+    }
+}
+
 hipError_t malloc_or_release(void **p, size_t bytes) {
     hipError_t e = hipMalloc(p, bytes);
     if (e != hipErrorOutOfMemory) return e;
-    // the device's idle cached blocks go back to the driver, then one retry
+    // what the device holds idle goes back to the driver, then one retry
     (void)hipGetLastError();
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return e;
     release_idle_blocks(dev);
+    release_idle_build_scratch(dev);
+    trim_idle_workspaces(dev);
     return hipMalloc(p, bytes);
 }
 
@@ -525,6 +582,10 @@ void *Workspace::get(int slot, size_t bytes, hipStream_t s) {
         cap[slot] = 0;
     }
     size_t want = bytes + bytes / 8; // some headroom for the next, slightly larger call
+    if (dev < 0 && hipGetDevice(&dev) != hipSuccess) {
+        (void)hipGetLastError();
+        dev = -1;
+    }
     hipError_t e = malloc_or_release(&p[slot], want);
     if (e != hipSuccess) {
         (void)hip_fail(e, "hipMalloc(workspace)");
@@ -544,6 +605,16 @@ void Workspace::release() {
     if (done) (void)hipEventDestroy(done);
     done = nullptr;
     used = false;
+}
+
+void Workspace::trim() {
+    if (used && done) (void)hipEventSynchronize(done);
+    for (int i = 0; i < WS_NSLOTS; ++i) {
+        if (p[i]) (void)hipFree(p[i]);
+        p[i] = nullptr;
+        cap[i] = 0;
+    }
+    (void)hipGetLastError();
 }
 
 hipError_t Workspace::enter(hipStream_t s) {

@@ -1245,6 +1245,21 @@ BuildScratch &build_scratch(int dev) {
     return pool[dev & 63];
 }
 
+} // namespace
+
+void release_idle_build_scratch(int dev) {
+    BuildScratch &b = build_scratch(dev);
+    if (held_here(&b) || !b.mu.try_lock()) return;
+    // unlocked scratch has no kernel in flight (the lock outlives the stream)
+    if (b.p) (void)hipFree(b.p);
+    b.p = nullptr;
+    b.bytes = 0;
+    b.shape.uploaded = false;
+    b.mu.unlock();
+}
+
+namespace {
+
 struct Carve {
     size_t off = 0;
     size_t take(size_t b) {
@@ -1292,9 +1307,13 @@ nbkd_status build_tree(Tree &t, const float *xyz, uint64_t n, int32_t leaf_size,
     struct ScratchLock {
         BuildScratch &b;
         hipStream_t s;
-        ScratchLock(BuildScratch &b_, hipStream_t s_) : b(b_), s(s_) { b.mu.lock(); }
+        ScratchLock(BuildScratch &b_, hipStream_t s_) : b(b_), s(s_) {
+            b.mu.lock();
+            hold_mark(&b);
+        }
         ~ScratchLock() {
             (void)hipStreamSynchronize(s);
+            hold_unmark(&b);
             b.mu.unlock();
         }
     } scr_lock(scr, s);

@@ -25,6 +25,7 @@ struct Workspace {
     std::mutex mu;
     void *p[WS_NSLOTS] = {};
     size_t cap[WS_NSLOTS] = {};
+    int dev = -1; // device of the slots (set when one is allocated)
     // the last call's stream and an event recorded at its end: a call on
     // another stream first waits for it on the device (enter), since its
     // kernels may still read or write the slots when the host call returned
@@ -34,9 +35,22 @@ struct Workspace {
     // returns nullptr on failure (hip error recorded via set_error)
     void *get(int slot, size_t bytes, hipStream_t s);
     void release();
+    void trim(); // with mu held: wait for the last call, free every slot
+    // every workspace is listed (api.cpp) so that an out-of-memory retry can
+    // trim the idle ones of its device
+    Workspace();
+    ~Workspace();
+    Workspace(const Workspace &) = delete;
+    Workspace &operator=(const Workspace &) = delete;
     hipError_t enter(hipStream_t s); // with mu held, before the first enqueue
     void leave(hipStream_t s);       // with mu held, after the last enqueue
 };
+
+// scratch this thread holds locked (a workspace, the build scratch): the
+// out-of-memory retry leaves it alone (its try_lock would be the owner's)
+void hold_mark(const void *p);
+void hold_unmark(const void *p);
+bool held_here(const void *p);
 
 // one call's use of a workspace: lock, order after the previous call, record the end
 struct WsCall {
@@ -44,8 +58,14 @@ struct WsCall {
     Workspace &w;
     hipStream_t s;
     hipError_t err;
-    WsCall(Workspace &w_, hipStream_t s_) : lk(w_.mu), w(w_), s(s_) { err = w.enter(s); }
-    ~WsCall() { w.leave(s); }
+    WsCall(Workspace &w_, hipStream_t s_) : lk(w_.mu), w(w_), s(s_) {
+        hold_mark(&w);
+        err = w.enter(s);
+    }
+    ~WsCall() {
+        w.leave(s);
+        hold_unmark(&w);
+    }
 };
 
 constexpr int NBKD_PAD_LEAVES = 8;
@@ -147,10 +167,12 @@ bool stats_enabled();
 constexpr int NBKD_NSTATS = 17; // see capi.STATS_NAMES (collect kernel) + exact-kernel and retried queries
 void stats_store(const uint64_t *v);
 
-// hipMalloc that, when the device is out of memory, first returns the
-// device's idle cached tree blocks (api.cpp, tree_malloc) and retries once; the
-// query workspace, the build scratch and DevBuf allocate through it
+// hipMalloc that, when the device is out of memory, first returns what the
+// device holds idle -- the cached tree blocks (api.cpp, tree_malloc), the build
+// scratch and every workspace no call holds -- and retries once; the query
+// workspace, the build scratch and DevBuf allocate through it
 hipError_t malloc_or_release(void **p, size_t bytes);
+void release_idle_build_scratch(int dev); // build.hip
 
 // RAII device allocation (plain hipMalloc; freed after the stream drained).
 // The stream-ordered pool (hipMallocAsync) is deliberately not used: mixing it

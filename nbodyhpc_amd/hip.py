@@ -29,6 +29,7 @@ def _hip():
         L.hipFree.argtypes = [vp]
         L.hipMemcpy.argtypes = [vp, vp, sz, ctypes.c_int]
         L.hipMemset.argtypes = [vp, ctypes.c_int, sz]
+        L.hipMemGetInfo.argtypes = [ctypes.POINTER(sz), ctypes.POINTER(sz)]
         L.hipDeviceSynchronize.argtypes = []
         L.hipSetDevice.argtypes = [ctypes.c_int]
         L.hipGetDeviceCount.argtypes = [ctypes.POINTER(ctypes.c_int)]
@@ -75,6 +76,13 @@ def set_device(d: int):
 
 def synchronize():
     _ok(_hip().hipDeviceSynchronize(), "hipDeviceSynchronize")
+
+
+def mem_info():
+    """(free, total) bytes of the current device (hipMemGetInfo)."""
+    f, t = ctypes.c_size_t(), ctypes.c_size_t()
+    _ok(_hip().hipMemGetInfo(ctypes.byref(f), ctypes.byref(t)), "hipMemGetInfo")
+    return int(f.value), int(t.value)
 
 
 class DeviceArray:
