@@ -415,6 +415,11 @@ def _sr_worker(rank, world, port, n, k, hscale, kind, outdir):
     try:
         if kind == "lognormal":
             xyz, ids, bounds = synth.lognormal_slab(n, rank, world, grid=16)
+        elif kind == "strong":
+            # bench.py's strong split: every rank draws the one-GPU set and
+            # keeps its own slab (ids = row numbers of synth.uniform)
+            xyz, ids = slab.gen_uniform_slab(n, 20261016, 1.0, rank, world)
+            bounds = slab.bounds_list(world, 1.0)
         else:
             xyz, ids = _slab_points(n // world, 17, rank, world)
             bounds = slab.bounds_list(world, 1.0)
@@ -444,7 +449,8 @@ def _sr_worker(rank, world, port, n, k, hscale, kind, outdir):
 @pytest.mark.parametrize("world,n,k,hscale,kind", [
     (2, 8000, 8, 0.05, "uniform"), (3, 9000, 8, 0.05, "uniform"),
     (4, 400, 48, 0.02, "uniform"),  # k-th radii wider than a slab: hops to the 2nd neighbour
-    (2, 12_000, 8, 0.1, "lognormal"), (3, 12_000, 16, 0.1, "lognormal")])
+    (2, 12_000, 8, 0.1, "lognormal"), (3, 12_000, 16, 0.1, "lognormal"),
+    (2, 20_000, 32, 1.0, "strong"), (3, 30_000, 32, 0.1, "strong")])
 def test_second_round_exchange_equals_single_tree(world, n, k, hscale, kind, tmp_path, oracle):
     """SURVEY.md §8(e)(3): with a thin halo many slab-local rows are not exact;
     after the second-round exchange every row equals the single-tree oracle
@@ -463,7 +469,13 @@ def test_second_round_exchange_equals_single_tree(world, n, k, hscale, kind, tmp
     pts = np.empty_like(allp)
     pts[ids] = allp  # global id order
     gd, gi = oracle.tree(pts, 16, 1.0).query(pts, k, workers=4)
-    assert sum(int(x["v0"]) for x in res) > 0  # the thin halo did leave rows inexact
+    if kind == "strong":
+        # the ranks' rows tile the one-GPU problem: every row of synth.uniform once
+        from nbodyhpc_amd import synth
+        assert np.array_equal(np.sort(ids), np.arange(n, dtype=np.uint32))
+        assert np.array_equal(pts, synth.uniform(n, 20261016, 1.0))
+    if hscale < 1.0:
+        assert sum(int(x["v0"]) for x in res) > 0  # the thin halo did leave rows inexact
     assert sum(int(x["fwd"]) for x in res) == sum(int(x["v0"]) for x in res)
     if world == 4:
         assert max(int(x["hops"]) for x in res) >= 2
