@@ -98,7 +98,7 @@ def _rank_points(n_per, rank, world):
     return xyz, ids
 
 
-def _worker(rank, world, port, n_per, k, outdir, rccl=False, hscale=1.0):
+def _worker(rank, world, port, n_per, k, outdir, rccl=False, hscale=1.0, same_gpu=False):
     from nbodyhpc_amd import capi, hip
 
     hip.preload()  # the ROCm 7.2 runtime must load before torch's bundled one
@@ -107,11 +107,11 @@ def _worker(rank, world, port, n_per, k, outdir, rccl=False, hscale=1.0):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    dev = rank if rccl else 0
+    dev = rank if (rccl and not same_gpu) else 0
     try:
         hip.set_device(dev)
         xyz, ids = _rank_points(n_per, rank, world)
-        comm = slab.init_comm(dist, rank, world, dev) if rccl else None
+        comm = slab.init_comm(dist, rank, world, dev, log=slab.log_stderr) if rccl else None
         if rccl and comm is None:
             raise RuntimeError("RCCL communicator did not start")
         ds = slab.DeviceSlab(xyz, ids, rank, world, 1.0, dev, dist, comm=comm)
@@ -144,7 +144,7 @@ def _worker(rank, world, port, n_per, k, outdir, rccl=False, hscale=1.0):
         dist.destroy_process_group()
 
 
-def _run_two_ranks(tmp_path, oracle, rccl, hscale=1.0):
+def _run_two_ranks(tmp_path, oracle, rccl, hscale=1.0, same_gpu=False):
     import multiprocessing as mp
 
     from tests.parity import assert_knn_equal
@@ -152,7 +152,7 @@ def _run_two_ranks(tmp_path, oracle, rccl, hscale=1.0):
     ctx = mp.get_context("spawn")  # plain multiprocessing: torch must not load first
     port = _free_port()
     procs = [ctx.Process(target=_worker, args=(r, world, port, n_per, k, str(tmp_path), rccl,
-                                               hscale))
+                                               hscale, same_gpu))
              for r in range(world)]
     for p in procs:
         p.start()
