@@ -849,7 +849,7 @@ def main():
         "traversal_per_query": {"distance_evals": pts_scanned / own,
                                 "candidates": st["candidates"] / own},
         "traversal_per_packet": {kk: st[kk] / max(st["packets"], 1)
-                                 for kk in ("node_visits", "dense_steps", "sparse_iters",
+                                 for kk in ("node_visits", "leaves_reached", "sparse_iters",
                                             "points_staged", "candidates", "leaves_scanned")},
         "lanes_per_scanned_chunk": st["chunk_lanes"] / max(st["leaves_scanned"], 1),
         "fallback_queries": st["fallback_queries"], "retry_queries": st["retry_queries"],

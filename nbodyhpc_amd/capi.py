@@ -301,7 +301,7 @@ def stats_read():
 # clocks (shader cycles summed over waves): tree walk, leaf staging wait, leaf
 # need test, dense scan, sparse scan, bound update; lanes needing a staged
 # chunk, summed over chunks
-STATS_NAMES = ("node_visits", "pair_evals", "dense_steps", "sparse_iters", "points_staged",
+STATS_NAMES = ("node_visits", "pair_evals", "leaves_reached", "sparse_iters", "points_staged",
                "packets", "candidates", "leaves_scanned", "fallback_queries", "retry_queries",
                "clk_walk", "clk_wait", "clk_leaf_test", "clk_dense", "clk_sparse", "clk_tighten",
                "chunk_lanes")

@@ -469,7 +469,7 @@ struct CollectLdsG {
         glds_f32((TBOX), W.tb, lane, 6);                                                           \
     } while (0)
 
-// st: node visits, leaves scanned, points staged, dense points, sparse
+// st: node visits, leaves scanned, points staged, leaves reached, sparse
 // iterations, pair evaluations, then 6 phase clocks, then lanes needing a
 // staged chunk summed over chunks (STATS only)
 template <bool PER, bool M, bool STATS>
@@ -514,6 +514,7 @@ __device__ __forceinline__ void grp_packet(const DevTree &t, const float *__rest
         bool ha;
         NBKD_GWALK(ha, pa, ea);
         if (!ha) break;
+        if constexpr (STATS) ++st[3]; // leaves reached (staged), needed by some lane or not
         // chunks: a leaf of 65..128 points is staged as its two halves, each
         // with its own tight box (hinfo); other leaves in runs of 64 points
         // under the leaf's tight box (leafinfo)

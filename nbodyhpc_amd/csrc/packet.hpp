@@ -112,6 +112,17 @@ __device__ __forceinline__ uint32_t lane_set(uint32_t old, uint32_t val, uint64_
     return r;
 }
 
+// The push's seven selects run only when the far child is pushed (a uniform
+// branch): collect 51.96 -> 50.65 ms at 1e8 against the branch-free form
+// (profiles/r03_ab1_collect_variants.txt); NBKD_CPUSH=0 restores it for A/B.
+#ifndef NBKD_CPUSH
+#define NBKD_CPUSH 1
+#endif
+#if NBKD_CPUSH
+#define NBKD_PUSH_IF(C) if (C)
+#else
+#define NBKD_PUSH_IF(C)
+#endif
 // one internal node with split axis D (compile-time): test both children for
 // every lane, push the far one when both are wanted, step into the near one
 // (the walk branches on the node's axis, so no per-lane selects pick the axis)
@@ -127,7 +138,7 @@ __device__ __forceinline__ uint32_t lane_set(uint32_t old, uint32_t val, uint64_
         const uint32_t right_votes = (uint32_t)__popcll(wm & __ballot(qd > split));                \
         const bool right_first = 2 * right_votes > (uint32_t)__popcll(wm);                         \
         const uint64_t wn = right_first ? wr : wl, wf = right_first ? wl : wr;                     \
-        {                                                                                          \
+        NBKD_PUSH_IF(wn != 0 && wf != 0) {                                                         \
             /* push the far child when both are wanted: far = left child [lo, split] if          \
                right_first, else right child [split, hi]; one v_cndmask per word */                \
             const bool push = wn != 0 && wf != 0;                                                  \
