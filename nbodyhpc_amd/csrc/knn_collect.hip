@@ -601,9 +601,11 @@ __device__ __forceinline__ void grp_packet(const DevTree &t, const float *__rest
                             const uint32_t j = d2_bucket(d, W.scl[qs]);
                             atomicAdd(&W.hist[j >> 2][owner], 1u << (8 * (j & 3)));
                             const uint32_t sl = atomicAdd(&W.cnt[owner], 1u);
-                            if (sl < capg)
-                                col[((sl >> 4) * qpp + owner) * 16u + (sl & 15u)] =
-                                    make_uint2(__float_as_uint(d), c0 + pi);
+                            // a row past capg is a failure whose column is never read (both
+                            // selects): its extra hits overwrite its last slot (no branch)
+                            const uint32_t sw = min(sl, capg - 1u);
+                            col[((sw >> 4) * qpp + owner) * 16u + (sw & 15u)] =
+                                make_uint2(__float_as_uint(d), c0 + pi);
                         }
                     }
                 }

@@ -112,20 +112,14 @@ __device__ __forceinline__ uint32_t lane_set(uint32_t old, uint32_t val, uint64_
     return r;
 }
 
-// The push's seven selects run only when the far child is pushed (a uniform
-// branch): collect 51.96 -> 50.65 ms at 1e8 against the branch-free form
-// (profiles/r03_ab1_collect_variants.txt); NBKD_CPUSH=0 restores it for A/B.
-#ifndef NBKD_CPUSH
-#define NBKD_CPUSH 1
-#endif
-#if NBKD_CPUSH
-#define NBKD_PUSH_IF(C) if (C)
-#else
-#define NBKD_PUSH_IF(C)
-#endif
 // one internal node with split axis D (compile-time): test both children for
-// every lane, push the far one when both are wanted, step into the near one
-// (the walk branches on the node's axis, so no per-lane selects pick the axis)
+// every lane; a single wanted child is entered, and only when both are wanted
+// the lanes vote which one is near (entered) and which far (pushed, its seven
+// selects under a uniform branch).  The walk branches on the node's axis, so
+// no per-lane selects pick the axis.  Against the form that voted and ran the
+// push's selects at every node: collect 51.96 -> 49.4 ms at 1e8 with
+// knn_collect's clamped stores (profiles/r03_ab1_collect_variants.txt,
+// r03_ab3_lazy_vote.txt), radius count 129.0 -> 126.1 ms (r03_ab2_push_ball.txt).
 #define NBKD_GSTEP(D)                                                                              \
     {                                                                                              \
         const float split = nd.split;                                                              \
@@ -135,24 +129,21 @@ __device__ __forceinline__ uint32_t lane_set(uint32_t old, uint32_t val, uint64_
         const float dl = (((D) == 0 ? tl : tm[0]) + ((D) == 1 ? tl : tm[1])) + ((D) == 2 ? tl : tm[2]); \
         const float dr = (((D) == 0 ? tr : tm[0]) + ((D) == 1 ? tr : tm[1])) + ((D) == 2 ? tr : tm[2]); \
         const uint64_t wl = __ballot(dl <= kth), wr = __ballot(dr <= kth);                         \
-        const uint32_t right_votes = (uint32_t)__popcll(wm & __ballot(qd > split));                \
-        const bool right_first = 2 * right_votes > (uint32_t)__popcll(wm);                         \
-        const uint64_t wn = right_first ? wr : wl, wf = right_first ? wl : wr;                     \
-        NBKD_PUSH_IF(wn != 0 && wf != 0) {                                                         \
-            /* push the far child when both are wanted: far = left child [lo, split] if          \
-               right_first, else right child [split, hi]; one v_cndmask per word */                \
-            const bool push = wn != 0 && wf != 0;                                                  \
-            const uint64_t pmask = push ? (1ull << sp) : 0ull;                                     \
+        bool go_right = wr != 0;                                                                   \
+        if (wl != 0 && wr != 0) {                                                                  \
+            const uint32_t right_votes = (uint32_t)__popcll(wm & __ballot(qd > split));            \
+            const bool right_first = 2 * right_votes > (uint32_t)__popcll(wm);                     \
+            const uint64_t pmask = 1ull << sp;                                                     \
             sk_node = lane_set(sk_node, right_first ? nd.left : nd.right, pmask);                  \
             _Pragma("unroll") for (int a = 0; a < 6; ++a) {                                        \
                 const bool is_split = right_first ? a == 2 * (D) + 1 : a == 2 * (D);               \
                 sk_b[a] = lane_set(sk_b[a], is_split ? split : bx[a], pmask);                      \
             }                                                                                      \
-            sp += push ? 1 : 0;                                                                    \
+            ++sp;                                                                                  \
+            go_right = right_first;                                                                \
+        } else if (wl == 0 && wr == 0) {                                                           \
+            continue;                                                                              \
         }                                                                                          \
-        if (wn == 0 && wf == 0) continue;                                                          \
-        const bool go_near = wn != 0;                                                              \
-        const bool go_right = go_near == right_first;                                              \
         node = go_right ? nd.right : nd.left;                                                      \
         nd = cnodes[node];                                                                         \
         tm[D] = go_right ? tr : tl;                                                                \
@@ -160,7 +151,7 @@ __device__ __forceinline__ uint32_t lane_set(uint32_t old, uint32_t val, uint64_
             bx[2 * (D)] = unif(split);                                                             \
         else                                                                                       \
             bx[2 * (D) + 1] = unif(split);                                                         \
-        wm = go_near ? wn : wf;                                                                    \
+        wm = go_right ? wr : wl;                                                                   \
         have = true;                                                                               \
     }
 
