@@ -190,8 +190,14 @@ const Rccl *rccl() {
     Rccl &r = g_rccl;
     if (r.tried) return r.ok ? &r : nullptr;
     r.tried = true;
-    void *h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
-    if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+    // the image's RCCL first, by path: it is built against the HIP runtime this
+    // library links (ROCm 7.2).  By soname a process that has imported torch
+    // gets torch's bundled librccl, which calls torch's own HIP runtime: that
+    // one sees no device once ours owns it, and ncclCommInitRank fails with
+    // "no ROCm-capable device is detected" (profiles/r03_rccl_probe_*.log).
+    // hip.preload() loads it before torch for the same reason.
+    void *h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+    if (!h) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
     if (!h) {
         const char *e = dlerror();
         r.err = std::string("cannot load librccl.so.1: ") + (e ? e : "?");

@@ -57,6 +57,13 @@ def preload():
     from . import capi
 
     capi.lib()
+    # RCCL too (nbkd_comm_probe: a dlopen, nothing starts): the image's librccl,
+    # bound to this runtime.  Loaded after torch, the soname would resolve to
+    # torch's bundled librccl, whose own HIP runtime sees no device here.
+    try:
+        capi.comm_probe()
+    except Exception:
+        pass  # no RCCL: the multi-GPU paths stage over gloo
 
 
 def _ok(rc, what):

@@ -204,6 +204,63 @@ def test_two_rank_slab_knn_rccl(gpu, oracle, tmp_path):
     _run_two_ranks(tmp_path, oracle, rccl=True, hscale=0.1)
 
 
+def _rccl_probe_worker(rank, world, port, outdir):
+    from nbodyhpc_amd import hip
+
+    hip.preload()  # as bench.py: the image's HIP runtime and RCCL before torch
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from nbodyhpc_amd import capi
+
+    msgs = []
+    try:
+        dev = rank if capi.device_count() >= world else 0
+        hip.set_device(dev)
+        comm = slab.init_comm(dist, rank, world, dev, log=msgs.append)
+        maps = open("/proc/self/maps").read()
+        rccl = sorted({ln.split()[-1] for ln in maps.splitlines() if "librccl" in ln})
+        with open(os.path.join(outdir, f"p{rank}.txt"), "w") as f:
+            f.write(f"comm={comm is not None}\n" + "\n".join(msgs) + "\nRCCL " + " ".join(rccl))
+        if comm is not None:
+            comm.close()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rccl_starts_in_a_torch_process(gpu, tmp_path):
+    """The RCCL the slab path drives must be the image's (bound to libnbkd's
+    HIP runtime) even though torch, imported for gloo, brings its own librccl:
+    that one calls torch's HIP runtime, which sees no device here, and
+    ncclCommInitRank failed with 'unhandled cuda error' before any rank could
+    meet.  On a one-GPU box two ranks then get past bootstrap and device
+    detection to RCCL's duplicate-device check ('invalid usage'); with two
+    GPUs the communicator starts."""
+    import multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    procs = [ctx.Process(target=_rccl_probe_worker, args=(r, 2, port, str(tmp_path)))
+             for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+    for p in procs:
+        if p.exitcode is None:
+            p.kill()
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    for r in range(2):
+        txt = open(os.path.join(tmp_path, f"p{r}.txt")).read()
+        assert "/opt/rocm" in txt.split("RCCL", 1)[1], txt
+        if gpu.device_count() >= 2:
+            assert "comm=True" in txt, txt
+        else:
+            assert "comm=False" in txt and "invalid usage" in txt, txt
+
+
 def test_forward_and_row_kernels_match_host(gpu):
     """nbkd_slab_forward == slab.side_needs (per side, f32); row gather / scatter."""
     from nbodyhpc_amd import hip
