@@ -555,7 +555,16 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist  # gloo: CPU-side coordination only
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        # gloo prints "[Gloo] Rank r is connected to ..." on stdout (C++, every
+        # rank): stdout carries only rank 0's JSON line, so send it to stderr
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+        finally:
+            os.dup2(saved, 1)
+            os.close(saved)
     # rehearsal of the N > 1 path on a one-GPU box: every rank on device 0 and
     # the halo staged over gloo (RCCL needs one GPU per rank)
     same_dev = os.environ.get("NBKD_BENCH_SAME_DEVICE") == "1"
