@@ -56,6 +56,8 @@ void free_tree(Tree &t) {
     tree_free(t.hsplit);
     tree_free(t.ginfo);
     tree_free(t.hinfo);
+    tree_free(t.nbox);
+    t.nbox = nullptr;
     t.ginfo = t.hinfo = nullptr;
     t.leafinfo = nullptr;
     t.hsplit = nullptr;

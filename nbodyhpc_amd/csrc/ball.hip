@@ -52,10 +52,12 @@ __device__ __forceinline__ float box_ub2(float qx, float qy, float qz, const flo
     return (ux * ux + uy * uy) + uz * uz;
 }
 
-// occupancy per variant ([periodic][fill]).  The count kernels spill a few
-// registers at 8 waves per SIMD (20 / 104 B per lane, periodic / not; the
-// periodic 1e8 count writes 4.7 GB, r03f), but at 7 waves without spills the
-// periodic count ran 128.5 ms against 124.3 (r03g): the spills stay in L2
+// occupancy per variant ([periodic][fill]).  With the node-id stack the
+// periodic count fits 8 waves per SIMD without spills (62 VGPRs); the
+// non-periodic count still spills 44 B per lane.  Round 3 before the node-id
+// stack: the periodic count spilled 20 B per lane at 8 waves (4.7 GB written
+// per 1e8 count, r03f), and 7 waves without spills ran 128.5 ms against 124.3
+// (r03g): spills that stay in L2 cost less than the lost occupancy
 constexpr int BALL_OCC[2][2] = {{8, 8}, {8, 8}};
 
 template <bool PER, bool FILL>
@@ -83,9 +85,9 @@ ball_packet_kernel(DevTree t, const uint32_t *__restrict__ linfo, const float *_
     if constexpr (!FILL) W.qs[lane] = make_float4(qx, qy, qz, 0.0f);
 
     uint32_t sk_node = 0;
-    float sk_b[6] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
     int sp = 0;
     const cnode_ptr cnodes = (cnode_ptr)t.nodes;
+    const cbox_ptr cboxes = (cbox_ptr)t.nbox;
     uint32_t node = 0;
     float bx[6];
 #pragma unroll
@@ -98,7 +100,7 @@ ball_packet_kernel(DevTree t, const uint32_t *__restrict__ linfo, const float *_
     uint64_t wm = __ballot((tm[0] + tm[1]) + tm[2] <= thr);
     bool have = wm != 0;
     nbkd_node nd = cnodes[0]; // record of `node` while `have`
-    // the shared packet walk (packet.hpp: per-axis steps, branch-free pushes)
+    // the shared packet walk (packet.hpp: per-axis steps, node-id stack)
     constexpr bool M = PER, STATS = false;
     const float kth = thr;
     uint64_t st[1] = {0};

@@ -358,6 +358,34 @@ scatter_kernel(const Tile *__restrict__ tiles, const LSeg *__restrict__ segs,
     }
 }
 
+// ------------------------------------------------------------------ cell boxes
+// Per node: the root box cut by the splits on its path (what the packet walk
+// carries in bx when it reaches the node).  One thread per node descends from
+// the root; in preorder the left subtree of c is [c + 1, right(c)).
+__global__ void __launch_bounds__(TB)
+cellbox_kernel(const nbkd_node *__restrict__ nodes, uint64_t nnodes, float lo0, float hi0,
+               float *__restrict__ nbox) {
+    for (uint64_t i = blockIdx.x * (uint64_t)TB + threadIdx.x; i < nnodes;
+         i += (uint64_t)gridDim.x * TB) {
+        float b[6] = {lo0, hi0, lo0, hi0, lo0, hi0};
+        uint32_t c = 0;
+        while (c != (uint32_t)i) {
+            const nbkd_node nd = nodes[c];
+            if (nd.dimension < 0) break; // not reached for a valid id
+            if ((uint32_t)i < nd.right) {
+                b[2 * nd.dimension + 1] = nd.split;
+                c = c + 1;
+            } else {
+                b[2 * nd.dimension] = nd.split;
+                c = nd.right;
+            }
+        }
+        float4 *o = reinterpret_cast<float4 *>(nbox + 8 * i);
+        o[0] = make_float4(b[0], b[1], b[2], b[3]);
+        o[1] = make_float4(b[4], b[5], 0.0f, 0.0f);
+    }
+}
+
 // ------------------------------------------------------------------ small segments
 __device__ __forceinline__ uint32_t subtree_nodes(uint32_t count, uint32_t leaf,
                                                   const uint32_t *__restrict__ tab_c,
@@ -1505,6 +1533,14 @@ nbkd_status build_tree(Tree &t, const float *xyz, uint64_t n, int32_t leaf_size,
         uint64_t blocks = std::min<uint64_t>((t.nnodes + TB - 1) / TB, 4096);
         extract_splits_kernel<<<(unsigned)std::max<uint64_t>(blocks, 1), TB, 0, s>>>(
             t.nodes, t.nnodes, t.splits);
+        NBKD_HIP(hipGetLastError());
+    }
+    {
+        NBKD_HIP(tree_malloc((void **)&t.nbox, std::max<uint64_t>(t.nnodes, 1) * 32));
+        uint64_t blocks = std::min<uint64_t>((t.nnodes + TB - 1) / TB, 16384);
+        const float lo0 = t.periodic ? 0.0f : -FLT_MAX, hi0 = t.periodic ? t.box : FLT_MAX;
+        cellbox_kernel<<<(unsigned)std::max<uint64_t>(blocks, 1), TB, 0, s>>>(t.nodes, t.nnodes,
+                                                                              lo0, hi0, t.nbox);
         NBKD_HIP(hipGetLastError());
     }
     if (t.depth <= 30) {

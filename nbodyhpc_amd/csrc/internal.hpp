@@ -106,6 +106,11 @@ struct Tree {
     // internal nodes' split values in the 4-level blocked heap order below
     // (hblk_blocks(depth) lines of 16 floats), or nullptr
     float *hsplit = nullptr;
+    // per node id: its cell box (the root box cut by the splits on its path:
+    // [0, L]^3 periodic, [-FLT_MAX, FLT_MAX]^3 otherwise) as lo.x, hi.x, lo.y,
+    // hi.y, lo.z, hi.z, 0, 0 (32 B): the packet walk's stack holds node ids
+    // only and reads a popped node's box here
+    float *nbox = nullptr;
     float bbox_lo[3] = {0.0f, 0.0f, 0.0f}, bbox_hi[3] = {0.0f, 0.0f, 0.0f}; // of the real points
     // leaves holding padding points (FLT_MAX, n <= position id < n8): node ids
     int npad_leaves = 0;
@@ -124,10 +129,11 @@ struct DevTree {
     uint32_t n8;
     uint32_t nnodes;
     float box;
+    const float *__restrict__ nbox;
 };
 
 inline DevTree view(const Tree &t) {
-    return DevTree{t.x, t.y, t.z, t.idx, t.nodes, (uint32_t)t.n8, (uint32_t)t.nnodes, t.box};
+    return DevTree{t.x, t.y, t.z, t.idx, t.nodes, (uint32_t)t.n8, (uint32_t)t.nnodes, t.box, t.nbox};
 }
 
 // Tuning.  The production library reads no environment variable: every

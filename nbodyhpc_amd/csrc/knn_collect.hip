@@ -485,9 +485,9 @@ __device__ __forceinline__ void grp_packet(const DevTree &t, const float *__rest
     const float L = t.box;
     uint32_t last_cnt = 0;
     uint32_t sk_node = 0;
-    float sk_b[6] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
     int sp = 0;
     const cnode_ptr cnodes = (cnode_ptr)t.nodes;
+    const cbox_ptr cboxes = (cbox_ptr)t.nbox;
     uint32_t node = 0;
     float bx[6];
 #pragma unroll

@@ -97,8 +97,9 @@ __device__ __forceinline__ void knn_fail_check(bool valid, bool seeded, uint32_t
 // ------------------------------------------------------------------ packet walk
 // The wave's depth-first walk (knn_collect.hip, ball.hip).  The macros expect in
 // scope: lane, qx/qy/qz, the bound kth, L, cnodes, the walk state node / nd (its
-// record while `have`) / have / wm / bx[6] / tm[3], the wave stack sp / sk_node /
-// sk_b[6], the metric switch M and STATS / st (node visits in st[0]).
+// record while `have`) / have / wm / bx[6] / tm[3], the wave stack sp / sk_node,
+// the cell boxes cboxes, the metric switch M and STATS / st (node visits in
+// st[0]).
 // v = lanes in `mask` ? val : old, as one v_cndmask (a select of a uniform
 // value into one lane otherwise compiles to exec-masked branches)
 __device__ __forceinline__ float lane_set(float old, float val, uint64_t mask) {
@@ -111,6 +112,23 @@ __device__ __forceinline__ uint32_t lane_set(uint32_t old, uint32_t val, uint64_
     asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(old), "v"(val), "s"(mask));
     return r;
 }
+
+// The wave stack holds node ids only: a pushed far child's id in lane sp of
+// sk_node.  A popped node's box is read back from the tree's per-node cell
+// boxes (Tree::nbox: the root box cut by the splits on the node's path, the
+// values bx held when it was pushed), one s_load_dwordx8 beside the node
+// record.  Round 2 kept the box in six more stack VGPRs (six selects per push,
+// six readlanes per pop): collect 50.03 -> 48.80 ms, radius count 126.1 ->
+// 121.8 ms at 1e8, same output SHA (profiles/r03_ab7_node_stack.txt); the
+// collect kernel needs 58 VGPRs instead of 64.
+struct NodeBox {
+    float b[8];
+};
+#if defined(__HIP_DEVICE_COMPILE__)
+typedef const __attribute__((address_space(4))) NodeBox *cbox_ptr;
+#else
+typedef const NodeBox *cbox_ptr;
+#endif
 
 // one internal node with split axis D (compile-time): test both children for
 // every lane; a single wanted child is entered, and only when both are wanted
@@ -135,10 +153,6 @@ __device__ __forceinline__ uint32_t lane_set(uint32_t old, uint32_t val, uint64_
             const bool right_first = 2 * right_votes > (uint32_t)__popcll(wm);                     \
             const uint64_t pmask = 1ull << sp;                                                     \
             sk_node = lane_set(sk_node, right_first ? nd.left : nd.right, pmask);                  \
-            _Pragma("unroll") for (int a = 0; a < 6; ++a) {                                        \
-                const bool is_split = right_first ? a == 2 * (D) + 1 : a == 2 * (D);               \
-                sk_b[a] = lane_set(sk_b[a], is_split ? split : bx[a], pmask);                      \
-            }                                                                                      \
             ++sp;                                                                                  \
             go_right = right_first;                                                                \
         } else if (wl == 0 && wr == 0) {                                                           \
@@ -163,7 +177,10 @@ __device__ __forceinline__ uint32_t lane_set(uint32_t old, uint32_t val, uint64_
             if (sp == 0) break;                                                                    \
             --sp;                                                                                  \
             node = (uint32_t)__builtin_amdgcn_readlane((int)sk_node, sp);                          \
-            _Pragma("unroll") for (int a = 0; a < 6; ++a) bx[a] = rdlane(sk_b[a], sp);             \
+            {                                                                                      \
+                const NodeBox nb_ = cboxes[node];                                                  \
+                _Pragma("unroll") for (int a = 0; a < 6; ++a) bx[a] = nb_.b[a];                    \
+            }                                                                                      \
             tm[0] = box_lb_axis<M>(qx, bx[0], bx[1], L);                                           \
             tm[1] = box_lb_axis<M>(qy, bx[2], bx[3], L);                                           \
             tm[2] = box_lb_axis<M>(qz, bx[4], bx[5], L);                                           \

@@ -28,8 +28,16 @@ def main():
     for r in range(rounds):
         for name in libs:
             env = dict(os.environ)
-            if name != "prod":
-                env["NBKD_LIB"] = os.path.join(ROOT, "nbodyhpc_amd", "lib", "exp", name, "libnbkd.so")
+            # "lib@VAR=V+VAR2=W": a build plus environment knobs (the experiments
+            # build, `python -m nbodyhpc_amd.build --experiments`, is "exp")
+            lib, _, knobs = name.partition("@")
+            for kv in filter(None, knobs.split("+")):
+                kk, _, vv = kv.partition("=")
+                env[kk] = vv
+            if lib == "exp":
+                env["NBKD_LIB"] = os.path.join(ROOT, "nbodyhpc_amd", "lib", "exp", "libnbkd.so")
+            elif lib != "prod":
+                env["NBKD_LIB"] = os.path.join(ROOT, "nbodyhpc_amd", "lib", "exp", lib, "libnbkd.so")
             out = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "knn_time.py")] + extra,
                                  env=env, capture_output=True, text=True, timeout=600)
             if out.returncode != 0:
@@ -39,14 +47,14 @@ def main():
             line["name"] = name
             print(json.dumps(line), flush=True)
             res[name].append(line)
-    print("name        wall_ms  collect  select  leaf_key  sort  retry  sha", flush=True)
+    print("name                      wall_ms  collect  select  leaf_key  sort  retry  sha", flush=True)
     for name, ls in res.items():
         med = lambda f: statistics.median(f(x) for x in ls)  # noqa: E731
         if ls[0].get("ball"):
-            print(f"{name:10s} {med(lambda x: x['wall_ms']):8.2f}  (radius count) "
+            print(f"{name:24s} {med(lambda x: x['wall_ms']):8.2f}  (radius count) "
                   f"{','.join(sorted(set(x['sha'] for x in ls)))}", flush=True)
             continue
-        print(f"{name:10s} {med(lambda x: x['wall_ms']):8.2f} {med(lambda x: x['phases_ms']['knn_collect']):8.2f} "
+        print(f"{name:24s} {med(lambda x: x['wall_ms']):8.2f} {med(lambda x: x['phases_ms']['knn_collect']):8.2f} "
               f"{med(lambda x: x['phases_ms']['knn_select']):7.2f} {med(lambda x: x['phases_ms']['leaf_key']):8.2f} "
               f"{med(lambda x: x['phases_ms']['sort']):5.2f} {med(lambda x: x['phases_ms']['knn_retry']):6.2f} "
               f"{','.join(sorted(set(x['sha'] for x in ls)))}", flush=True)
