@@ -494,6 +494,9 @@ def run_c5(args, rank, world, local_rank, dist, same_dev, barrier, allmax, allsu
         per_rank = [int(x.item()) for x in counts]
     else:
         per_rank = [own]
+    # collectives on every rank, before rank 0 alone writes the line
+    sr_fwd = 0.0 if ds is None else allsum(float(sr_acc["rows_forwarded"])) / max(sr_acc["calls"], 1)
+    sr_hops = 0 if ds is None else int(allmax(float(sr_acc["hops"])))
     if rank != 0:
         return
     q_total = sums[0] * args.steps
@@ -532,9 +535,8 @@ def run_c5(args, rank, world, local_rank, dist, same_dev, barrier, allmax, allsu
             # was resolved by the second-round exchange (no rebuild, no widening)
             "kth_rows_past_halo": violations,
             "second_round": {"transport": rows.transport,
-                             "rows_forwarded_per_pass": allsum(float(sr_acc["rows_forwarded"]))
-                             / max(sr_acc["calls"], 1),
-                             "max_hops": int(allmax(float(sr_acc["hops"])))}},
+                             "rows_forwarded_per_pass": sr_fwd,
+                             "max_hops": sr_hops}},
         "bounds": bounds,
         "build_ms": build_ms,
         "generate_s": gen_s,
