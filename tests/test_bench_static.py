@@ -1,0 +1,44 @@
+"""bench.py's N > 1 lines: every collective (gloo all-reduce / all-gather /
+barrier) must run on every rank, so none may follow the point where the other
+ranks return and rank 0 alone writes the JSON line.  (Round 3 found C5's
+second-round summary all-reduces after that point: N = 2 ended with
+"connection closed by peer".)"""
+import ast
+import os
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+COLLECTIVES = {"allsum", "allmax", "allgather_int", "barrier", "all_reduce", "all_gather",
+               "broadcast", "second_round"}
+
+
+def _is_rank0_return(node):
+    """`if rank != 0: return`"""
+    if not isinstance(node, ast.If) or not node.body or not isinstance(node.body[0], ast.Return):
+        return False
+    t = node.test
+    return (isinstance(t, ast.Compare) and isinstance(t.left, ast.Name) and t.left.id == "rank"
+            and isinstance(t.ops[0], ast.NotEq))
+
+
+def _called_names(node):
+    for n in ast.walk(node):
+        if isinstance(n, ast.Call):
+            f = n.func
+            if isinstance(f, ast.Name):
+                yield f.id
+            elif isinstance(f, ast.Attribute):
+                yield f.attr
+
+
+def test_no_collective_after_rank0_return():
+    tree = ast.parse(open(os.path.join(ROOT, "bench.py")).read())
+    checked = 0
+    for fn in ast.walk(tree):
+        if not isinstance(fn, ast.FunctionDef):
+            continue
+        for i, stmt in enumerate(fn.body):
+            if _is_rank0_return(stmt):
+                checked += 1
+                late = {name for s in fn.body[i + 1:] for name in _called_names(s)} & COLLECTIVES
+                assert not late, f"{fn.name}: {sorted(late)} after `if rank != 0: return`"
+    assert checked >= 2  # main's headline line and run_c5's line
