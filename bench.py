@@ -89,6 +89,28 @@ def pmc_traffic(n_particles, k, q_per_launch, kind="knn"):
     return None, None
 
 
+def roofline_entry(traffic, traffic_source, kernel_ms, work_achieved, **extra):
+    """The roofline object of one kernel.  `achieved` / `frac` are HBM
+    bandwidth as the counters see it: HBM bytes per launch (rocprofv3 PMC of
+    THIS library build: FETCH_SIZE x2 + WRITE_SIZE, each scaled by the
+    calibration of this code's access shapes, profiles/*_pmc_calibration.json)
+    / the launch's HIP-event duration / 8 TB/s, so frac <= 1.  Without a PMC
+    summary of this build both are null.  `work_achieved` / `work_frac` are
+    the reference's algorithmic bytes per launch / the same
+    duration: a work rate, which exceeds the HBM peak because one staged leaf
+    serves 64 queries of a packet."""
+    sec = kernel_ms * 1e-3
+    ach = None if traffic is None or sec <= 0 else traffic / sec / 1e9
+    out = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": None if ach is None else ach / HBM_PEAK_GBS,
+           "traffic": traffic, "traffic_source": traffic_source,
+           "basis": "PMC HBM bytes per launch (calibrated) / HIP-event launch time",
+           "work_achieved": work_achieved, "work_frac": work_achieved / HBM_PEAK_GBS,
+           "kernel_ms_per_launch": kernel_ms}
+    out.update(extra)
+    return out
+
+
 def bytes_per_query(k, nodes=REF_NODES_1E8, points=REF_POINTS_1E8):
     return 16.0 * nodes + 12.0 * points + 12.0 + 8.0 * k
 
@@ -135,6 +157,7 @@ def parse():
     p.add_argument("--input", default=None,
                    help="raw float32 (N, 3) particle file (reference main.cpp -f format) "
                         "instead of the synthetic set; N > 1 streams each rank's slab")
+    p.add_argument("--launch-probe", action="store_true", help=argparse.SUPPRESS)
     p.add_argument("--input-format", choices=("raw", "gadget"), default="raw",
                    help="gadget: a Gadget-2 snapshot (format 1/2, multi-file; N > 1 streams each "
                         "rank's slab unless --redistribute); the box is its BoxSize")
@@ -156,11 +179,15 @@ def gen_uniform(n, seed, box):
 
 
 def cpu_baseline(points, k, leafsize, box, sample, gpu_d, gpu_i):
-    """The reference's own C++ (oracle/_ref) when built, else the C restatement
-    (oracle/liborc.so), timed on this host's cores on a bounded sample."""
-    from oracle.oracle import Oracle, Reference, REF_PATH
-    kind = "reference" if os.path.exists(REF_PATH) else "port"
-    lib = Reference() if kind == "reference" else Oracle()
+    """The C restatement of the reference (oracle/liborc.so, pinned bit for bit to
+    the reference's own compiled C++ by tests/test_oracle.py; same median-split
+    tree, 8-wide leaf scan + loser tree, contiguous-block thread pool), timed on
+    this host's cores on a bounded sample.  The reference itself does not travel
+    to the GPU box; the port/reference speed ratio measured in
+    the build container is in BASELINE.md."""
+    from oracle.oracle import Oracle
+    kind = "port"
+    lib = Oracle()
     cores = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
     cores = max(1, min(cores, 64))
     t0 = time.perf_counter()
@@ -314,18 +341,15 @@ def suite(args, capi, hip, tree, dev_pts, n, k, L, stream, od, oi):
                            "kernel_ms": kern_ms / steps, "r": r, "mean_count": float(c.mean()),
                            "expected_mean_count": expect, "queries": n}
     if n == 100_000_000 and abs(args.radius - 0.01) < 1e-12:
-        # algorithmic bytes per query / kernel time; frac > 1 means the leaves are
+        # algorithmic bytes per query / kernel time; work_frac > 1 means the leaves are
         # re-read from cache (the kernel is VALU-bound: profiles/r01k_ball_pmc.txt)
         br = 16.0 * REF_BALL_NODES_1E8 + 12.0 * REF_BALL_POINTS_1E8 + 16.0
         ach = br * n / (kern_ms / steps * 1e-3) / 1e9
         traffic, tsrc = pmc_traffic(n, k, n, kind="ball")
-        out["radius_count"]["roofline"] = {
-            "bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": ach / HBM_PEAK_GBS, "bytes_per_query": br,
-            "traffic": traffic, "traffic_source": tsrc,
-            "hbm_frac": (None if traffic is None else
-                         traffic / (kern_ms / steps * 1e-3) / (HBM_PEAK_GBS * 1e9)),
-            "kernel": "ball_packet_kernel<periodic, count> (nbodyhpc_amd/csrc/ball.hip)"}
+        out["radius_count"]["roofline"] = roofline_entry(
+            traffic, tsrc, kern_ms / steps, ach,
+            kernel="ball_packet_kernel<periodic, count> (nbodyhpc_amd/csrc/ball.hip)",
+            bytes_per_query=br, queries_per_launch=n)
     log(f"suite: radius count {n / sec:.3e} q/s, mean {c.mean():.1f} (expect {expect:.1f})")
     # C3: CSR batch (host in / host out: PCIe-inclusive)
     b = min(args.csr_batch, n)
@@ -544,29 +568,93 @@ def run_c5(args, rank, world, local_rank, dist, same_dev, barrier, allmax, allsu
     print(json.dumps(out), flush=True)
 
 
+def visible_gpus() -> int:
+    """GPUs this process may use, counted without initialising the HIP runtime
+    (torch.cuda.device_count() does not initialise it on this image)."""
+    import torch
+    return int(torch.cuda.device_count())
+
+
+def free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(args) -> int:
+    """`python bench.py --gpus N` (N > 1) without a launcher: start the N ranks
+    as children (torch.distributed.run, one process per GPU, rendezvous on
+    127.0.0.1) before this process touches the GPU, and exit with their exit
+    code; rank 0's JSON line reaches stdout through the inherited descriptor.
+    Never execs: the parent only waits.  With fewer visible GPUs than N it
+    fails, unless NBKD_BENCH_SAME_DEVICE=1 (every rank on GPU 0: a rehearsal of
+    the N > 1 path on a one-GPU box)."""
+    import subprocess
+    same_dev = os.environ.get("NBKD_BENCH_SAME_DEVICE") == "1"
+    if not same_dev and not args.launch_probe:
+        have = visible_gpus()
+        if have < args.gpus:
+            log(f"error: --gpus {args.gpus} but only {have} GPU(s) visible; refusing to "
+                f"report an N={args.gpus} line from fewer GPUs (NBKD_BENCH_SAME_DEVICE=1 "
+                f"rehearses N ranks on GPU 0)")
+            return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr=127.0.0.1",
+           f"--master-port={free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    log("starting ranks: " + " ".join(cmd))
+    sys.stdout.flush()
+    env = dict(os.environ)
+    env.setdefault("OMP_NUM_THREADS", "16")
+    return subprocess.call(cmd, env=env)
+
+
+def init_gloo(rank, world):
+    import torch.distributed as dist  # gloo: CPU-side coordination only
+    # gloo prints "[Gloo] Rank r is connected to ..." on stdout (C++, every
+    # rank): stdout carries only rank 0's JSON line, so send it to stderr
+    sys.stdout.flush()
+    saved = os.dup(1)
+    os.dup2(2, 1)
+    try:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    finally:
+        os.dup2(saved, 1)
+        os.close(saved)
+    return dist
+
+
+def launch_probe(rank, world, dist):
+    """--launch-probe (tests): the ranks meet over gloo and rank 0 prints one
+    JSON line naming them; no GPU is touched."""
+    import torch
+    out = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
+    dist.all_gather(out, torch.tensor([rank], dtype=torch.int64))
+    if rank == 0:
+        print(json.dumps({"n_gpus": world, "ranks": [int(x.item()) for x in out],
+                          "launch_probe": True}), flush=True)
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args))
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
+    if args.launch_probe:
+        dist = init_gloo(rank, world)
+        launch_probe(rank, world, dist)
+        dist.destroy_process_group()
+        return
     from nbodyhpc_amd import capi, hip
 
     hip.preload()  # before torch: see hip.preload
     dist = None
     if world > 1:
-        import torch.distributed as dist  # gloo: CPU-side coordination only
-        # gloo prints "[Gloo] Rank r is connected to ..." on stdout (C++, every
-        # rank): stdout carries only rank 0's JSON line, so send it to stderr
-        sys.stdout.flush()
-        saved = os.dup(1)
-        os.dup2(2, 1)
-        try:
-            dist.init_process_group("gloo", rank=rank, world_size=world)
-        finally:
-            os.dup2(saved, 1)
-            os.close(saved)
+        dist = init_gloo(rank, world)
     # rehearsal of the N > 1 path on a one-GPU box: every rank on device 0 and
     # the halo staged over gloo (RCCL needs one GPU per rank)
     same_dev = os.environ.get("NBKD_BENCH_SAME_DEVICE") == "1"
@@ -832,23 +920,12 @@ def main():
         "halo": halo,
         "build_ms": build_ms,
         "build_ms_first": build_ms_first,
-        "roofline": {
-            "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-            "traffic_source": traffic_source,
-            # counter bytes / kernel time / peak: the HBM fraction rocprof sees
-            # (achieved / frac are a work rate in the reference's bytes: the
-            # packet kernel reads a staged leaf once for 64 queries)
-            "hbm_frac": (None if traffic is None else
-                         traffic / (col_avg_ms * 1e-3) / (HBM_PEAK_GBS * 1e9)),
-            # whole-step rate in the reference's bytes over all GPUs' peak
-            "step_frac": value * bq / (HBM_PEAK_GBS * 1e9 * world),
-            "kernel": "knn_collect_grp_kernel<periodic> (nbodyhpc_amd/csrc/knn_collect.hip)",
-            "kernel_ms_per_launch": col_avg_ms,
-            "launches_per_step": col_launches / args.steps,
-            "queries_per_launch": q_per_launch,
-            "bytes_per_query": bq,
-        },
+        "roofline": roofline_entry(
+            traffic, traffic_source, col_avg_ms, achieved,
+            kernel="knn_collect_grp_kernel<periodic> (nbodyhpc_amd/csrc/knn_collect.hip)",
+            step_work_frac=value * bq / (HBM_PEAK_GBS * 1e9 * world),
+            launches_per_step=col_launches / args.steps, queries_per_launch=q_per_launch,
+            bytes_per_query=bq),
         "breakdown_ms_per_step": {
             "leaf_key": key_ms / args.steps, "sort": sort_ms / args.steps,
             "knn": knn_ms / args.steps, "knn_collect": col_ms / args.steps,

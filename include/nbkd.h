@@ -69,7 +69,7 @@ typedef struct {
  * Replaces: PyKDTree::PyKDTree / make_positions_and_indices (kdtree/src/cpp/pybind.cpp:14-56,76-88)
  *           and KDTree::KDTree (kdtree/src/cpp/kdtree.cpp:95-131).
  *   leaf_size  as the caller passes it; the reference clamps to >= 16
- *              (kdtree/src/cpp/include/kdtree/kdtree_impl.hpp:485).
+ *              (kdtree/src/cpp/include/kdtree/kdtree_impl.hpp:88-92).
  *   periodic   0 or 1; when 1 every coordinate must lie in [0, box_size].
  *   device     HIP device ordinal (< 0: the calling thread's current device).
  * The node table equals the reference's for the same (points, leaf_size):

@@ -1,7 +1,7 @@
 // GPU tree builder for gfx950.
 //
 // Produces the reference's node table (KDTreeBuilder::build_node,
-// kdtree/src/cpp/include/kdtree/kdtree_impl.hpp:492-540) on the device:
+// kdtree/src/cpp/include/kdtree/kdtree_impl.hpp:98-146) on the device:
 //   * leaf iff count <= max(leaf_size, 16)                       (:485, :495)
 //   * m = (count / 2) / 8 * 8; split = m-th order statistic of the
 //     segment's coordinate on axis depth % 3                      (:502-510)
@@ -1307,7 +1307,7 @@ nbkd_status build_tree(Tree &t, const float *xyz, uint64_t n, int32_t leaf_size,
         return NBKD_ETOOMANY;
     }
     // leaf_size_ = max(leaf_size, 2 * block_size): size_t comparison, so a
-    // negative int becomes huge (kdtree_impl.hpp:485)
+    // negative int becomes huge (kdtree_impl.hpp:88-92)
     uint64_t leaf64 = leaf_size < 0 ? (uint64_t)(int64_t)leaf_size : (uint64_t)leaf_size;
     leaf64 = std::max<uint64_t>(leaf64, 16);
     const uint32_t leaf = (uint32_t)std::min<uint64_t>(leaf64, UINT32_MAX);

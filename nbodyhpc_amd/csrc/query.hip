@@ -1,7 +1,7 @@
 // Batched kNN / radius queries for gfx950.
 //
 // Reference semantics (what the results must equal):
-//   traversal       KDTreeQuery::compute   kdtree/src/cpp/include/kdtree/kdtree_impl.hpp:620-662
+//   traversal       KDTreeQuery::compute   kdtree/src/cpp/include/kdtree/kdtree_impl.hpp:226-268
 //   point metric    L2 / L2Periodic        kdtree/src/cpp/include/kdtree/kdtree.hpp:23-31, 72-84
 //   box metric      box_distance           kdtree/src/cpp/include/kdtree/kdtree.hpp:35-45, 89-107
 //   insertion       d2 < current k-th      kdtree/src/cpp/kdtree_asm_systemv.asm:148-188
@@ -49,7 +49,7 @@ leaf_key_kernel(DevTree t, const float *__restrict__ q, uint32_t m, uint32_t *__
     nbkd_node nd = t.nodes[0];
     while (nd.dimension >= 0) {
         float v = p[nd.dimension];
-        node = v > nd.split ? nd.right : nd.left; // near child, kdtree_impl.hpp:633
+        node = v > nd.split ? nd.right : nd.left; // near child, kdtree_impl.hpp:239
         nd = t.nodes[node];
     }
     keys[i] = nd.left >> 3;
@@ -136,7 +136,7 @@ leaf_key3_kernel(const float4 *__restrict__ hb, int o, uint32_t n8, uint32_t lea
                                   : ((pos & 2) ? ((pos & 1) ? a2.z : a2.y)
                                                : ((pos & 1) ? a2.x : a1.w));
                 const uint32_t mm = (count / 2) / 8 * 8;
-                const bool right = p[dim] > s; // near child, kdtree_impl.hpp:633
+                const bool right = p[dim] > s; // near child, kdtree_impl.hpp:239
                 if (right) {
                     lo[dim] = s;
                     left += mm;
@@ -189,7 +189,7 @@ leaf_key2_kernel(const float *__restrict__ splits, const uint32_t *__restrict__ 
             }
             const uint32_t mm = (count / 2) / 8 * 8;
             const float s = splits[node];
-            if (p[dim] > s) { // near child, kdtree_impl.hpp:633
+            if (p[dim] > s) { // near child, kdtree_impl.hpp:239
                 lo[dim] = s;
                 uint32_t sub = 1;
                 if (mm > leaf) {
@@ -569,7 +569,7 @@ nbkd_status radix_sort(Workspace &ws, uint32_t *k0, uint32_t *v0, uint32_t *k1, 
 }
 
 // ------------------------------------------------------------------ reference-exact traversal
-// One lane per query, replaying KDTreeQuery::compute (kdtree_impl.hpp:620-662)
+// One lane per query, replaying KDTreeQuery::compute (kdtree_impl.hpp:226-268)
 // step for step: near child first (left unless q[dim] > split), near visited iff
 // box_d2 < k-th, far skipped iff k-th < box_d2 (checked after the near subtree),
 // leaf points inserted iff d2 < k-th into the reference's loser tree

@@ -9,10 +9,10 @@
  *
  *   padding / SoA / box check   kdtree/src/cpp/pybind.cpp:14-56
  *   build (median split)        kdtree/src/cpp/include/kdtree/kdtree_impl.hpp:78-146
- *                               (leaf_size_ = max(leaf, 2*block) :485, m = (count/2)/8*8 :502-503)
+ *                               (leaf_size_ = max(leaf, 2*block) :88-92, m = (count/2)/8*8 :108-109)
  *   constructor checks          kdtree/src/cpp/kdtree.cpp:95-131
  *   distance metrics            kdtree/src/cpp/include/kdtree/kdtree.hpp:20-121
- *   traversal                   kdtree/src/cpp/include/kdtree/kdtree_impl.hpp:616-662
+ *   traversal                   kdtree/src/cpp/include/kdtree/kdtree_impl.hpp:226-268
  *   loser (tournament) tree     kdtree/src/cpp/include/kdtree/tournament_tree.hpp:18-105
  *   leaf scan (asm semantics)   kdtree/src/cpp/kdtree_asm_systemv.asm:3-61,76-188
  *                               kdtree/src/cpp/include/kdtree/kdtree_opt.hpp:20-44 (Vanilla)
@@ -214,7 +214,7 @@ static int push_node(orc_tree *t, orc_node nd) {
     return (int)(t->nnodes++);
 }
 
-/* KDTreeBuilder::build_node, kdtree_impl.hpp:492-540 (non-threaded branch :542-551) */
+/* KDTreeBuilder::build_node, kdtree_impl.hpp:98-146 (non-threaded branch :148-157) */
 static int64_t build_node(orc_tree *t, orc_pt *pts, int dim, uint32_t left, uint32_t count,
                           uint32_t leaf) {
     if (count <= leaf) {
@@ -262,7 +262,7 @@ ORC_EXPORT int orc_build(const float *aos, int64_t n, int32_t leafsize, int32_t 
         orc_free(t);
         return st;
     }
-    /* leaf_size_ = max(leaf_size, 2 * block_size) with block_size 8, kdtree_impl.hpp:485.
+    /* leaf_size_ = max(leaf_size, 2 * block_size) with block_size 8, kdtree_impl.hpp:88-92.
      * The int -> size_t conversion there makes negative leaf sizes huge. */
     uint64_t leaf = leafsize < 0 ? (uint64_t)(int64_t)leafsize : (uint64_t)leafsize;
     if (leaf < 16) leaf = 16;
@@ -359,22 +359,34 @@ typedef struct {
     uint64_t visited, pruned, points;
 } orc_query;
 
-/* process_leaf + insert semantics: kdtree_impl.hpp:606-614, asm :148-188 */
+/* process_leaf + insert semantics: kdtree_impl.hpp:212-220, asm :148-188.
+ * Like the asm, a block of 8 distances is computed first (a loop gcc turns into
+ * AVX2 at -O3 -mavx2; no FMA, -ffp-contract=off), then each lane is re-checked
+ * against the current top in order (asm :168-169).  Leaves hold multiples of 8
+ * points (splits at multiples of 8, n padded to n8). */
 static void process_leaf(orc_query *Q, const orc_node *nd) {
     const orc_tree *t = Q->t;
+    const float qx = Q->q[0], qy = Q->q[1], qz = Q->q[2], L = t->box;
     float top = Q->lt[0].d;
-    for (uint32_t i = nd->left; i < nd->right; ++i) {
-        float d = t->periodic ? d2_per(Q->q[0], Q->q[1], Q->q[2], t->x[i], t->y[i], t->z[i], t->box)
-                              : d2_l2(Q->q[0], Q->q[1], Q->q[2], t->x[i], t->y[i], t->z[i]);
-        if (d < top) {
-            lt_replace_top(Q->lt, d, t->idx[i]);
-            top = Q->lt[0].d;
+    float d[8];
+    for (uint32_t i = nd->left; i < nd->right; i += 8) {
+        const float *px = t->x + i, *py = t->y + i, *pz = t->z + i;
+        if (t->periodic) {
+            for (int j = 0; j < 8; ++j) d[j] = d2_per(qx, qy, qz, px[j], py[j], pz[j], L);
+        } else {
+            for (int j = 0; j < 8; ++j) d[j] = d2_l2(qx, qy, qz, px[j], py[j], pz[j]);
+        }
+        for (int j = 0; j < 8; ++j) {
+            if (d[j] < top) {
+                lt_replace_top(Q->lt, d[j], t->idx[i + j]);
+                top = Q->lt[0].d;
+            }
         }
     }
     Q->points += nd->right - nd->left;
 }
 
-/* KDTreeQuery::compute, kdtree_impl.hpp:620-662 */
+/* KDTreeQuery::compute, kdtree_impl.hpp:226-268 */
 static void compute(orc_query *Q, const orc_node *node, const float bounds[6]) {
     const orc_tree *t = Q->t;
     Q->visited += 1;
@@ -480,9 +492,13 @@ static void *knn_worker(void *arg) {
         free(wtmp);
         return NULL;
     }
+    uint64_t st[3] = {0, 0, 0}; /* local: adjacent jobs' counters would share lines */
     for (int64_t i = J->begin; i < J->end; ++i)
         find_closest(J->t, J->q + 3 * i, J->k, lt, wtmp, J->out_d + (size_t)i * J->k,
-                     J->out_i + (size_t)i * J->k, J->want_sqrt, J->stats);
+                     J->out_i + (size_t)i * J->k, J->want_sqrt, st);
+    J->stats[0] = st[0];
+    J->stats[1] = st[1];
+    J->stats[2] = st[2];
     free(lt);
     free(wtmp);
     return NULL;

@@ -69,7 +69,7 @@ def assert_knn_equal(d_got, i_got, d_ref, i_ref, points, queries, boxsize=None, 
 
 def check_tree_structure(nodes, x, y, z, idx, n, leaf, n8=None):
     """Structural invariants of a reference-shaped tree (test_builders.cpp:86-139,
-    kdtree_impl.hpp:492-540): preorder, left child = id + 1, leaves cover
+    kdtree_impl.hpp:98-146): preorder, left child = id + 1, leaves cover
     [0, n8) in order with sizes % 8 == 0 and <= max(leaf, 16), points of the left
     subtree <= split <= points of the right subtree, idx a permutation."""
     leaf = max(int(leaf), 16)

@@ -42,3 +42,38 @@ def test_no_collective_after_rank0_return():
                 late = {name for s in fn.body[i + 1:] for name in _called_names(s)} & COLLECTIVES
                 assert not late, f"{fn.name}: {sorted(late)} after `if rank != 0: return`"
     assert checked >= 2  # main's headline line and run_c5's line
+
+
+def _run_bench(args, env_extra=None, timeout=120):
+    import json
+    import subprocess
+    import sys
+    env = {kk: v for kk, v in os.environ.items()
+           if kk not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "NBKD_BENCH_SAME_DEVICE")}
+    env.update(env_extra or {})
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, env=env,
+                       capture_output=True, text=True, timeout=timeout, cwd=ROOT)
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    return p.returncode, [json.loads(ln) for ln in lines], p.stderr
+
+
+def test_gpus_n_without_launcher_starts_n_ranks():
+    """`python bench.py --gpus 2` with no WORLD_SIZE starts two ranks itself
+    (torch.distributed.run children; the parent never execs) and forwards rank
+    0's one JSON line: the --launch-probe ranks meet over gloo without a GPU."""
+    rc, lines, err = _run_bench(["--gpus", "2", "--launch-probe"])
+    assert rc == 0, err[-2000:]
+    assert len(lines) == 1, lines
+    assert lines[0]["n_gpus"] == 2 and lines[0]["ranks"] == [0, 1]
+
+
+def test_gpus_n_with_fewer_gpus_fails_cleanly():
+    """Fewer visible GPUs than --gpus (none here): a non-zero exit and no JSON
+    line, never an n_gpus: 1 line for an N = 2 request."""
+    import torch
+    if torch.cuda.device_count() >= 2:
+        import pytest
+        pytest.skip("two GPUs are visible")
+    rc, lines, err = _run_bench(["--gpus", "2", "--steps", "1", "--warmup", "0"])
+    assert rc != 0 and not lines
+    assert "GPU(s) visible" in err

@@ -146,7 +146,7 @@ def test_ball_count_oracle_vs_scipy(oracle):
 
 
 def test_tree_shape_function():
-    """node count is a pure function of (n8, leaf): kdtree_impl.hpp:492-510"""
+    """node count is a pure function of (n8, leaf): kdtree_impl.hpp:98-109"""
     from functools import lru_cache
 
     @lru_cache(None)
