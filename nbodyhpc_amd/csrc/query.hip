@@ -1002,10 +1002,21 @@ nbkd_status knn_locked(const Tree &t, const float *q, uint64_t m, int k, float *
             // the re-walk rounds' columns: 8 capg (packets of 64 or one query
             // per wave), then 64 capg (one query per wave)
             const uint32_t capr = capg * 8u, capr2 = capg * 64u;
-            const uint64_t rb = std::max<uint64_t>(budget / ((uint64_t)capr * 8u) / 64u * 64u, 64);
-            const uint64_t rb2 = std::max<uint64_t>(budget / ((uint64_t)capr2 * 8u), 64);
-            // a round's pass covers at most min(cap, mm) queries, in packets of 64
+            // A round-1 batch holds at most rb queries (the 8 capg columns' budget)
+            // and round 1 takes up to ~10 % of the queries; round 2 rb2 per batch,
+            // up to ~1 %.  The columns are sized for THAT, not for every query
+            // failing: at m = 1e5, k = 32 sizing them for m held ~5.7 GB of
+            // scratch where the first pass needs ~90 MB.  What a round cannot
+            // take (never on the benchmark sets) spills to the next round, the
+            // last to the exact kernel.
             const uint64_t mm64 = ((uint64_t)mm + 63) / 64 * 64;
+            const uint64_t rb = std::min<uint64_t>(
+                std::max<uint64_t>(budget / ((uint64_t)capr * 8u) / 64u * 64u, 64),
+                std::max<uint64_t>(64, ((uint64_t)mm / 10 + 63) / 64 * 64));
+            const uint64_t rb2 = std::min<uint64_t>(
+                std::max<uint64_t>(budget / ((uint64_t)capr2 * 8u), 64),
+                std::max<uint64_t>(64, (uint64_t)mm / 100 + 1));
+            // a round's pass covers at most min(cap, mm) queries, in packets of 64
             const uint64_t cap1 = std::min<uint64_t>(rb, mm64), cap2 = std::min<uint64_t>(rb2, mm);
             const uint64_t cand_bytes =
                 std::max<uint64_t>({batch * capg * 8u, cap1 * capr * 8u, cap2 * capr2 * 8u});

@@ -85,6 +85,11 @@ def synchronize():
     _ok(_hip().hipDeviceSynchronize(), "hipDeviceSynchronize")
 
 
+def stream_synchronize(handle):
+    """hipStreamSynchronize on a raw stream handle (None: the null stream)."""
+    _ok(_hip().hipStreamSynchronize(handle), "hipStreamSynchronize")
+
+
 def mem_info():
     """(free, total) bytes of the current device (hipMemGetInfo)."""
     f, t = ctypes.c_size_t(), ctypes.c_size_t()

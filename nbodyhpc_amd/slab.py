@@ -627,7 +627,17 @@ def merge_rows(d2a, ia, d2b, ib, k):
     d2 = np.take_along_axis(d2, o, axis=1)
     ii = np.take_along_axis(ii, o, axis=1)
     keep = ii != _PAD
-    keep[:, 1:] &= ~((ii[:, 1:] == ii[:, :-1]) & (d2[:, 1:] == d2[:, :-1]))
+    # deduplicate by id alone: of each id's copies keep the first in (d2, id)
+    # order (a stable sort by id keeps that order inside a run of one id), so
+    # two trees' copies of one particle never both survive, even if their d2
+    # differed in the last bit
+    o2 = np.argsort(ii, axis=1, kind="stable")
+    s2 = np.take_along_axis(ii, o2, axis=1)
+    first = np.ones_like(keep)
+    first[:, 1:] = s2[:, 1:] != s2[:, :-1]
+    dup = np.empty_like(keep)
+    np.put_along_axis(dup, o2, ~first, axis=1)
+    keep &= ~dup
     rank = np.cumsum(keep, axis=1) - 1
     sel = keep & (rank < k)
     r, c = np.nonzero(sel)
@@ -771,7 +781,32 @@ class DeviceRows:
         self.stream = stream
         self._cap = 0
         self._list = self._sides = None
+        self._bufs = {}  # grow-only device buffers, reused across calls
         self.transport = "rccl" if ds.comm is not None else "gloo"
+
+    def _buf(self, key, nbytes):
+        from . import hip
+
+        b = self._bufs.get(key)
+        if b is None or b.nbytes < nbytes:
+            old = 0 if b is None else b.nbytes
+            b = hip.DeviceArray((max(int(nbytes), 2 * old, 4096),), np.uint8)
+            self._bufs[key] = b
+        return b
+
+    def _put(self, key, a):
+        """host array -> the reused device buffer `key` (synchronous copy)"""
+        from . import hip
+
+        a = np.ascontiguousarray(a)
+        b = self._buf(key, a.nbytes)
+        hip.memcpy(b.ptr, a.ctypes.data, a.nbytes, hip.H2D)
+        return b
+
+    def _sync(self):
+        from . import hip
+
+        hip.stream_synchronize(self.stream)
 
     def forward(self, cl, ch):
         from . import capi, hip
@@ -800,12 +835,14 @@ class DeviceRows:
 
         if len(u) == 0:
             return np.zeros((0, 3), np.float32)
-        du = hip.DeviceArray.from_numpy(np.ascontiguousarray(u, np.uint32))
-        dq = hip.DeviceArray((len(u), 3), np.float32)
+        du = self._put("u", np.ascontiguousarray(u, np.uint32))
+        dq = self._buf("q", 12 * len(u))
         capi.rows_gather(self.ds.xyz.ptr, 12, du.ptr, len(u), dq.ptr, self.ds.device,
                          self.stream)
-        hip.synchronize()
-        return dq.numpy()
+        self._sync()
+        out = np.empty((len(u), 3), np.float32)
+        hip.memcpy(out.ctypes.data, dq.ptr, out.nbytes, hip.D2H)
+        return out
 
     def knn_sq(self, q):
         q = np.ascontiguousarray(q, np.float32).reshape(-1, 3)
@@ -822,40 +859,41 @@ class DeviceRows:
         rb = int(np.prod(row_shape)) * np.dtype(dtype).itemsize
         sr = np.ascontiguousarray(send_r, dtype)
         sl = np.ascontiguousarray(send_l, dtype)
-        bufs = [hip.DeviceArray((max(a.nbytes, 4),), np.uint8) for a in (sr, sl)]
-        for b, a in zip(bufs, (sr, sl)):
-            hip.memcpy(b.ptr, a.ctypes.data, a.nbytes, hip.H2D)
-        rl = hip.DeviceArray((max(n_fl * rb, 4),), np.uint8)
-        rr = hip.DeviceArray((max(n_fr * rb, 4),), np.uint8)
-        pairs = [(bufs[0].ptr, sr.nbytes, right, rl.ptr, n_fl * rb, left),
-                 (bufs[1].ptr, sl.nbytes, left, rr.ptr, n_fr * rb, right)]
+        bs_r, bs_l = self._put("xs_r", sr), self._put("xs_l", sl)
+        rl, rr = self._buf("xr_l", n_fl * rb), self._buf("xr_r", n_fr * rb)
+        pairs = [(bs_r.ptr, sr.nbytes, right, rl.ptr, n_fl * rb, left),
+                 (bs_l.ptr, sl.nbytes, left, rr.ptr, n_fr * rb, right)]
         err = _enqueue_agreed(self.ds.dist, self.ds.rank, "second-round exchange",
                               lambda: self.ds.comm.exchange(pairs, stream=self.stream))
         if err is not None:
-            # every rank failed to enqueue: the buffers may still be touched
-            _ABANDONED.extend(bufs + [rl, rr])
+            # every rank failed to enqueue: the buffers may still be touched, so
+            # they leave the reuse cache and are never freed
+            for key in ("xs_r", "xs_l", "xr_l", "xr_r"):
+                _ABANDONED.append(self._bufs.pop(key))
             self.transport = "gloo"
             return _bytes_sendrecv(self.ds.dist, right, left, send_r, send_l, n_fl, n_fr,
                                    row_shape, dtype, tags)
-        hip.synchronize()
+        self._sync()
         shape = lambda n: (n,) + tuple(row_shape)
-        out_l = rl.numpy_head(n_fl * rb).view(dtype).reshape(shape(n_fl))
-        out_r = rr.numpy_head(n_fr * rb).view(dtype).reshape(shape(n_fr))
+        out_l = np.empty(shape(n_fl), dtype)
+        out_r = np.empty(shape(n_fr), dtype)
+        hip.memcpy(out_l.ctypes.data, rl.ptr, out_l.nbytes, hip.D2H)
+        hip.memcpy(out_r.ctypes.data, rr.ptr, out_r.nbytes, hip.D2H)
         return out_l, out_r
 
     def write(self, u, d2, ids):
-        from . import capi, hip
+        from . import capi
 
         if len(u) == 0:
             return
-        du = hip.DeviceArray.from_numpy(np.ascontiguousarray(u, np.uint32))
+        du = self._put("u", np.ascontiguousarray(u, np.uint32))
         dev, s = self.ds.device, self.stream
         if self.kth_ptr is not None:
-            col = hip.DeviceArray.from_numpy(np.sqrt(np.ascontiguousarray(d2[:, self.k - 1])))
+            col = self._put("d", np.sqrt(np.ascontiguousarray(d2[:, self.k - 1])))
             capi.rows_scatter(col.ptr, 4, du.ptr, len(u), self.kth_ptr, dev, s)
         else:
-            dd = hip.DeviceArray.from_numpy(np.sqrt(np.asarray(d2, np.float32)))
-            di = hip.DeviceArray.from_numpy(np.ascontiguousarray(ids, np.uint32))
+            dd = self._put("d", np.sqrt(np.asarray(d2, np.float32)))
+            di = self._put("i", np.ascontiguousarray(ids, np.uint32))
             capi.rows_scatter(dd.ptr, 4 * self.k, du.ptr, len(u), self.od_ptr, dev, s)
             capi.rows_scatter(di.ptr, 4 * self.k, du.ptr, len(u), self.oi_ptr, dev, s)
-        hip.synchronize()
+        self._sync()

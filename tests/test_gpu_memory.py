@@ -59,3 +59,29 @@ def test_oom_retry_releases_idle_scratch(gpu, oracle):
     oa = oracle.tree(pa, 64, 1.0)
     dr, ir = oa.query(qa[sel], 32, workers=8)
     assert_knn_equal(da[sel], ia[sel], dr, ir, pa, qa[sel], 1.0)
+
+
+@pytest.mark.parametrize("k", [32, 200])
+def test_small_query_scratch_is_bounded(gpu, oracle, k):
+    """The query scratch of a small call is sized for that call: the retry
+    rounds' columns cover ~10 % / ~1 % of its queries, not every query failing
+    (a 1e5-query k = 32 call held ~5.7 GB)."""
+    from nbodyhpc_amd import hip, synth
+    pts = synth.uniform(1_000_000, 103, 1.0)
+    t = gpu.Tree(pts, leafsize=64, boxsize=1.0)
+    m = 100_000
+    dq = hip.DeviceArray.from_numpy(pts[:m])
+    od = hip.DeviceArray((m, k), np.float32)
+    oi = hip.DeviceArray((m, k), np.uint32)
+    hip.synchronize()
+    free0, _ = hip.mem_info()
+    t.query_device(dq.ptr, m, k, od.ptr, oi.ptr)
+    hip.synchronize()
+    free1, _ = hip.mem_info()
+    grew = free0 - free1
+    assert grew < (512 << 20), f"a {m}-query k={k} call grew the scratch by {grew >> 20} MiB"
+    o = oracle.tree(pts, 64, 1.0)
+    sel = np.arange(0, m, 13)
+    dr, ir = o.query(pts[sel], k, workers=8)
+    assert_knn_equal(od.numpy()[sel], oi.numpy()[sel], dr, ir, pts, pts[sel], 1.0)
+    t.close()

@@ -507,3 +507,17 @@ def test_side_needs_matches_violations_host():
     f32 = np.float32
     left, right = slab.side_needs(x, dk, f32(f32(lo) - f32(h)), f32(f32(hi) + f32(h)))
     assert int((left | right).sum()) == slab.violations_host(q, dk, rank, world, box, h)
+
+
+def test_merge_rows_dedupes_by_id_even_when_d2_differs():
+    """One particle returned by two trees with d2 one ulp apart: only the
+    smaller copy survives, so it cannot push the true k-th neighbour out."""
+    k = 3
+    d_a = np.array([[0.1, 0.2, 0.3]], np.float32)
+    i_a = np.array([[7, 8, 9]], np.uint32)
+    bump = np.nextafter(np.float32(0.2), np.float32(1.0))
+    d_b = np.array([[bump, 0.25, 0.5]], np.float32)
+    i_b = np.array([[8, 11, 12]], np.uint32)
+    od, oi = slab.merge_rows(d_a, i_a, d_b, i_b, k)
+    assert oi.tolist() == [[7, 8, 11]]
+    assert od[0].tolist() == [np.float32(0.1), np.float32(0.2), np.float32(0.25)]
