@@ -17,10 +17,21 @@
  * than k points runs on grids that read the failure count on the device), and
  * so does nbkd_query_ball_count.  nbkd_query_ball_csr waits (its offsets are
  * host memory), and the first call of a tree, or one needing more scratch than
- * any before it, may also wait while the scratch grows.  Calls on
- * one tree are serialised, and a call on another stream first waits for the
- * tree's previous call to finish on the device (the tree's scratch memory is
- * reused).
+ * any before it, may also wait while the scratch grows.  Calls on one tree
+ * from several host threads run concurrently (the reference's query is const,
+ * kdtree/src/cpp/pybind.cpp:90): a tree keeps up to 4 scratch workspaces and
+ * each call holds one; a call reusing a workspace from another stream first
+ * waits for that workspace's previous call on the device.
+ *
+ * Host buffers of any size: a call with host queries or host outputs runs in
+ * batches of "host_batch" queries (nbkd_set_tuning; default ~1 GiB of queries
+ * and results per batch) through two device slots, the next batch's queries
+ * copied in and the previous batch's results copied out on a second stream
+ * while one batch computes, so device scratch stays bounded for any m (the
+ * reference streams any m its host memory holds, pybind.cpp:103-104,164-172).
+ * Between batches the call runs the thread's interrupt check
+ * (nbkd_set_interrupt; the reference polls PyErr_CheckSignals every 1000
+ * queries, pybind.cpp:128-133) and returns NBKD_EINTR when it asks to stop.
  *
  * Every entry point returns an nbkd_status; on failure nbkd_last_error()
  * (thread-local) holds a message.  Statuses NBKD_EINVAL / NBKD_EBOX /
@@ -44,7 +55,8 @@ enum {
     NBKD_EBOX = 2,     /* periodic build: a coordinate outside [0, box_size]           */
     NBKD_ETOOMANY = 3, /* more than UINT32_MAX (padded) points                         */
     NBKD_ENOMEM = 4,   /* host or device allocation failed                             */
-    NBKD_EDEVICE = 5   /* HIP runtime error, no device, or kernel failure              */
+    NBKD_EDEVICE = 5,  /* HIP runtime error, no device, or kernel failure              */
+    NBKD_EINTR = 6     /* the calling thread's interrupt check asked to stop (nbkd_set_interrupt) */
 };
 
 /* flags */
@@ -137,9 +149,19 @@ void nbkd_free(nbkd_tree *tree);
  *                      whose seed ball holds fewer than k points is re-walked.
  *   "candidate_bytes"  HBM budget of one collect / select batch's candidate
  *                      columns (default 0 = min(24 GiB, free / 4)).
+ *   "host_batch"       queries per batch of a host-buffer call (default 0 =
+ *                      about 1 GiB of queries plus results per batch).
  * NEW (no reference counterpart: kdtree/src/cpp/pybind.cpp:196-216 has no knobs). */
 nbkd_status nbkd_set_tuning(const char *name, double value);
 nbkd_status nbkd_get_tuning(const char *name, double *value);
+
+/* The calling thread's interrupt check: host-buffer query calls (kNN, k-th
+ * distance, radius count) call fn(user) between batches and stop with
+ * NBKD_EINTR when it returns nonzero (results of that call are then
+ * undefined).  NULL removes it.  Replaces the reference's
+ * PyErr_CheckSignals poll (kdtree/src/cpp/pybind.cpp:128-133).  NEW. */
+typedef int (*nbkd_interrupt_fn)(void *user);
+nbkd_status nbkd_set_interrupt(nbkd_interrupt_fn fn, void *user);
 
 /* thread-local message of the last failure on this thread ("" if none) */
 const char *nbkd_last_error(void);

@@ -15,7 +15,7 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("NBKD_LIB") or os.path.join(PKG, "lib", "libnbkd.so")
 HEADER = os.path.join(os.path.dirname(PKG), "include", "nbkd.h")
 
-NBKD_OK, NBKD_EINVAL, NBKD_EBOX, NBKD_ETOOMANY, NBKD_ENOMEM, NBKD_EDEVICE = range(6)
+NBKD_OK, NBKD_EINVAL, NBKD_EBOX, NBKD_ETOOMANY, NBKD_ENOMEM, NBKD_EDEVICE, NBKD_EINTR = range(7)
 NBKD_INPUT_DEVICE = 0x1
 NBKD_OUTPUT_DEVICE = 0x2
 NBKD_ACCUMULATE = 0x4
@@ -67,6 +67,7 @@ _PROTOS = {
     "nbkd_rows_gather": (_i32, [_c_p, _u64, _c_p, _u64, _c_p, _i32, _c_p]),
     "nbkd_rows_scatter": (_i32, [_c_p, _u64, _c_p, _u64, _c_p, _i32, _c_p]),
     "nbkd_set_tuning": (_i32, [ctypes.c_char_p, ctypes.c_double]),
+    "nbkd_set_interrupt": (_i32, [_c_p, _c_p]),
     "nbkd_get_tuning": (_i32, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_double)]),
     "nbkd_comm_probe": (_i32, []),
     "nbkd_comm_unique_id": (_i32, [_c_p]),

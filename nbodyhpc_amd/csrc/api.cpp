@@ -67,6 +67,8 @@ void free_tree(Tree &t) {
     t.idx = nullptr;
     t.nodes = nullptr;
     t.ws.release();
+    for (auto &w : t.ws_extra) w->release();
+    t.ws_extra.clear();
 }
 } // namespace
 
@@ -212,11 +214,43 @@ void tree_free(void *p) {
 
 namespace {
 // nbkd_set_tuning knobs (process-wide); defaults are the measured optima
-std::atomic<double> g_tune[TUNE_N] = {{3.5}, {0.0}};
-const char *const g_tune_names[TUNE_N] = {"knn_seed_margin", "candidate_bytes"};
+std::atomic<double> g_tune[TUNE_N] = {{3.5}, {0.0}, {0.0}};
+const char *const g_tune_names[TUNE_N] = {"knn_seed_margin", "candidate_bytes", "host_batch"};
+thread_local nbkd_interrupt_fn t_intr = nullptr;
+thread_local void *t_intr_user = nullptr;
 } // namespace
 
 double tuning(int id) { return g_tune[id].load(std::memory_order_relaxed); }
+
+bool interrupted() { return t_intr != nullptr && t_intr(t_intr_user) != 0; }
+
+Workspace &acquire_ws(const Tree &t) {
+    if (t.ws.mu.try_lock()) return t.ws;
+    {
+        std::lock_guard<std::mutex> g(t.ws_mu);
+        for (auto &w : t.ws_extra)
+            if (w->mu.try_lock()) return *w;
+        if ((int)t.ws_extra.size() < NBKD_MAX_WS - 1) {
+            t.ws_extra.emplace_back(new Workspace());
+            Workspace &w = *t.ws_extra.back();
+            w.mu.lock();
+            return w;
+        }
+    }
+    t.ws.mu.lock();
+    return t.ws;
+}
+
+AllWs::AllWs(const Tree &t_, hipStream_t s) : t(t_), pool(t_.ws_mu) {
+    locks.emplace_back(t.ws.mu);
+    for (auto &w : t.ws_extra) locks.emplace_back(w->mu);
+    // the stream waits for every workspace's last call
+    auto wait = [&](Workspace &w) {
+        if (w.used && w.done) (void)hipStreamWaitEvent(s, w.done, 0);
+    };
+    wait(t.ws);
+    for (auto &w : t.ws_extra) wait(*w);
+}
 
 void set_error(const std::string &msg) { g_err = msg; }
 
@@ -516,6 +550,12 @@ nbkd_status nbkd_get_tuning(const char *name, double *value) {
     return NBKD_EINVAL;
 }
 
+nbkd_status nbkd_set_interrupt(nbkd_interrupt_fn fn, void *user) {
+    t_intr = fn;
+    t_intr_user = user;
+    return NBKD_OK;
+}
+
 nbkd_status nbkd_timing_enable(int32_t enable) {
     g_timing = enable != 0;
     return NBKD_OK;
@@ -607,6 +647,31 @@ void Workspace::release() {
     if (done) (void)hipEventDestroy(done);
     done = nullptr;
     used = false;
+    for (hipEvent_t &e : pev) {
+        if (e) (void)hipEventDestroy(e);
+        e = nullptr;
+    }
+    if (copy) (void)hipStreamDestroy(copy);
+    copy = nullptr;
+}
+
+hipError_t Workspace::pipe_init() {
+    if (!copy) {
+        hipError_t e = hipStreamCreateWithFlags(&copy, hipStreamNonBlocking);
+        if (e != hipSuccess) {
+            copy = nullptr;
+            return e;
+        }
+    }
+    for (hipEvent_t &ev : pev)
+        if (!ev) {
+            hipError_t e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+            if (e != hipSuccess) {
+                ev = nullptr;
+                return e;
+            }
+        }
+    return hipSuccess;
 }
 
 void Workspace::trim() {

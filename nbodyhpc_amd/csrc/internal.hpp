@@ -6,6 +6,7 @@
 #include <cfloat>
 #include <cstdint>
 #include <cstdlib>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -14,13 +15,19 @@
 
 namespace nbkd {
 
-// Grow-only per-tree scratch for queries (one query at a time per tree:
-// Workspace::mu is held for the whole call).
+// Grow-only scratch for queries.  A tree holds up to NBKD_MAX_WS of them
+// (Tree::ws + Tree::ws_extra): each call locks one for its whole duration, so
+// calls from several host threads on one const tree run concurrently, as the
+// reference's `const` query does (kdtree/src/cpp/pybind.cpp:90).
 enum WsSlot {
     WS_Q = 0, WS_KEYS, WS_KEYS2, WS_ORDER, WS_TMP, WS_HIST, WS_SUMS, WS_OUTD, WS_OUTI,
     WS_COUNT, WS_OFF, WS_IDX, WS_STATS, WS_LIST, WS_LT, WS_TG, WS_CAND, WS_CCOUNT,
-    WS_LIST2, WS_RSORT, WS_KTHD, WS_KTHI, WS_KB, WS_NSLOTS
+    WS_LIST2, WS_RSORT, WS_KTHD, WS_KTHI, WS_KB,
+    // host-buffer pipeline (query.hip host_pipeline): two slots of queries and
+    // of up to two result arrays
+    WS_HQ0, WS_HQ1, WS_HO00, WS_HO01, WS_HO10, WS_HO11, WS_NSLOTS
 };
+constexpr int NBKD_MAX_WS = 4;
 struct Workspace {
     std::mutex mu;
     void *p[WS_NSLOTS] = {};
@@ -32,6 +39,11 @@ struct Workspace {
     hipStream_t last = nullptr;
     hipEvent_t done = nullptr;
     bool used = false;
+    // the host-buffer pipeline's copy stream (non-blocking) and its events:
+    // [0..1] queries in, [2..3] batch computed, per slot
+    hipStream_t copy = nullptr;
+    hipEvent_t pev[4] = {};
+    hipError_t pipe_init(); // creates copy / pev once
     // returns nullptr on failure (hip error recorded via set_error)
     void *get(int slot, size_t bytes, hipStream_t s);
     void release();
@@ -59,6 +71,12 @@ struct WsCall {
     hipStream_t s;
     hipError_t err;
     WsCall(Workspace &w_, hipStream_t s_) : lk(w_.mu), w(w_), s(s_) {
+        hold_mark(&w);
+        err = w.enter(s);
+    }
+    // a workspace already locked by acquire_ws
+    WsCall(Workspace &w_, hipStream_t s_, std::adopt_lock_t)
+        : lk(w_.mu, std::adopt_lock), w(w_), s(s_) {
         hold_mark(&w);
         err = w.enter(s);
     }
@@ -117,6 +135,21 @@ struct Tree {
     uint32_t pad_leaves[NBKD_PAD_LEAVES] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu,
                                             0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
     mutable Workspace ws;
+    // further workspaces for concurrent calls (created on demand, at most
+    // NBKD_MAX_WS - 1), guarded by ws_mu
+    mutable std::mutex ws_mu;
+    mutable std::vector<std::unique_ptr<Workspace>> ws_extra;
+};
+
+// a workspace of t, locked: the first free one, else a new one (up to
+// NBKD_MAX_WS), else wait for the tree's first workspace (api.cpp)
+Workspace &acquire_ws(const Tree &t);
+// every workspace of t locked and drained on stream s (nbkd_set_ids)
+struct AllWs {
+    const Tree &t;
+    std::unique_lock<std::mutex> pool;
+    std::vector<std::unique_lock<std::mutex>> locks;
+    AllWs(const Tree &t_, hipStream_t s);
 };
 
 // plain-value view passed to kernels
@@ -147,7 +180,10 @@ inline const char *knob(const char *env) { return getenv(env); }
 #else
 inline const char *knob(const char *) { return nullptr; }
 #endif
-enum TuneId { TUNE_KNN_SEED = 0, TUNE_CAND_BYTES, TUNE_N };
+enum TuneId { TUNE_KNN_SEED = 0, TUNE_CAND_BYTES, TUNE_HOST_BATCH, TUNE_N };
+// the calling thread's interrupt check (nbkd_set_interrupt): true = abandon
+// the call (host-buffer calls check it between batches)
+bool interrupted();
 double tuning(int id); // api.cpp (nbkd_set_tuning)
 
 // error plumbing (api.cpp)

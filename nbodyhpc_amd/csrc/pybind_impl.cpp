@@ -9,7 +9,12 @@
 // (query_ball_count / query_ball_csr) and export() for parity tests.
 // `max_threads` and `workers` are accepted and ignored: the build and the
 // queries run on the GPU (the reference ignores max_threads too,
-// kdtree/src/cpp/kdtree.cpp:116).
+// kdtree/src/cpp/kdtree.cpp:116).  Queries release the GIL, may be called from
+// several Python threads on one tree at once (the library gives each call its
+// own scratch), accept any number of rows (host buffers stream through bounded
+// device memory) and stop with KeyboardInterrupt on Ctrl-C: the library polls
+// PyErr_CheckSignals between batches, as the reference does every 1000 queries
+// (kdtree/src/cpp/pybind.cpp:128-133).
 #include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
@@ -31,6 +36,29 @@ using farray = py::array_t<float, py::array::c_style | py::array::forcecast>;
     if (st == NBKD_ENOMEM) throw std::bad_alloc();
     throw std::runtime_error(nbkd_last_error());
 }
+
+// nbkd_set_interrupt callback: runs on the calling thread between batches of a
+// host-buffer query, with the GIL released around it
+int check_signals(void *hit) {
+    py::gil_scoped_acquire gil;
+    if (PyErr_CheckSignals() != 0) { // pybind.cpp:128-133
+        *static_cast<bool *>(hit) = true;
+        return 1;
+    }
+    return 0;
+}
+
+// one query call: the interrupt check installed for its duration (GIL held
+// when constructed and when finish() runs)
+struct Interruptible {
+    bool hit = false;
+    Interruptible() { nbkd_set_interrupt(check_signals, &hit); }
+    ~Interruptible() { nbkd_set_interrupt(nullptr, nullptr); }
+    void finish(nbkd_status st) {
+        if (st == NBKD_EINTR && hit) throw py::error_already_set(); // KeyboardInterrupt
+        if (st != NBKD_OK) raise(st);
+    }
+};
 
 void check(nbkd_status st) {
     if (st != NBKD_OK) raise(st);
@@ -90,11 +118,12 @@ class PyKDTree {
         float *d = dist.mutable_data();
         uint32_t *i = idx.mutable_data();
         nbkd_status st;
+        Interruptible intr;
         {
             py::gil_scoped_release nogil;
             st = nbkd_query_knn(h_, q, (uint64_t)m, k, d, i, 0u, nullptr);
         }
-        check(st);
+        intr.finish(st);
         return {dist, idx};
     }
 
@@ -107,11 +136,12 @@ class PyKDTree {
         const float *q = points.data();
         float *o = out.mutable_data();
         nbkd_status st;
+        Interruptible intr;
         {
             py::gil_scoped_release nogil;
             st = nbkd_query_kth(h_, q, (uint64_t)m, k, o, 0u, nullptr);
         }
-        check(st);
+        intr.finish(st);
         return out;
     }
 
@@ -122,11 +152,12 @@ class PyKDTree {
         const float *q = points.data();
         uint32_t *o = out.mutable_data();
         nbkd_status st;
+        Interruptible intr;
         {
             py::gil_scoped_release nogil;
             st = nbkd_query_ball_count(h_, q, (uint64_t)m, r, o, 0u, nullptr);
         }
-        check(st);
+        intr.finish(st);
         return out;
     }
 

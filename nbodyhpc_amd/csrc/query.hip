@@ -831,9 +831,8 @@ SeedParams seed_params(const Tree &t, int k) {
     return p;
 }
 
-nbkd_status sort_queries(const Tree &t, const float *dq, uint32_t m, uint32_t *&order,
+nbkd_status sort_queries(const Tree &t, Workspace &ws, const float *dq, uint32_t m, uint32_t *&order,
                          hipStream_t s, float *tg = nullptr, const SeedParams *sp = nullptr) {
-    Workspace &ws = t.ws;
     order = (uint32_t *)ws.get(WS_ORDER, (size_t)m * 4, s);
     uint32_t *tmp = (uint32_t *)ws.get(WS_TMP, (size_t)m * 4, s);
     uint32_t *keys = (uint32_t *)ws.get(WS_KEYS, (size_t)m * 4, s);
@@ -873,13 +872,13 @@ nbkd_status sort_queries(const Tree &t, const float *dq, uint32_t m, uint32_t *&
     return radix_sort(ws, keys, order, keys2, tmp, m, key_bits(t), s, &order);
 }
 
-nbkd_status stage_queries(const Tree &t, const float *q, uint64_t m, uint32_t flags,
+nbkd_status stage_queries(Workspace &ws, const float *q, uint64_t m, uint32_t flags,
                           const float *&dq, hipStream_t s) {
     if (flags & NBKD_INPUT_DEVICE) {
         dq = q;
         return NBKD_OK;
     }
-    float *buf = (float *)t.ws.get(WS_Q, m * 3 * sizeof(float), s);
+    float *buf = (float *)ws.get(WS_Q, m * 3 * sizeof(float), s);
     if (!buf) return NBKD_ENOMEM;
     NBKD_HIP(hipMemcpyAsync(buf, q, m * 3 * sizeof(float), hipMemcpyHostToDevice, s));
     NBKD_HIP(hipStreamSynchronize(s));
@@ -927,14 +926,14 @@ bool collect_disabled() {
 
 // out_i == nullptr: k-th distance only (out_d: m floats); the caller
 // (query_kth) uses it only where the collect/select path runs
-nbkd_status knn_locked(const Tree &t, const float *q, uint64_t m, int k, float *out_d,
+nbkd_status knn_locked(const Tree &t, Workspace &ws, const float *q, uint64_t m, int k, float *out_d,
                        uint32_t *out_i, uint32_t flags, hipStream_t s) {
     const uint32_t mm = (uint32_t)m;
     const bool kth_only = out_i == nullptr;
     const bool sq = (flags & NBKD_SQUARED) != 0;
     const size_t row_words = kth_only ? 1 : (size_t)k;
     const float *dq = nullptr;
-    nbkd_status rc = stage_queries(t, q, m, flags, dq, s);
+    nbkd_status rc = stage_queries(ws, q, m, flags, dq, s);
     if (rc) return rc;
     // the collect / select path needs the sub-leaf groups (every non-empty
     // tree has them); k > 1024 and the empty tree take the exact kernel
@@ -942,22 +941,22 @@ nbkd_status knn_locked(const Tree &t, const float *q, uint64_t m, int k, float *
     const SeedParams sp = seed_params(t, k);
     float *tg = nullptr;
     if (packet && sp.on) {
-        tg = (float *)t.ws.get(WS_TG, (size_t)mm * 4, s);
+        tg = (float *)ws.get(WS_TG, (size_t)mm * 4, s);
         if (!tg) return NBKD_ENOMEM;
     }
     uint32_t *ord = nullptr;
-    rc = sort_queries(t, dq, mm, ord, s, tg, &sp);
+    rc = sort_queries(t, ws, dq, mm, ord, s, tg, &sp);
     if (rc) return rc;
     float *dd = out_d;
     uint32_t *di = out_i;
     if (!(flags & NBKD_OUTPUT_DEVICE)) {
-        dd = (float *)t.ws.get(WS_OUTD, m * row_words * 4, s);
-        di = kth_only ? nullptr : (uint32_t *)t.ws.get(WS_OUTI, m * (size_t)k * 4, s);
+        dd = (float *)ws.get(WS_OUTD, m * row_words * 4, s);
+        di = kth_only ? nullptr : (uint32_t *)ws.get(WS_OUTI, m * (size_t)k * 4, s);
         if (!dd || (!di && !kth_only)) return NBKD_ENOMEM;
     }
     unsigned long long *stats = nullptr;
     if (stats_enabled()) {
-        stats = (unsigned long long *)t.ws.get(WS_STATS, NBKD_NSTATS * 8, s);
+        stats = (unsigned long long *)ws.get(WS_STATS, NBKD_NSTATS * 8, s);
         if (!stats) return NBKD_ENOMEM;
         NBKD_HIP(hipMemsetAsync(stats, 0, NBKD_NSTATS * 8, s));
     }
@@ -966,7 +965,7 @@ nbkd_status knn_locked(const Tree &t, const float *q, uint64_t m, int k, float *
     // and queries whose seed radius held fewer than k points
     uint32_t *list = nullptr, *count = nullptr;
     if (packet && (t.periodic || tg)) {
-        list = (uint32_t *)t.ws.get(WS_LIST, (size_t)mm * 4 + 16, s);
+        list = (uint32_t *)ws.get(WS_LIST, (size_t)mm * 4 + 16, s);
         if (!list) return NBKD_ENOMEM;
         count = list + mm;
         NBKD_HIP(hipMemsetAsync(count, 0, 4, s));
@@ -982,7 +981,7 @@ nbkd_status knn_locked(const Tree &t, const float *q, uint64_t m, int k, float *
             std::max<uint64_t>((512ull << 20) / (32ull * (uint64_t)k), TB), 65536ull);
         threads = (uint32_t)std::min<uint64_t>(threads, ((uint64_t)mm + TB - 1) / TB * TB);
         threads = std::max<uint32_t>(threads / TB * TB, TB);
-        LtEntry *lt = (LtEntry *)t.ws.get(WS_LT, (size_t)threads * 2 * k * sizeof(LtEntry), s);
+        LtEntry *lt = (LtEntry *)ws.get(WS_LT, (size_t)threads * 2 * k * sizeof(LtEntry), s);
         if (!lt) return NBKD_ENOMEM;
         if (t.periodic)
             knn_exact_kernel<true><<<threads / TB, TB, 0, s>>>(view(t), dq, ord, nullptr, mm, k,
@@ -1021,13 +1020,13 @@ nbkd_status knn_locked(const Tree &t, const float *q, uint64_t m, int k, float *
             const uint64_t cand_bytes =
                 std::max<uint64_t>({batch * capg * 8u, cap1 * capr * 8u, cap2 * capr2 * 8u});
             const uint64_t cc_words = std::max<uint64_t>(batch, cap1);
-            uint2 *cand = (uint2 *)t.ws.get(WS_CAND, cand_bytes, s);
-            uint32_t *ccount = (uint32_t *)t.ws.get(WS_CCOUNT, cc_words * 4u, s);
+            uint2 *cand = (uint2 *)ws.get(WS_CAND, cand_bytes, s);
+            uint32_t *ccount = (uint32_t *)ws.get(WS_CCOUNT, cc_words * 4u, s);
             // k > 64: per-query final bounds, collect -> wave select (any batch
             // of any round holds at most max(batch, mm) queries)
             float *kb = nullptr;
             if (k > 64) {
-                kb = (float *)t.ws.get(WS_KB, std::max<uint64_t>(batch, (uint64_t)mm) * 4u, s);
+                kb = (float *)ws.get(WS_KB, std::max<uint64_t>(batch, (uint64_t)mm) * 4u, s);
                 if (!kb) return NBKD_ENOMEM;
             }
             // Seed failures (fewer than k points in the seed ball, or more than
@@ -1038,8 +1037,8 @@ nbkd_status knn_locked(const Tree &t, const float *q, uint64_t m, int k, float *
             // fixed grids that read that count (QSpan), and what a round does
             // not resolve goes to the next one, the last to the exact kernel.
             const uint64_t nwords = ((uint64_t)mm + 31) / 32;
-            uint32_t *bits = (uint32_t *)t.ws.get(WS_RSORT, nwords * 4u + 64u, s);
-            uint32_t *rq = (uint32_t *)t.ws.get(WS_LIST2, (size_t)mm * 8 + 256, s);
+            uint32_t *bits = (uint32_t *)ws.get(WS_RSORT, nwords * 4u + 64u, s);
+            uint32_t *rq = (uint32_t *)ws.get(WS_LIST2, (size_t)mm * 8 + 256, s);
             if (!cand || !ccount || !bits || !rq) return NBKD_ENOMEM;
             uint32_t *rq_count = rq + (size_t)mm;      // round-1 queries (compaction)
             uint32_t *r2 = rq_count + 16;               // round-2 list (ids)
@@ -1060,7 +1059,7 @@ nbkd_status knn_locked(const Tree &t, const float *q, uint64_t m, int k, float *
             }
             {
                 TimedScope ts2("knn_retry_order", s);
-                rc = compact_failures(t.ws, bits, mm, ord, rq, rq_count, s);
+                rc = compact_failures(ws, bits, mm, ord, rq, rq_count, s);
                 if (rc) return rc;
             }
             if (stats) NBKD_HIP(hipMemcpyAsync(stats + 9, rq_count, 4, hipMemcpyDeviceToDevice, s));
@@ -1124,7 +1123,7 @@ nbkd_status knn_locked(const Tree &t, const float *q, uint64_t m, int k, float *
         if (list) {
             TimedScope ts("knn_fallback", s);
             const uint32_t threads = 16384;
-            LtEntry *lt = (LtEntry *)t.ws.get(WS_LT, (size_t)threads * 2 * k * sizeof(LtEntry), s);
+            LtEntry *lt = (LtEntry *)ws.get(WS_LT, (size_t)threads * 2 * k * sizeof(LtEntry), s);
             if (!lt) return NBKD_ENOMEM;
             if (t.periodic)
                 knn_exact_kernel<true><<<threads / TB, TB, 0, s>>>(view(t), dq, list, count, mm, k,
@@ -1172,45 +1171,153 @@ kth_column_kernel(const float *__restrict__ rows, uint32_t m, int k, float *__re
 
 } // namespace
 
+// Host-buffer calls of any size (a 1e9-query host call needed
+// ~256 GB of device row scratch).  The m queries run in batches of hb through
+// two device slots: while batch i computes on `s`, the copy stream `cp` brings
+// batch i+1's queries in and takes batch i-1's results out (pageable copies,
+// staged by the runtime), so device scratch is bounded by hb whatever m is.
+// run(dq, nb, outs, s) enqueues one batch with device inputs and outputs.
+// Inputs or outputs already on the device are used in place.  The thread's
+// interrupt check (nbkd_set_interrupt) runs between batches.
+uint64_t host_batch(size_t bytes_per_query, uint64_t m) {
+    const double tb = tuning(TUNE_HOST_BATCH);
+    uint64_t hb = tb > 0.0 ? (uint64_t)tb
+                           : (1ull << 30) / std::max<size_t>(bytes_per_query, 1);
+    hb = std::max<uint64_t>(hb / 64 * 64, 64);
+    return std::min<uint64_t>(hb, m);
+}
+
+template <typename Run>
+nbkd_status host_pipeline(Workspace &ws, const float *q, uint64_t m, uint32_t flags, int nout,
+                          const size_t *obytes, void *const *outs, Run run, hipStream_t s) {
+    const bool in_dev = (flags & NBKD_INPUT_DEVICE) != 0, out_dev = (flags & NBKD_OUTPUT_DEVICE) != 0;
+    size_t per_q = in_dev ? 0 : 12;
+    for (int j = 0; j < nout; ++j) per_q += out_dev ? 0 : obytes[j];
+    const uint64_t hb = host_batch(per_q, m);
+    NBKD_HIP(ws.pipe_init());
+    hipStream_t cp = ws.copy;
+    hipEvent_t *ev_in = ws.pev, *ev_comp = ws.pev + 2;
+    // the previous call of this workspace may still use the slots
+    if (ws.used && ws.done) NBKD_HIP(hipStreamWaitEvent(cp, ws.done, 0));
+    const int nbat_slots = m > hb ? 2 : 1;
+    float *qslot[2] = {nullptr, nullptr};
+    void *oslot[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
+    for (int b = 0; b < nbat_slots; ++b) {
+        if (!in_dev) {
+            qslot[b] = (float *)ws.get(WS_HQ0 + b, hb * 12, s);
+            if (!qslot[b]) return NBKD_ENOMEM;
+        }
+        if (!out_dev)
+            for (int j = 0; j < nout; ++j) {
+                oslot[b][j] = ws.get(WS_HO00 + 2 * b + j, hb * obytes[j], s);
+                if (!oslot[b][j]) return NBKD_ENOMEM;
+            }
+    }
+    nbkd_status rc = NBKD_OK;
+    bool comp_rec[2] = {false, false};
+    const uint64_t nbat = (m + hb - 1) / hb;
+    for (uint64_t i = 0; i <= nbat && rc == NBKD_OK; ++i) {
+        if (i < nbat) {
+            const int b = (int)(i & 1) % nbat_slots;
+            const uint64_t b0 = i * hb, nb = std::min<uint64_t>(hb, m - b0);
+            if (i > 0 && interrupted()) {
+                set_error("interrupted");
+                rc = NBKD_EINTR;
+                break;
+            }
+            const float *dq = q + 3 * b0;
+            if (!in_dev) {
+                // the slot's previous batch has finished reading it
+                if (comp_rec[b]) NBKD_HIP(hipStreamWaitEvent(cp, ev_comp[b], 0));
+                NBKD_HIP(hipMemcpyAsync(qslot[b], q + 3 * b0, nb * 12, hipMemcpyHostToDevice, cp));
+                NBKD_HIP(hipEventRecord(ev_in[b], cp));
+                NBKD_HIP(hipStreamWaitEvent(s, ev_in[b], 0));
+                dq = qslot[b];
+            }
+            void *o[2] = {nullptr, nullptr};
+            for (int j = 0; j < nout; ++j)
+                o[j] = out_dev ? (void *)((char *)outs[j] + b0 * obytes[j]) : oslot[b][j];
+            rc = run(dq, nb, o, s);
+            if (rc) break;
+            NBKD_HIP(hipEventRecord(ev_comp[b], s));
+            comp_rec[b] = true;
+        }
+        if (i >= 1 && !out_dev) {
+            // batch i-1's results (computed on s) out on cp, into the caller's
+            // memory; returns once they have landed, so its slot is free again
+            const int pb = (int)((i - 1) & 1) % nbat_slots;
+            const uint64_t p0 = (i - 1) * hb, pn = std::min<uint64_t>(hb, m - p0);
+            NBKD_HIP(hipStreamWaitEvent(cp, ev_comp[pb], 0));
+            for (int j = 0; j < nout; ++j)
+                NBKD_HIP(hipMemcpyAsync((char *)outs[j] + p0 * obytes[j], oslot[pb][j],
+                                        pn * obytes[j], hipMemcpyDeviceToHost, cp));
+            NBKD_HIP(hipStreamSynchronize(cp));
+        }
+    }
+    if (rc) {
+        // nothing of this call may still touch the slots or the caller's memory
+        (void)hipStreamSynchronize(s);
+        (void)hipStreamSynchronize(cp);
+        return rc;
+    }
+    // host queries: the caller may free them once the call returns
+    if (!in_dev) NBKD_HIP(hipStreamSynchronize(cp));
+    return NBKD_OK;
+}
+
 nbkd_status query_knn(const Tree &t, const float *q, uint64_t m, int k, float *out_d,
                       uint32_t *out_i, uint32_t flags, hipStream_t s) {
     nbkd_status rc = knn_args(k, m);
     if (rc || m == 0) return rc;
-    WsCall call(t.ws, s);
+    Workspace &ws = acquire_ws(t);
+    WsCall call(ws, s, std::adopt_lock);
     NBKD_HIP(call.err);
-    return knn_locked(t, q, m, k, out_d, out_i, flags, s);
+    const uint32_t dev_io = NBKD_INPUT_DEVICE | NBKD_OUTPUT_DEVICE;
+    if ((flags & dev_io) == dev_io) return knn_locked(t, ws, q, m, k, out_d, out_i, flags, s);
+    const size_t ob[2] = {(size_t)k * 4, (size_t)k * 4};
+    void *const outs[2] = {out_d, out_i};
+    return host_pipeline(ws, q, m, flags, 2, ob, outs,
+                         [&](const float *dq, uint64_t nb, void *const *o, hipStream_t st) {
+                             return knn_locked(t, ws, dq, nb, k, (float *)o[0], (uint32_t *)o[1],
+                                               flags | dev_io, st);
+                         }, s);
+}
+
+// device in, device out: the k-th distances of m queries
+static nbkd_status kth_locked(const Tree &t, Workspace &ws, const float *dq, uint64_t m, int k,
+                              float *out_d, uint32_t flags, hipStream_t s) {
+    // the collect/select path writes the k-th distance alone; elsewhere the
+    // rows go to scratch and column k-1 is copied out
+    if (k <= KNN_PACKET_KMAX && t.ginfo && seed_params(t, k).on && !collect_disabled())
+        return knn_locked(t, ws, dq, m, k, out_d, nullptr, flags, s);
+    float *rd = (float *)ws.get(WS_KTHD, m * (size_t)k * 4, s);
+    uint32_t *ri = (uint32_t *)ws.get(WS_KTHI, m * (size_t)k * 4, s);
+    if (!rd || !ri) return NBKD_ENOMEM;
+    nbkd_status rc = knn_locked(t, ws, dq, m, k, rd, ri, flags, s);
+    if (rc) return rc;
+    kth_column_kernel<<<(unsigned)((m + TB - 1) / TB), TB, 0, s>>>(rd, (uint32_t)m, k, out_d);
+    NBKD_HIP(hipGetLastError());
+    return NBKD_OK;
 }
 
 nbkd_status query_kth(const Tree &t, const float *q, uint64_t m, int k, float *out_d,
                       uint32_t flags, hipStream_t s) {
     nbkd_status rc = knn_args(k, m);
     if (rc || m == 0) return rc;
-    WsCall call(t.ws, s);
+    Workspace &ws = acquire_ws(t);
+    WsCall call(ws, s, std::adopt_lock);
     NBKD_HIP(call.err);
-    // the collect/select path writes the k-th distance alone; elsewhere the
-    // rows go to scratch and column k-1 is copied out
-    if (k <= KNN_PACKET_KMAX && t.ginfo && seed_params(t, k).on && !collect_disabled())
-        return knn_locked(t, q, m, k, out_d, nullptr, flags, s);
-    float *rd = (float *)t.ws.get(WS_KTHD, m * (size_t)k * 4, s);
-    uint32_t *ri = (uint32_t *)t.ws.get(WS_KTHI, m * (size_t)k * 4, s);
-    if (!rd || !ri) return NBKD_ENOMEM;
-    rc = knn_locked(t, q, m, k, rd, ri, flags | NBKD_OUTPUT_DEVICE, s);
-    if (rc) return rc;
-    float *dst = out_d;
-    if (!(flags & NBKD_OUTPUT_DEVICE)) {
-        dst = (float *)t.ws.get(WS_OUTD, m * 4, s);
-        if (!dst) return NBKD_ENOMEM;
-    }
-    kth_column_kernel<<<(unsigned)((m + TB - 1) / TB), TB, 0, s>>>(rd, (uint32_t)m, k, dst);
-    NBKD_HIP(hipGetLastError());
-    if (!(flags & NBKD_OUTPUT_DEVICE)) {
-        NBKD_HIP(hipMemcpyAsync(out_d, dst, m * 4, hipMemcpyDeviceToHost, s));
-        NBKD_HIP(hipStreamSynchronize(s));
-    }
-    return NBKD_OK;
+    const uint32_t dev_io = NBKD_INPUT_DEVICE | NBKD_OUTPUT_DEVICE;
+    if ((flags & dev_io) == dev_io) return kth_locked(t, ws, q, m, k, out_d, flags, s);
+    const size_t ob[1] = {4};
+    void *const outs[1] = {out_d};
+    return host_pipeline(ws, q, m, flags, 1, ob, outs,
+                         [&](const float *dq, uint64_t nb, void *const *o, hipStream_t st) {
+                             return kth_locked(t, ws, dq, nb, k, (float *)o[0], flags | dev_io, st);
+                         }, s);
 }
 
-static nbkd_status ball_common(const Tree &t, const float *q, uint64_t m, float r,
+static nbkd_status ball_common(const Tree &t, Workspace &ws, const float *q, uint64_t m, float r,
                                uint32_t *out_count, uint64_t *offsets, uint32_t *out_idx,
                                uint64_t capacity, uint32_t flags, hipStream_t s) {
     if (m >= (1ull << 32)) {
@@ -1222,13 +1329,11 @@ static nbkd_status ball_common(const Tree &t, const float *q, uint64_t m, float 
         return NBKD_OK;
     }
     const uint32_t mm = (uint32_t)m;
-    WsCall call(t.ws, s);
-    NBKD_HIP(call.err);
     const float *dq = nullptr;
-    nbkd_status rc = stage_queries(t, q, m, flags, dq, s);
+    nbkd_status rc = stage_queries(ws, q, m, flags, dq, s);
     if (rc) return rc;
     uint32_t *ord = nullptr;
-    rc = sort_queries(t, dq, mm, ord, s);
+    rc = sort_queries(t, ws, dq, mm, ord, s);
     if (rc) return rc;
     const float r2 = r * r;
     // periodic queries outside [0, L]^3: listed, every point tested for them.
@@ -1237,7 +1342,7 @@ static nbkd_status ball_common(const Tree &t, const float *q, uint64_t m, float 
     uint32_t *list = nullptr, nout = 0;
     const bool count_only = offsets == nullptr;
     if (t.periodic) {
-        list = (uint32_t *)t.ws.get(WS_LIST, (size_t)mm * 8 + 16, s);
+        list = (uint32_t *)ws.get(WS_LIST, (size_t)mm * 8 + 16, s);
         if (!list) return NBKD_ENOMEM;
         NBKD_HIP(hipMemsetAsync(list + mm, 0, 4, s));
         outside_box_kernel<<<(mm + TB - 1) / TB, TB, 0, s>>>(dq, mm, t.box, list, list + mm);
@@ -1258,7 +1363,7 @@ static nbkd_status ball_common(const Tree &t, const float *q, uint64_t m, float 
     uint32_t *cnt = out_count;
     const bool dev_out = flags & NBKD_OUTPUT_DEVICE;
     if (!cnt || !dev_out) {
-        cnt = (uint32_t *)t.ws.get(WS_COUNT, m * 4, s);
+        cnt = (uint32_t *)ws.get(WS_COUNT, m * 4, s);
         if (!cnt) return NBKD_ENOMEM;
     }
     {
@@ -1284,13 +1389,13 @@ static nbkd_status ball_common(const Tree &t, const float *q, uint64_t m, float 
         set_error("query_ball_csr: capacity smaller than the number of neighbours");
         return NBKD_EINVAL;
     }
-    uint64_t *doff = (uint64_t *)t.ws.get(WS_OFF, (m + 1) * 8, s);
+    uint64_t *doff = (uint64_t *)ws.get(WS_OFF, (m + 1) * 8, s);
     if (!doff) return NBKD_ENOMEM;
     NBKD_HIP(hipMemcpyAsync(doff, offsets, (m + 1) * 8, hipMemcpyHostToDevice, s));
     NBKD_HIP(hipStreamSynchronize(s));
     uint32_t *di = out_idx;
     if (!dev_out) {
-        di = (uint32_t *)t.ws.get(WS_IDX, std::max<uint64_t>(offsets[m], 1) * 4, s);
+        di = (uint32_t *)ws.get(WS_IDX, std::max<uint64_t>(offsets[m], 1) * 4, s);
         if (!di) return NBKD_ENOMEM;
     }
     {
@@ -1307,12 +1412,40 @@ static nbkd_status ball_common(const Tree &t, const float *q, uint64_t m, float 
 
 nbkd_status query_ball_count(const Tree &t, const float *q, uint64_t m, float r,
                              uint32_t *out_count, uint32_t flags, hipStream_t s) {
-    return ball_common(t, q, m, r, out_count, nullptr, nullptr, 0, flags, s);
+    if (m >= (1ull << 32)) {
+        set_error("more than 2^32 - 1 queries per call are not supported");
+        return NBKD_EINVAL;
+    }
+    if (m == 0) return NBKD_OK;
+    Workspace &ws = acquire_ws(t);
+    WsCall call(ws, s, std::adopt_lock);
+    NBKD_HIP(call.err);
+    const uint32_t dev_io = NBKD_INPUT_DEVICE | NBKD_OUTPUT_DEVICE;
+    if ((flags & dev_io) == dev_io)
+        return ball_common(t, ws, q, m, r, out_count, nullptr, nullptr, 0, flags, s);
+    const size_t ob[1] = {4};
+    void *const outs[1] = {out_count};
+    return host_pipeline(ws, q, m, flags, 1, ob, outs,
+                         [&](const float *dq, uint64_t nb, void *const *o, hipStream_t st) {
+                             return ball_common(t, ws, dq, nb, r, (uint32_t *)o[0], nullptr,
+                                                nullptr, 0, flags | dev_io, st);
+                         }, s);
 }
 
 nbkd_status query_ball_csr(const Tree &t, const float *q, uint64_t m, float r, uint64_t *offsets,
                            uint32_t *out_idx, uint64_t capacity, uint32_t flags, hipStream_t s) {
-    return ball_common(t, q, m, r, nullptr, offsets, out_idx, capacity, flags, s);
+    if (m >= (1ull << 32)) {
+        set_error("more than 2^32 - 1 queries per call are not supported");
+        return NBKD_EINVAL;
+    }
+    if (m == 0) {
+        if (offsets) offsets[0] = 0;
+        return NBKD_OK;
+    }
+    Workspace &ws = acquire_ws(t);
+    WsCall call(ws, s, std::adopt_lock);
+    NBKD_HIP(call.err);
+    return ball_common(t, ws, q, m, r, nullptr, offsets, out_idx, capacity, flags, s);
 }
 
 } // namespace nbkd

@@ -277,8 +277,7 @@ nbkd_status nbkd_set_ids(nbkd_tree *tree, const uint32_t *ids, uint32_t flags, v
     if (t.n8 == 0) return NBKD_OK;
     DevGuard g(t.device);
     hipStream_t s = (hipStream_t)stream;
-    WsCall call(t.ws, s);
-    NBKD_HIP(call.err);
+    AllWs all(t, s); // no query of this tree runs while its ids change
     const uint32_t *dids = ids;
     DevBuf tmp;
     if (!(flags & NBKD_INPUT_DEVICE)) {
@@ -290,7 +289,8 @@ nbkd_status nbkd_set_ids(nbkd_tree *tree, const uint32_t *ids, uint32_t flags, v
     const unsigned blocks = (unsigned)((t.n8 + 255) / 256);
     remap_ids_kernel<<<blocks, 256, 0, s>>>(t.idx, t.n8, t.n, dids);
     NBKD_HIP(hipGetLastError());
-    if (tmp.p) NBKD_HIP(hipStreamSynchronize(s));
+    // every later call on any workspace (any stream) sees the new ids
+    NBKD_HIP(hipStreamSynchronize(s));
     return NBKD_OK;
     SLAB_CATCH
 }
