@@ -3,9 +3,9 @@
   nbodyhpc_amd/lib/libnbkd.so              hipcc --offload-arch=gfx950: C ABI + HIP kernels
   nbodyhpc_amd/kdtree/_impl<ext-suffix>    g++: pybind11 module over the C ABI
   nbodyhpc_amd/lib/exp/libnbkd.so          (--experiments only) the same sources with
-                                           -DNBKD_EXPERIMENTS: the A/B kernels and the
-                                           NBKD_* environment overrides; loaded only
-                                           through NBKD_LIB, never by default
+                                           -DNBKD_EXPERIMENTS: the NBKD_* environment
+                                           overrides of the tuning knobs (A/B runs);
+                                           loaded only through NBKD_LIB, never by default
 
 Both are built in-tree so they travel with the repo snapshot to the GPU box.
 `python -m nbodyhpc_amd.build [--force] [--experiments]`.
@@ -32,8 +32,8 @@ ARCH = os.environ.get("NBKD_ARCH", "gfx950")
 # squared distances stop being bit-identical.
 HIP_FLAGS = ["--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
              "-Wall", "-Wno-unused-function", "-Wno-unused-const-variable"]
-SOURCES = ["api.cpp", "build.hip", "query.hip", "knn_packet.hip", "knn_collect.hip", "ball.hip",
-           "slab.hip", "deposit.hip"]
+SOURCES = ["api.cpp", "build.hip", "query.hip", "knn_collect.hip", "ball.hip", "slab.hip",
+           "deposit.hip"]
 HEADERS = [os.path.join(CSRC, "internal.hpp"), os.path.join(CSRC, "metric.hpp"),
            os.path.join(CSRC, "packet.hpp"),
            os.path.join(ROOT, "include", "nbkd.h")]

@@ -251,13 +251,6 @@ void tree_free(void *p);
 nbkd_status build_tree(Tree &t, const float *xyz, uint64_t n, int32_t leaf_size, bool input_dev,
                        hipStream_t s);
 
-// knn_packet.hip
-// tg: per-query seed bound on the k-th squared distance (nullptr: none); queries
-// that end with fewer than k points below it are appended to fail_list
-void launch_knn_packet(const Tree &t, const float *q, const uint32_t *order, uint32_t m, int k,
-                       const float *tg, float *od, uint32_t *oi, uint32_t *fail_list,
-                       uint32_t *fail_count, unsigned long long *stats, hipStream_t s);
-
 // The queries one collect / select pass handles (order[0 .. m)): a count known
 // on the host (count == nullptr: m), or, for the retry rounds, a count the
 // previous round left in device memory: m = min(*count - base, cap), 0 when

@@ -38,7 +38,6 @@ using namespace dev;
 
 constexpr int TB = 256;
 constexpr int WPB = TB / 64;
-constexpr int CHUNK = 32; // leaf points staged per step (leaves hold <= 32 at leafsize 32)
 
 constexpr int NB = 16; // distance buckets of the bound histogram
 
@@ -56,366 +55,6 @@ __device__ __forceinline__ uint32_t d2_bucket(float d, float c) {
     return min((uint32_t)(d * c), (uint32_t)(NB - 1));
 }
 
-#ifdef NBKD_EXPERIMENTS // the round-1 leaf-level scan, A/B only (NBKD_GROUPS=0)
-struct CollectLds {
-    // sparse mode, indexed by slot (the rank of a needing lane): its query xyz +
-    // bound, its bucket factor (d2_bucket) and its lane
-    float4 sq[64];
-    float scl[64];
-    uint8_t owners[64];
-    uint32_t cnt[64];          // per lane: candidates appended
-    uint32_t hist[NB / 4][64]; // per lane: NB 8-bit counts of candidates by d2 bucket
-    float pb[2][3][CHUNK]; // leaf points, double-buffered (PIPE)
-    float tb[2][8];        // the leaf's tight box (leafinfo words)
-};
-
-// Candidate columns, entries {d2 bits, tree position}: packet pk owns
-// cand[pk * 64 * capg ...) as capg/16 blocks of 64 lanes x 16 slots; slot s of
-// lane l sits at block s/16, row l, column s%16.  A lane appends in order, so
-// it fills whole 128-B lines (a slot-major layout left lines partly written and
-// tripled the HBM write traffic), and select reads each block as one contiguous
-// 8-KB run, transposed through LDS.
-// advance the packet walk to the next leaf some lane wants (FOUND = false: walk done)
-#define NBKD_COLLECT_WALK(FOUND, LEAF, LPOS, LEND)                                                             \
-    FOUND = false;                                                                                             \
-    for (;;) {                                                                                                 \
-        if (!have) {                                                                                           \
-            if (sp == 0) break;                                                                                \
-            --sp;                                                                                              \
-            node = __builtin_amdgcn_readlane(sk_node, sp);                                                     \
-_Pragma("unroll")                                                                                              \
-            for (int a = 0; a < 6; ++a) bx[a] = rdlane(sk_b[a], sp);                                           \
-            tm[0] = box_lb_axis<PER>(qx, bx[0], bx[1], L);                                                     \
-            tm[1] = box_lb_axis<PER>(qy, bx[2], bx[3], L);                                                     \
-            tm[2] = box_lb_axis<PER>(qz, bx[4], bx[5], L);                                                     \
-            wm = __ballot((tm[0] + tm[1]) + tm[2] <= kth);                                                     \
-            if (wm == 0) continue;                                                                             \
-        }                                                                                                      \
-        have = false;                                                                                          \
-        const nbkd_node nd = cnodes[node];                                                                     \
-        if constexpr (STATS) ++n_nodes;                                                                        \
-        const int dim = nd.dimension;                                                                          \
-        if (dim < 0) {                                                                                         \
-            LEAF = node;                                                                                       \
-            LPOS = nd.left;                                                                                    \
-            LEND = nd.right;                                                                                   \
-            FOUND = true;                                                                                      \
-            break;                                                                                             \
-        }                                                                                                      \
-        const float split = nd.split;                                                                          \
-        const float qd = dim == 0 ? qx : (dim == 1 ? qy : qz);                                                 \
-        const float lo = dim == 0 ? bx[0] : (dim == 1 ? bx[2] : bx[4]);                                        \
-        const float hi = dim == 0 ? bx[1] : (dim == 1 ? bx[3] : bx[5]);                                        \
-        const float tl = box_lb_axis<PER>(qd, lo, split, L);                                                   \
-        const float tr = box_lb_axis<PER>(qd, split, hi, L);                                                   \
-        const float dl = ((dim == 0 ? tl : tm[0]) + (dim == 1 ? tl : tm[1])) + (dim == 2 ? tl : tm[2]);        \
-        const float dr = ((dim == 0 ? tr : tm[0]) + (dim == 1 ? tr : tm[1])) + (dim == 2 ? tr : tm[2]);        \
-        const uint64_t wl = __ballot(dl <= kth), wr = __ballot(dr <= kth);                                     \
-        const uint32_t right_votes = (uint32_t)__popcll(wm & __ballot(qd > split));                            \
-        const bool right_first = 2 * right_votes > (uint32_t)__popcll(wm);                                     \
-        const uint64_t wn = right_first ? wr : wl, wf = right_first ? wl : wr;                                 \
-        const int near_slot = right_first ? 2 * dim : 2 * dim + 1;                                             \
-        const int far_slot = right_first ? 2 * dim + 1 : 2 * dim;                                              \
-        const uint32_t sb = __float_as_uint(split);                                                            \
-        if (wn != 0 && wf != 0) {                                                                              \
-            const uint32_t far_node = right_first ? nd.left : nd.right;                                        \
-            const bool me = lane == sp;                                                                        \
-            sk_node = me ? far_node : sk_node;                                                                 \
-_Pragma("unroll")                                                                                              \
-            for (int a = 0; a < 6; ++a) {                                                                      \
-                const uint32_t fv =                                                                            \
-                    __builtin_amdgcn_readfirstlane(a == far_slot ? sb : __float_as_uint(bx[a]));               \
-                sk_b[a] = me ? __uint_as_float(fv) : sk_b[a];                                                  \
-            }                                                                                                  \
-            ++sp;                                                                                              \
-        }                                                                                                      \
-        if (wn == 0 && wf == 0) continue;                                                                      \
-        const bool go_near = wn != 0;                                                                          \
-        const int slot = go_near ? near_slot : far_slot;                                                       \
-        const bool go_right = go_near == right_first;                                                          \
-        node = go_right ? nd.right : nd.left;                                                                  \
-        const float tnew = go_right ? tr : tl;                                                                 \
-_Pragma("unroll")                                                                                              \
-        for (int a = 0; a < 3; ++a) tm[a] = dim == a ? tnew : tm[a];                                           \
-_Pragma("unroll")                                                                                              \
-        for (int a = 0; a < 6; ++a)                                                                            \
-            bx[a] = __uint_as_float(__builtin_amdgcn_readfirstlane(a == slot ? sb : __float_as_uint(bx[a])));  \
-        wm = go_near ? wn : wf;                                                                                \
-        have = true;                                                                                           \
-    }
-
-// first chunk of a leaf and its tight box (leafinfo words 0..5) into LDS
-// buffer B: 4 direct-to-LDS loads, no VGPR staging, no wait
-#define NBKD_COLLECT_STAGE(B, LEAF, LPOS, LEND)                                                    \
-    do {                                                                                           \
-        const uint32_t cn_ = min((uint32_t)CHUNK, (LEND) - (LPOS));                                \
-        glds_f32(t.x + (LPOS), W.pb[B][0], lane, cn_);                                             \
-        glds_f32(t.y + (LPOS), W.pb[B][1], lane, cn_);                                             \
-        glds_f32(t.z + (LPOS), W.pb[B][2], lane, cn_);                                             \
-        glds_f32(reinterpret_cast<const float *>(linfo) + 8 * (size_t)(LEAF), W.tb[B], lane, 6);   \
-    } while (0)
-
-template <bool PER, int DENSE_MIN, int OCC, int G, bool STATS, bool PIPE>
-__global__ void __launch_bounds__(TB, OCC)
-knn_collect_kernel(DevTree t, const uint32_t *__restrict__ linfo, const float *__restrict__ q,
-                   const uint32_t *__restrict__ order, uint32_t m, int kq,
-                   const float *__restrict__ tg, float seed_mul, uint32_t qpp,
-                   uint2 *__restrict__ cand, uint32_t capg, uint32_t *__restrict__ ccount,
-                   unsigned long long *__restrict__ stats) {
-    __shared__ CollectLds Wl[WPB];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    CollectLds &W = Wl[wave];
-    // packet pk holds queries pk*qpp .. pk*qpp + qpp-1 (lanes < qpp): qpp = 64
-    // for kd-ordered batches, 1 for the retry of scattered seed failures
-    const uint32_t pk = blockIdx.x * WPB + wave;
-    const uint32_t gq = pk * qpp + lane;
-    const bool valid = (uint32_t)lane < qpp && gq < m;
-    const uint32_t qo = valid ? order[gq] : 0u;
-    const float qx = valid ? q[3 * (size_t)qo] : 0.0f;
-    const float qy = valid ? q[3 * (size_t)qo + 1] : 0.0f;
-    const float qz = valid ? q[3 * (size_t)qo + 2] : 0.0f;
-    const float L = t.box;
-    const float seed = valid ? fminf(tg[qo] * seed_mul, FLT_MAX) : -INFINITY;
-    float kth = seed;
-    // bound histogram scales (d2_bucket): bucket edge unit and bucket factor
-    const bool fin = seed < FLT_MAX && seed >= 1e-30f;
-    const float s_over_nb = fin ? seed * (1.0f / NB) : (seed > 0.0f ? INFINITY : 0.0f);
-    const float nb_over_s = fin ? (float)NB / seed * 1.00000095367431640625f : 0.0f;
-#pragma unroll
-    for (int w = 0; w < NB / 4; ++w) W.hist[w][lane] = 0u;
-    uint2 *const col = cand + (size_t)pk * qpp * capg; // qpp rows x capg slots, blocked by 16
-    uint32_t cnt = 0, last_cnt = 0;
-
-    uint64_t n_nodes = 0, n_leaves = 0, n_scanned = 0, n_dense = 0, n_sparse = 0, n_evals = 0;
-    // Stack: entry i in lane i of these VGPRs (node id + its box).  The
-    // current node's box stays wave-uniform (SGPRs); each lane keeps its three
-    // per-axis lower-bound terms of that box (tm), so a child's test only
-    // recomputes the split axis.  Children are tested when their parent is
-    // expanded: a far child no lane wants is never pushed (bounds only shrink).
-    uint32_t sk_node = 0;
-    float sk_b[6] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
-    int sp = 0;
-    const cnode_ptr cnodes = (cnode_ptr)t.nodes;
-    uint32_t node = 0;
-    float bx[6];
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-        bx[2 * a] = PER ? 0.0f : -FLT_MAX;
-        bx[2 * a + 1] = PER ? L : FLT_MAX;
-    }
-    float tm[3] = {box_lb_axis<PER>(qx, bx[0], bx[1], L), box_lb_axis<PER>(qy, bx[2], bx[3], L),
-                   box_lb_axis<PER>(qz, bx[4], bx[5], L)};
-    uint64_t wm = __ballot((tm[0] + tm[1]) + tm[2] <= kth);
-    bool have = wm != 0;
-
-    // Leaf pipeline (PIPE): leaf B's loads are in flight while leaf A is
-    // scanned.  The walk to B runs on the pre-A bound (less pruning at worst);
-    // the need test at B's scan uses the current bound.
-    uint32_t la = 0, pa = 0, ea = 0, lb = 0, pbb = 0, eb = 0;
-    bool ha = false, hb = false;
-    int b = 0;
-    // phase clocks of the work-counter instance (STATS): shader cycles per wave
-    // in the walk, the staging wait, the leaf test, dense and sparse scanning
-    // and the bound update
-    uint64_t ph[6] = {0, 0, 0, 0, 0, 0};
-    uint64_t tclk = STATS ? clock64() : 0;
-#define NBKD_PH(I)                                                                                 \
-    do {                                                                                           \
-        if constexpr (STATS) {                                                                     \
-            const uint64_t t_ = clock64();                                                         \
-            ph[I] += t_ - tclk;                                                                    \
-            tclk = t_;                                                                             \
-        }                                                                                          \
-    } while (0)
-    NBKD_COLLECT_WALK(ha, la, pa, ea);
-    if (ha) NBKD_COLLECT_STAGE(0, la, pa, ea);
-    NBKD_PH(0);
-    while (ha) {
-        if constexpr (PIPE) {
-            NBKD_COLLECT_WALK(hb, lb, pbb, eb);
-            if (hb) {
-                NBKD_COLLECT_STAGE(b ^ 1, lb, pbb, eb);
-                __builtin_amdgcn_s_waitcnt(0x0F74); // vmcnt(4): all but B's 4 loads
-            } else {
-                wait_vm0();
-            }
-        } else {
-            wait_vm0();
-        }
-        wave_sync();
-        NBKD_PH(1);
-        {
-            const uint32_t lpos = pa, lend = ea;
-            // first chunk + tight box already staged in buffer b (stage())
-            float (*const pb)[CHUNK] = W.pb[b];
-            uint32_t cn = min((uint32_t)CHUNK, lend - lpos);
-            const float tb[6] = {W.tb[b][0], W.tb[b][3], W.tb[b][1], W.tb[b][4], W.tb[b][2], W.tb[b][5]};
-            const uint64_t need = __ballot(box_lb2<PER>(qx, qy, qz, tb, L) <= kth);
-            NBKD_PH(2);
-            if (need != 0) {
-            const uint32_t nneed = (uint32_t)__popcll(need);
-            if constexpr (STATS) ++n_leaves;
-            for (uint32_t c0 = lpos;;) {
-                if constexpr (STATS) n_scanned += cn;
-                if (nneed >= (uint32_t)DENSE_MIN) {
-                    // every lane scans the chunk for its own query
-                    if constexpr (STATS) {
-                        n_dense += cn;
-                        n_evals += (uint64_t)cn * 64;
-                    }
-                    for (uint32_t u0 = 0; u0 < cn; u0 += G) {
-                        // d2 of G points for every lane, then the hits compacted:
-                        // the append runs max-hits-per-lane times, not once per point
-                        float dg[G];
-    #pragma unroll
-                        for (int u = 0; u < G; u += 4) {
-                            const float4 xv = *reinterpret_cast<const float4 *>(&pb[0][u0 + u]);
-                            const float4 yv = *reinterpret_cast<const float4 *>(&pb[1][u0 + u]);
-                            const float4 zv = *reinterpret_cast<const float4 *>(&pb[2][u0 + u]);
-                            dg[u] = point_d2_fast<PER>(qx, qy, qz, xv.x, yv.x, zv.x, L);
-                            dg[u + 1] = point_d2_fast<PER>(qx, qy, qz, xv.y, yv.y, zv.y, L);
-                            dg[u + 2] = point_d2_fast<PER>(qx, qy, qz, xv.z, yv.z, zv.z, L);
-                            dg[u + 3] = point_d2_fast<PER>(qx, qy, qz, xv.w, yv.w, zv.w, L);
-                        }
-                        uint32_t hm = 0;
-    #pragma unroll
-                        for (int u = 0; u < G; ++u) hm |= (dg[u] < kth ? 1u : 0u) << u;
-                        while (__any(hm != 0)) {
-                            if (hm != 0) {
-                                const uint32_t u = (uint32_t)__builtin_ctz(hm);
-                                hm &= hm - 1u;
-                                float d = dg[0];
-    #pragma unroll
-                                for (int v = 1; v < G; ++v) d = u == (uint32_t)v ? dg[v] : d;
-                                const uint32_t j = d2_bucket(d, nb_over_s);
-                                atomicAdd(&W.hist[j >> 2][lane], 1u << (8 * (j & 3)));
-                                if (cnt < capg)
-                                    col[((cnt >> 4) * qpp + lane) * 16u + (cnt & 15u)] =
-                                        make_uint2(__float_as_uint(d), c0 + u0 + u);
-                                ++cnt;
-                            }
-                        }
-                    }
-                    NBKD_PH(3);
-                } else {
-                    // (needing query, point) pairs compacted onto the 64 lanes:
-                    // slot = pair & (c2-1), point = pair >> log2(c2), c2 = pow2 >= nneed
-                    W.cnt[lane] = cnt;
-                    if ((need >> lane) & 1ull) {
-                        const uint32_t r = mbcnt64(need);
-                        W.owners[r] = (uint8_t)lane;
-                        W.sq[r] = make_float4(qx, qy, qz, kth);
-                        W.scl[r] = nb_over_s;
-                    }
-                    wave_sync();
-                    uint32_t c2 = 1;
-                    while (c2 < nneed) c2 <<= 1;
-                    const uint32_t lgc = (uint32_t)__builtin_ctz(c2);
-                    const uint32_t pairs = cn << lgc;
-                    if constexpr (STATS) n_evals += (uint64_t)cn * nneed;
-                    for (uint32_t p0 = 0; p0 < pairs; p0 += 64) {
-                        if constexpr (STATS) ++n_sparse;
-                        const uint32_t pi = p0 + lane;
-                        const uint32_t slot = pi & (c2 - 1u), pr = pi >> lgc;
-                        if (slot < nneed && pi < pairs) {
-                            const float4 qq = W.sq[slot];
-                            const float d = point_d2_fast<PER>(qq.x, qq.y, qq.z, pb[0][pr],
-                                                               pb[1][pr], pb[2][pr], L);
-                            if (d < qq.w) {
-                                const uint32_t owner = W.owners[slot];
-                                const uint32_t j = d2_bucket(d, W.scl[slot]);
-                                atomicAdd(&W.hist[j >> 2][owner], 1u << (8 * (j & 3)));
-                                const uint32_t sl = atomicAdd(&W.cnt[owner], 1u);
-                                if (sl < capg)
-                                    col[((sl >> 4) * qpp + owner) * 16u + (sl & 15u)] =
-                                        make_uint2(__float_as_uint(d), c0 + pr);
-                            }
-                        }
-                    }
-                    wave_sync();
-                    cnt = W.cnt[lane];
-                    NBKD_PH(4);
-                }
-                c0 += cn;
-                if (c0 >= lend) {
-                    // tighten: smallest bucket edge with >= k candidates below it
-                    // (the last bucket's edge is the seed itself: nothing to gain).
-                    // Only lanes holding >= k candidates, some of them new, can move.
-                    const bool upd = cnt >= (uint32_t)kq && cnt != last_cnt;
-                    if (__any(upd)) {
-                        wave_sync();
-                        if (upd) {
-                            last_cnt = cnt;
-                            // per word, h * 0x01010101 holds the prefix sums of its 4
-                            // byte counts (each < 256 while cnt <= capg; a lane past
-                            // capg is re-run anyway)
-                            const uint32_t p0 = W.hist[0][lane] * 0x01010101u;
-                            const uint32_t p1 = W.hist[1][lane] * 0x01010101u;
-                            const uint32_t p2 = W.hist[2][lane] * 0x01010101u;
-                            const uint32_t p3 = W.hist[3][lane] * 0x01010101u;
-                            const uint32_t c0w = p0 >> 24, c1w = c0w + (p1 >> 24), c2w = c1w + (p2 >> 24);
-                            const uint32_t kk = (uint32_t)kq;
-                            const uint32_t w = c0w >= kk ? 0u : c1w >= kk ? 1u : c2w >= kk ? 2u : 3u;
-                            const uint32_t base = w == 0 ? 0u : w == 1 ? c0w : w == 2 ? c1w : c2w;
-                            const uint32_t pw = w == 0 ? p0 : w == 1 ? p1 : w == 2 ? p2 : p3;
-                            const uint32_t need_k = kk - base; // first byte b with prefix >= need_k
-                            const uint32_t nb = (((pw & 0xFFu) < need_k) ? 1u : 0u) +
-                                                ((((pw >> 8) & 0xFFu) < need_k) ? 1u : 0u) +
-                                                ((((pw >> 16) & 0xFFu) < need_k) ? 1u : 0u) +
-                                                (((pw >> 24) < need_k) ? 1u : 0u);
-                            const uint32_t jstar = 4 * w + nb; // NB when fewer than k are counted
-                            if (jstar < (uint32_t)(NB - 1))
-                                kth = fminf(kth, (float)(jstar + 1) * s_over_nb);
-                        }
-                    }
-                    NBKD_PH(5);
-                    break;
-                }
-                cn = min((uint32_t)CHUNK, lend - c0);
-                wave_sync();
-                glds_f32(t.x + c0, pb[0], lane, cn);
-                glds_f32(t.y + c0, pb[1], lane, cn);
-                glds_f32(t.z + c0, pb[2], lane, cn);
-                wait_vm0();
-                wave_sync();
-            }
-            }
-        }
-        wave_sync();
-        if constexpr (PIPE) {
-            la = lb;
-            pa = pbb;
-            ea = eb;
-            ha = hb;
-            b ^= 1;
-        } else {
-            NBKD_COLLECT_WALK(ha, la, pa, ea);
-            if (ha) NBKD_COLLECT_STAGE(0, la, pa, ea);
-        }
-        NBKD_PH(0);
-    }
-#undef NBKD_PH
-    if (valid) ccount[gq] = cnt;
-    if (STATS && lane == 0) {
-        atomicAdd(&stats[0], (unsigned long long)n_nodes); // node visits of the packet walk
-        atomicAdd(&stats[1], (unsigned long long)n_evals);
-        atomicAdd(&stats[2], (unsigned long long)n_dense);
-        atomicAdd(&stats[3], (unsigned long long)n_sparse);
-        atomicAdd(&stats[4], (unsigned long long)n_scanned);
-        atomicAdd(&stats[5], 1ull);
-        atomicAdd(&stats[7], (unsigned long long)n_leaves);
-#pragma unroll
-        for (int i = 0; i < 6; ++i) atomicAdd(&stats[10 + i], (unsigned long long)ph[i]);
-    }
-    if (STATS) {
-        uint32_t c = valid ? cnt : 0u;
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
-        if (lane == 0) atomicAdd(&stats[6], (unsigned long long)c);
-    }
-}
-
-#endif // NBKD_EXPERIMENTS
 
 // ---------------------------------------------------------------- group variant
 // The same packet walk over a tree whose leaves are cut into 8-point groups
@@ -1220,21 +859,6 @@ knn_select_wave_kernel(DevTree t, const float *__restrict__ q, const uint32_t *_
     }
 }
 
-#ifdef NBKD_EXPERIMENTS
-int dense_min() {
-    const char *e = knob("NBKD_DENSE_MIN"); // tuning experiments only
-    return e ? atoi(e) : 33;
-}
-
-#endif
-
-bool groups_enabled() {
-    static const bool on = [] { // NBKD_GROUPS=0: leaf-level scan (A/B)
-        const char *e = knob("NBKD_GROUPS");
-        return !(e && atoi(e) == 0);
-    }();
-    return on;
-}
 
 // a device-counted pass's fixed grid: 8 blocks of 4 waves per CU
 unsigned resident_blocks() {
@@ -1264,7 +888,7 @@ void launch_collect(const Tree &t, const float *q, const uint32_t *order, QSpan 
     // count below the k-th's bucket is < 256, i.e. for k <= 255 (a wrapped or
     // carried byte can only make a larger cumulative count); above, no tightening
     if (k > 255) k = 0x7FFFFFFF;
-    if (t.ginfo && groups_enabled()) {
+    {
         // NBKD_XCD_MAP=0: hardware block order (A/B of the XCD-contiguous packet ranges)
         static const bool xcd = [] {
             const char *e = knob("NBKD_XCD_MAP");
@@ -1285,48 +909,6 @@ void launch_collect(const Tree &t, const float *q, const uint32_t *order, QSpan 
                 capg, ccount, nullptr, xcd && !span.count, kbound);
         return;
     }
-#ifdef NBKD_EXPERIMENTS
-    TimedScope ts(name, s);
-    const int dm = dense_min();
-    const char *eo = knob("NBKD_COLLECT_OCC"); // tuning experiments only
-    const int occ = eo ? atoi(eo) : 8;
-#define NBKD_COLLECT(DM, OC, G, P)                                                                 \
-    do {                                                                                           \
-        if (stats)                                                                                 \
-            knn_collect_kernel<PER, DM, OC, G, true, P><<<blocks, TB, 0, s>>>(                     \
-                view(t), t.leafinfo, q, order, m, k, tg, seed_mul, qpp, cand, capg, ccount, stats); \
-        else                                                                                       \
-            knn_collect_kernel<PER, DM, OC, G, false, P><<<blocks, TB, 0, s>>>(                    \
-                view(t), t.leafinfo, q, order, m, k, tg, seed_mul, qpp, cand, capg, ccount,        \
-                nullptr);                                                                          \
-    } while (0)
-    // NBKD_COLLECT_PIPE=1: prefetch the next leaf while scanning one.  Off by
-    // default: measured 74.5 vs 72.6 ms at 1e8 (8 waves per SIMD already hide
-    // the staging latency; the kernel is VALU-issue bound)
-    static const bool pipe = [] {
-        const char *e = knob("NBKD_COLLECT_PIPE");
-        return e && atoi(e) != 0;
-    }();
-    if (occ <= 6) {
-        NBKD_COLLECT(17, 6, 8, true);
-    } else if (occ == 7) {
-        NBKD_COLLECT(17, 7, 4, true);
-    } else if (dm <= 17) {
-        NBKD_COLLECT(17, 8, 4, true);
-    } else if (dm <= 33) {
-        if (pipe)
-            NBKD_COLLECT(33, 8, 4, true);
-        else
-            NBKD_COLLECT(33, 8, 4, false);
-    } else if (dm <= 49) {
-        NBKD_COLLECT(49, 8, 4, true);
-    } else {
-        NBKD_COLLECT(65, 8, 4, true);
-    }
-#undef NBKD_COLLECT
-#else
-    (void)stats;
-#endif
 }
 
 template <int R>

@@ -1,5 +1,5 @@
-// Device helpers shared by the packet kNN kernels (knn_packet.hip,
-// knn_collect.hip): direct-to-LDS loads, wave-local sync, the scalar-cache
+// Device helpers shared by the packet kernels (knn_collect.hip, ball.hip):
+// direct-to-LDS loads, wave-local sync, the scalar-cache
 // view of the node table, LDS-staged row stores and the fallback listing.
 #pragma once
 

@@ -1107,18 +1107,10 @@ nbkd_status knn_locked(const Tree &t, Workspace &ws, const float *q, uint64_t m,
                 NBKD_HIP(hipGetLastError());
             }
         } else {
-#ifdef NBKD_EXPERIMENTS
-            if (k > 64) {
-                set_error("experiments build: the no-seed packet kernel serves k <= 64 only");
-                return NBKD_EINVAL;
-            }
-            TimedScope ts("knn", s);
-            launch_knn_packet(t, dq, ord, mm, k, tg, dd, di, list, count, stats, s);
-            NBKD_HIP(hipGetLastError());
-#else
-            set_error("internal: the kNN query has no seed bound (experiments-only path)");
-            return NBKD_EDEVICE;
-#endif
+            // a seed margin <= 0 exists only in experiments builds (NBKD_KNN_SEED);
+            // the round-1 no-seed packet kernel it selected is retired
+            set_error("internal: the kNN query has no seed bound (knn_seed_margin <= 0)");
+            return NBKD_EINVAL;
         }
         if (list) {
             TimedScope ts("knn_fallback", s);
