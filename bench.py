@@ -244,6 +244,21 @@ def suite(args, capi, hip, tree, dev_pts, n, k, L, stream, od, oi):
     out["knn_independent_queries"] = {"queries_per_s": n / sec, "ms": sec * 1e3, "k": k,
                                       "queries": n, "query_seed": synth.SEED_QUERIES}
     log(f"suite: independent queries {n / sec:.3e} q/s")
+    # the drop-in surface with host buffers (PCIe-inclusive, never `value`): the
+    # same self-queries from a host (n, 3) array into host (n, k) arrays, as
+    # KDTree.query returns them; batches of host_batch queries stream through
+    # two device slots (query.hip host_pipeline)
+    ph = dev_pts.numpy_head(n)
+    tree.query(ph[:100_000], k)
+    t0 = time.perf_counter()
+    hd, hi_ = tree.query(ph, k)
+    sec = time.perf_counter() - t0
+    ok = bool(np.array_equal(hd[:, 0], np.zeros(n, np.float32)))
+    out["knn_host_to_host"] = {"queries_per_s": n / sec, "ms": sec * 1e3, "k": k, "queries": n,
+                               "output_bytes": int(hd.nbytes + hi_.nbytes),
+                               "self_distance_zero": ok}
+    del hd, hi_, ph
+    log(f"suite: host-to-host kNN {n / sec:.3e} q/s")
     # the same self-queries over a leafsize-128 tree (the reference wrapper's
     # default, kdtree/src/python/nbodyhpc/kdtree/__init__.py:17): 65..128-point
     # leaves are staged as two halves with their own tight boxes
@@ -792,10 +807,19 @@ def main():
                                                    stream=stream.handle)
     sr_acc = {"rows_forwarded": 0, "forwards": 0, "hops": 0, "calls": 0}
 
+    counters = {"timing": False, "stats": False}
+
     def step():
         tree.query_device(dev_pts.ptr, own, k, od.ptr, oi.ptr, stream.handle)
         if rows is not None:
+            # the second round's small host-in kNN calls stay out of the kernel
+            # timers and work counters (they describe the slab-local pass); its
+            # time is in the step's wall clock
+            capi.timing_enable(False)
+            capi.stats_enable(False)
             st = slab.second_round(rows, rank, world, ds.bounds, L, ds.h, k, dist)
+            capi.timing_enable(counters["timing"])
+            capi.stats_enable(counters["stats"])
             for kk in ("rows_forwarded", "forwards"):
                 sr_acc[kk] += st[kk]
             sr_acc["hops"] = max(sr_acc["hops"], st["hops"])
@@ -816,6 +840,7 @@ def main():
         for kk in sr_acc:
             sr_acc[kk] = 0
     capi.timing_enable(True)
+    counters["timing"] = True
     capi.timing_reset()
     barrier()
     hip.synchronize()
@@ -836,16 +861,19 @@ def main():
     col_ms, col_launches = capi.timing_read("knn_collect")
     sel_ms, _ = capi.timing_read("knn_select")
     capi.timing_enable(False)
+    counters["timing"] = False
     elapsed_max = allmax(elapsed)
     own_total = int(allsum(float(own)))  # file inputs: slabs differ in size
 
     # work counters of our own traversal (one extra, untimed pass)
     capi.stats_enable(True)
+    counters["stats"] = True
     step()
     stream.synchronize()
     st = capi.stats_read_all()
     pts_scanned = st["pair_evals"]
     capi.stats_enable(False)
+    counters["stats"] = False
 
     gpu_d = gpu_i = None
     parity_rows = min(args.cpu_sample, own)

@@ -127,3 +127,20 @@ def test_row_and_forward_arguments_rejected():
     assert L.nbkd_rows_scatter(None, 8, None, 3, None, 0, None) == capi.NBKD_EINVAL
     # zero rows: nothing to do, no device touched
     assert L.nbkd_rows_gather(None, 8, None, 0, None, 0, None) == capi.NBKD_OK
+
+
+def test_type_stub_names_the_reference_surface():
+    """_impl.pyi ships beside the extension (and beside the nbodyhpc.kdtree
+    re-export) and declares every member of the reference's stub
+    (kdtree/src/python/nbodyhpc/kdtree/_impl.pyi:1-18)."""
+    import ast
+    import os
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for rel in ("nbodyhpc_amd/kdtree/_impl.pyi", "nbodyhpc/kdtree/_impl.pyi"):
+        tree = ast.parse(open(os.path.join(root, rel)).read())
+        cls = [n for n in tree.body if isinstance(n, ast.ClassDef) and n.name == "KDTree"][0]
+        names = {f.name for f in cls.body if isinstance(f, ast.FunctionDef)}
+        assert {"__init__", "query", "n", "size", "periodic", "boxsize"} <= names
+        init = [f for f in cls.body if isinstance(f, ast.FunctionDef) and f.name == "__init__"][0]
+        assert [a.arg for a in init.args.args][:5] == ["self", "points", "leafsize", "max_threads",
+                                                       "boxsize"]

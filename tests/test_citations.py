@@ -1,0 +1,63 @@
+"""Every `file:line` citation of a reference source in this repo resolves:
+the cited lines exist in that file under /root/reference (VERDICT r03 found
+kdtree_impl.hpp citations past the end of the 275-line file).  Reads the
+reference as text only; skipped where it is absent (the GPU box)."""
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REF = "/root/reference"
+SCAN = ["oracle", "nbodyhpc_amd", "include", "tests", "nbodyhpc", "DESIGN.md", "INTEGRATION.md",
+        "bench.py", "README.md", "BASELINE.md", "__graft_entry__.py"]
+EXT = (".py", ".c", ".cpp", ".h", ".hpp", ".hip", ".md", ".pyi")
+CITE = re.compile(r"([A-Za-z0-9_./-]+\.(?:cpp|hpp|h|py|asm|pyi|txt|vert|frag)):(\d+)(?:-(\d+))?")
+
+
+def _ref_files():
+    by_name, by_path = {}, {}
+    for d, _, fs in os.walk(REF):
+        if "/.git" in d:
+            continue
+        for f in fs:
+            p = os.path.join(d, f)
+            rel = os.path.relpath(p, REF)
+            by_path[rel] = p
+            by_name.setdefault(f, []).append(p)
+    return by_name, by_path
+
+
+def _lines(path, cache={}):
+    if path not in cache:
+        with open(path, "rb") as f:
+            cache[path] = f.read().count(b"\n") + 1
+    return cache[path]
+
+
+@pytest.mark.skipif(not os.path.isdir(os.path.join(REF, "kdtree")), reason="reference absent")
+def test_reference_citations_resolve():
+    by_name, by_path = _ref_files()
+    bad, checked = [], 0
+    for top in SCAN:
+        p0 = os.path.join(ROOT, top)
+        files = [p0] if os.path.isfile(p0) else [
+            os.path.join(d, f) for d, _, fs in os.walk(p0) for f in fs if f.endswith(EXT)]
+        for fp in files:
+            if "/golden/" in fp or "__pycache__" in fp:
+                continue
+            txt = open(fp, encoding="utf-8", errors="replace").read()
+            for m in CITE.finditer(txt):
+                name, a, b = m.group(1), int(m.group(2)), int(m.group(3) or m.group(2))
+                cands = [by_path[name]] if name in by_path else [
+                    p for p in by_name.get(os.path.basename(name), []) if p.endswith(name)]
+                if not cands:
+                    continue  # not a reference file
+                checked += 1
+                # an ambiguous bare name (pybind.cpp in kdtree/ and rasterization/)
+                # must fit at least one of the files it may name
+                ns = [_lines(c) for c in cands]
+                if not any(1 <= a <= b <= n for n in ns):
+                    bad.append(f"{os.path.relpath(fp, ROOT)}: {m.group(0)} (files have {ns} lines)")
+    assert checked > 100
+    assert not bad, "\n".join(bad[:40])
