@@ -111,7 +111,7 @@ struct CollectLdsG {
 // st: node visits, leaves scanned, points staged, leaves reached, sparse
 // iterations, pair evaluations, then 6 phase clocks, then lanes needing a
 // staged chunk summed over chunks (STATS only)
-template <bool PER, bool M, bool STATS>
+template <bool PER, bool M, bool STATS, bool AHEAD>
 __device__ __forceinline__ void grp_packet(const DevTree &t, const float *__restrict__ ginfo,
                                            const uint32_t *__restrict__ linfo,
                                            const float *__restrict__ hinfo,
@@ -149,9 +149,30 @@ __device__ __forceinline__ void grp_packet(const DevTree &t, const float *__rest
         }                                                                                          \
     } while (0)
     uint32_t pa = 0, ea = 0;
+    // AHEAD: while a leaf's staging loads are in flight the walk goes on to the
+    // next leaf (its node loads are scalar, lgkmcnt, so the staging's vmcnt wait
+    // does not wait for them); the walk ahead prunes with the bounds from before
+    // this leaf's scan, which are looser, so it may reach a leaf the tightened
+    // bounds would skip: no lane then needs it (the per-leaf test below uses the
+    // current bounds), never a wrong result
+    bool ha_next = false;
+    uint32_t pa_next = 0, ea_next = 0, node_next = 0;
+    if constexpr (AHEAD) {
+        NBKD_GWALK(ha_next, pa_next, ea_next);
+        node_next = node;
+    }
     for (;;) {
         bool ha;
-        NBKD_GWALK(ha, pa, ea);
+        uint32_t lnode;
+        if constexpr (AHEAD) {
+            ha = ha_next;
+            pa = pa_next;
+            ea = ea_next;
+            lnode = node_next;
+        } else {
+            NBKD_GWALK(ha, pa, ea);
+            lnode = node;
+        }
         if (!ha) break;
         if constexpr (STATS) ++st[3]; // leaves reached (staged), needed by some lane or not
         // chunks: a leaf of 65..128 points is staged as its two halves, each
@@ -161,12 +182,17 @@ __device__ __forceinline__ void grp_packet(const DevTree &t, const float *__rest
         const uint32_t lc = lend - pa;
         const bool halves = hinfo != nullptr && lc > (uint32_t)GCHUNK && lc <= 2u * GCHUNK;
         const uint32_t hm = (lc / 2) / 8 * 8;
-        const float *const lbox = halves ? hinfo + 12 * (size_t)node
-                                         : reinterpret_cast<const float *>(linfo) + 8 * (size_t)node;
+        const float *const lbox = halves ? hinfo + 12 * (size_t)lnode
+                                         : reinterpret_cast<const float *>(linfo) + 8 * (size_t)lnode;
         uint32_t c0 = pa;
         uint32_t cn = halves ? hm : min((uint32_t)GCHUNK, lc);
         NBKD_COLLECT_STAGE_G(pa, cn, lbox);
         NBKD_PH(0);
+        if constexpr (AHEAD) {
+            NBKD_GWALK(ha_next, pa_next, ea_next);
+            node_next = node;
+            NBKD_PH(0);
+        }
         wait_vm0();
         wave_sync();
         NBKD_PH(1);
@@ -296,7 +322,7 @@ __device__ __forceinline__ void grp_packet(const DevTree &t, const float *__rest
 }
 
 // one packet of the collect pass
-template <bool PER, bool STATS>
+template <bool PER, bool STATS, bool AHEAD>
 __device__ __forceinline__ void collect_packet(
     const DevTree &t, const float *__restrict__ ginfo, const uint32_t *__restrict__ linfo,
     const float *__restrict__ hinfo, const float *__restrict__ q, const uint32_t *__restrict__ order,
@@ -320,7 +346,7 @@ __device__ __forceinline__ void collect_packet(
     uint32_t cnt = 0;
     uint64_t st[13] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     float kth = seed;
-    grp_packet<PER, PER, STATS>(t, ginfo, linfo, hinfo, W, lane, qx, qy, qz, kth, s_over_nb,
+    grp_packet<PER, PER, STATS, AHEAD>(t, ginfo, linfo, hinfo, W, lane, qx, qy, qz, kth, s_over_nb,
                                 nb_over_s, col, qpp, capg, kq, cnt, st);
     if (valid) ccount[gq] = cnt;
     // the final bound: at least k candidates lie strictly below it (bound
@@ -349,7 +375,7 @@ __device__ __forceinline__ void collect_packet(
 // A static pass launches one wave per packet; a device-counted pass (the
 // retry rounds: LOOP) a fixed grid that strides over its packets.  Only the
 // LOOP instance carries the loop (in the first pass it cost a 12-28 B spill).
-template <bool PER, int OCC, bool STATS, bool LOOP>
+template <bool PER, int OCC, bool STATS, bool LOOP, bool AHEAD>
 __global__ void __launch_bounds__(TB, OCC)
 knn_collect_grp_kernel(DevTree t, const float *__restrict__ ginfo,
                        const uint32_t *__restrict__ linfo, const float *__restrict__ hinfo,
@@ -368,13 +394,13 @@ knn_collect_grp_kernel(DevTree t, const float *__restrict__ ginfo,
     if constexpr (LOOP) {
         for (uint32_t pk = bid * WPB + wave; pk < npk; pk += gridDim.x * WPB) {
             wave_sync(); // the previous packet's LDS reads are done
-            collect_packet<PER, STATS>(t, ginfo, linfo, hinfo, q, order, m, kq, tg, seed_mul, qpp,
+            collect_packet<PER, STATS, AHEAD>(t, ginfo, linfo, hinfo, q, order, m, kq, tg, seed_mul, qpp,
                                        cand, capg, ccount, stats, kbound, W, lane, pk);
         }
     } else {
         const uint32_t pk = bid * WPB + wave;
         if (pk < npk)
-            collect_packet<PER, STATS>(t, ginfo, linfo, hinfo, q, order, m, kq, tg, seed_mul, qpp,
+            collect_packet<PER, STATS, AHEAD>(t, ginfo, linfo, hinfo, q, order, m, kq, tg, seed_mul, qpp,
                                        cand, capg, ccount, stats, kbound, W, lane, pk);
     }
 }
@@ -860,6 +886,16 @@ knn_select_wave_kernel(DevTree t, const float *__restrict__ q, const uint32_t *_
 }
 
 
+// walk ahead to the next leaf while a leaf's staging is in flight (grp_packet
+// AHEAD); NBKD_COLLECT_AHEAD in an experiments build
+bool collect_ahead() {
+    static const bool on = [] {
+        const char *e = knob("NBKD_COLLECT_AHEAD");
+        return e && atoi(e) != 0;
+    }();
+    return on;
+}
+
 // a device-counted pass's fixed grid: 8 blocks of 4 waves per CU
 unsigned resident_blocks() {
     static const unsigned b = [] {
@@ -895,18 +931,22 @@ void launch_collect(const Tree &t, const float *q, const uint32_t *order, QSpan 
             return !(e && atoi(e) == 0);
         }();
         TimedScope ts(name, s);
+#define NBKD_GRP(STATS, LOOP, AHEAD, STP, XCD)                                                     \
+    knn_collect_grp_kernel<PER, 8, STATS, LOOP, AHEAD><<<blocks, TB, 0, s>>>(                      \
+        view(t), t.ginfo, t.leafinfo, t.hinfo, q, order, span, k, tg, seed_mul, qpp, cand, capg,   \
+        ccount, STP, XCD, kbound)
         if (span.count)
-            knn_collect_grp_kernel<PER, 8, false, true><<<blocks, TB, 0, s>>>(
-                view(t), t.ginfo, t.leafinfo, t.hinfo, q, order, span, k, tg, seed_mul, qpp, cand,
-                capg, ccount, nullptr, false, kbound);
-        else if (stats)
-            knn_collect_grp_kernel<PER, 8, true, false><<<blocks, TB, 0, s>>>(
-                view(t), t.ginfo, t.leafinfo, t.hinfo, q, order, span, k, tg, seed_mul, qpp, cand,
-                capg, ccount, stats, xcd && !span.count, kbound);
+            NBKD_GRP(false, true, false, nullptr, false);
+        else if (collect_ahead()) {
+            if (stats)
+                NBKD_GRP(true, false, true, stats, xcd);
+            else
+                NBKD_GRP(false, false, true, nullptr, xcd);
+        } else if (stats)
+            NBKD_GRP(true, false, false, stats, xcd);
         else
-            knn_collect_grp_kernel<PER, 8, false, false><<<blocks, TB, 0, s>>>(
-                view(t), t.ginfo, t.leafinfo, t.hinfo, q, order, span, k, tg, seed_mul, qpp, cand,
-                capg, ccount, nullptr, xcd && !span.count, kbound);
+            NBKD_GRP(false, false, false, nullptr, xcd);
+#undef NBKD_GRP
         return;
     }
 }
