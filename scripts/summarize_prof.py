@@ -9,9 +9,15 @@ writes
   profiles/<round>_pmc_knn.json       HBM bytes per knn launch from the FETCH_SIZE and
                                       WRITE_SIZE passes (separate runs), gfx950-corrected
   profiles/<round>_bench.json         the bench line of the same call
-FETCH_SIZE / WRITE_SIZE are rocprofv3 derived counters in KiB; on gfx950 FETCH_SIZE
-reports half the bytes of wide coalesced reads (MI355X_MICROARCH.md, HBM section),
-so fetched bytes = 2 * 1024 * FETCH_SIZE.  WRITE_SIZE is taken as reported.
+FETCH_SIZE / WRITE_SIZE are rocprofv3 derived counters in KiB, calibrated on this
+code's access shapes by scripts/calib/pmc_calib.hip (profiles/r04a_pmc_calibration.json):
+FETCH_SIZE reports exactly half the bytes of every read shape measured (16-B and
+4-B per lane loads, 4-B global_load_lds), so fetched bytes = 2 * 1024 * FETCH_SIZE;
+WRITE_SIZE reports full-line stores exactly at any width (16, 8 or 4 B per lane:
+the select kernel's row stores) and a partly written 128-B line as 32-B sectors
+(one 8-B or 4-B store alone in a line counts 32 B), i.e. the bytes the L2
+actually writes back, so it is taken as reported: the collect kernel's candidate
+columns show their sector write-amplification in it, not an undercount.
 """
 import csv
 import glob
@@ -100,8 +106,9 @@ def main():
             "fetch_bytes_per_launch_corrected": 2.0 * 1024.0 * f_kib,
             "write_bytes_per_launch": 1024.0 * w_kib,
             "hbm_bytes_per_launch": hbm,
-            "note": "FETCH_SIZE doubled (gfx950 wide-read correction); Infinity-Cache hits "
-                    "are counted by these counters, not excluded",
+            "note": "FETCH_SIZE doubled, WRITE_SIZE as reported (calibration: "
+                    "profiles/r04a_pmc_calibration.json); Infinity-Cache hits are counted "
+                    "by these counters, not excluded",
         }
         json.dump(out, open(os.path.join(prof, f"{tag}_pmc_knn.json"), "w"), indent=1)
         print(json.dumps(out, indent=1))
