@@ -534,3 +534,19 @@ def test_device_output_queries_are_asynchronous(gpu, oracle):
                 assert_knn_equal(d, i, dr, ir, pts, host_q[sel], 1.0)
     finally:
         gpu.set_tuning("knn_seed_margin", saved)
+
+
+@pytest.mark.parametrize("box,r", [(1.0, 0.35), (2.5, 0.6), (1.0, 0.499)])
+def test_ball_count_wide_radius_periodic_images(gpu, oracle, box, r):
+    """Radii comparable to L/2: many (query, leaf) pairs reach their points
+    through the periodic image, where the count kernel must keep the periodic
+    per-axis minimum; elsewhere it uses the plain d2 (same bits when every
+    point of the leaf lies within L/2 on each axis).  Counts equal brute force."""
+    rng = np.random.Generator(np.random.PCG64(31))
+    pts = (rng.uniform(0, 1, (30_000, 3)) * box).astype(np.float32)
+    pts = np.minimum(pts, np.float32(box))
+    q = np.concatenate([pts[:300], (rng.uniform(0, 1, (300, 3)) * box).astype(np.float32),
+                        np.array([[0, 0, 0], [box, box, box], [box / 2, 0, box]], np.float32)])
+    t = gpu.Tree(pts, leafsize=64, boxsize=box)
+    c = t.ball_count(q, r)
+    assert np.array_equal(c, oracle.ball_count_brute(pts, q, r, box))
