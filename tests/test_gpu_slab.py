@@ -379,3 +379,80 @@ def test_two_rank_slab_deposit_on_one_gpu(gpu, oracle, tmp_path):
     r = np.concatenate([b[2] for b in balls])
     ref = oracle.deposit(xyz, w, r, grid, float(grid[0]), (1.0, 1.0, 1.0), 4)
     np.testing.assert_allclose(got, ref, rtol=2e-5, atol=1e-6 * float(ref.max()))
+
+
+def _multihop_worker(rank, world, port, bounds, n, k, h, outdir):
+    from nbodyhpc_amd import hip
+
+    hip.preload()
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from nbodyhpc_amd import capi, synth
+        hip.set_device(0)
+        allp = synth.uniform(n, 91, 1.0)
+        mine = np.nonzero(slab.slab_of(allp[:, 0], bounds) == rank)[0]
+        xyz, ids = allp[mine], mine.astype(np.uint32)
+        own = len(xyz)
+        ds = slab.DeviceSlab(xyz, ids, rank, world, 1.0, 0, dist, comm=None, bounds=bounds)
+        ds.exchange(h)
+        t = capi.Tree(n=ds.n_local, dev_ptr=ds.xyz.ptr, leafsize=32, boxsize=1.0, device=0)
+        t.set_ids(dev_ptr=ds.ids.ptr)
+        od = hip.DeviceArray((own, k), np.float32)
+        oi = hip.DeviceArray((own, k), np.uint32)
+        t.query_device(ds.xyz.ptr, own, k, od.ptr, oi.ptr)
+        hip.synchronize()
+        st = slab.second_round(slab.DeviceRows(ds, t, k, od.ptr, oi.ptr), rank, world, bounds,
+                               1.0, ds.h, k, dist)
+        rk = hip.DeviceArray((own,), np.float32)
+        t.query_kth_device(ds.xyz.ptr, own, k, rk.ptr)
+        hip.synchronize()
+        slab.second_round(slab.DeviceRows(ds, t, k, kth_ptr=rk.ptr), rank, world, bounds, 1.0,
+                          ds.h, k, dist)
+        hip.synchronize()
+        np.savez(os.path.join(outdir, f"m{rank}.npz"), ids=ids, d=od.numpy(), i=oi.numpy(),
+                 rk=rk.numpy(), hops=st["hops"], fwd=st["rows_forwarded"])
+        t.close()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,bounds", [(3, [0.0, 0.45, 0.5, 1.0]),
+                                          (4, [0.0, 0.3, 0.33, 0.36, 1.0])])
+def test_multi_hop_second_round_on_one_gpu(gpu, oracle, tmp_path, world, bounds):
+    """hops >= 2 of the second round on the device path
+    (nbkd_slab_forward, rows gather / scatter, DeviceRows over gloo), W = 3
+    and 4 ranks sharing the one GPU.  Slabs 0.03-0.05 wide and a halo of
+    0.005 make rows near them reach two or three slabs away; every row and
+    k-th distance equals the single-tree oracle."""
+    import multiprocessing as mp
+
+    from nbodyhpc_amd import synth
+    from tests.parity import assert_knn_equal
+    n, k, h = 30_000, 16, 0.005
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    procs = [ctx.Process(target=_multihop_worker, args=(r, world, port, bounds, n, k, h,
+                                                        str(tmp_path)))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=300)
+    for p in procs:
+        if p.exitcode is None:
+            p.kill()
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    allp = synth.uniform(n, 91, 1.0)
+    gd, gi = oracle.tree(allp, 32, 1.0).query(allp, k, workers=16)
+    hops = 0
+    for r in range(world):
+        x = np.load(os.path.join(tmp_path, f"m{r}.npz"))
+        ids = x["ids"]
+        assert_knn_equal(x["d"], x["i"], gd[ids], gi[ids], allp, allp[ids], 1.0)
+        assert np.array_equal(x["rk"].view(np.uint32), gd[ids][:, -1].view(np.uint32))
+        hops = max(hops, int(x["hops"]))
+    assert hops >= 2
