@@ -889,11 +889,8 @@ knn_select_wave_kernel(DevTree t, const float *__restrict__ q, const uint32_t *_
 // walk ahead to the next leaf while a leaf's staging is in flight (grp_packet
 // AHEAD); NBKD_COLLECT_AHEAD in an experiments build
 bool collect_ahead() {
-    static const bool on = [] {
-        const char *e = knob("NBKD_COLLECT_AHEAD");
-        return e && atoi(e) != 0;
-    }();
-    return on;
+    const char *e = knob("NBKD_COLLECT_AHEAD"); // read per launch: A/B within one process
+    return e && atoi(e) != 0;
 }
 
 // a device-counted pass's fixed grid: 8 blocks of 4 waves per CU
