@@ -172,35 +172,49 @@ static inline void swap_pt(orc_pt *a, orc_pt *b) {
     *b = t;
 }
 
-/* Hoare-partition quickselect: afterwards p[m].k is the m-th order statistic,
- * p[0..m) <= p[m] <= p[m+1..n). */
-static void quickselect(orc_pt *p, int64_t n, int64_t m) {
-    int64_t lo = 0, hi = n - 1;
-    while (hi > lo) {
-        int64_t mid = lo + (hi - lo) / 2;
-        /* median of three into p[mid] */
-        if (p[mid].k < p[lo].k) swap_pt(&p[mid], &p[lo]);
-        if (p[hi].k < p[lo].k) swap_pt(&p[hi], &p[lo]);
-        if (p[hi].k < p[mid].k) swap_pt(&p[hi], &p[mid]);
-        float piv = p[mid].k;
-        int64_t i = lo, j = hi;
-        while (i <= j) {
-            while (p[i].k < piv) ++i;
-            while (piv < p[j].k) --j;
-            if (i <= j) {
-                swap_pt(&p[i], &p[j]);
-                ++i;
-                --j;
-            }
+/* Floyd-Rivest selection (the algorithm the reference's AVX2 selection follows,
+ * kdtree_selection.cpp:322-368: a sample window when the range exceeds 600,
+ * then a Hoare-style partition around the sampled pivot): afterwards p[m].k is
+ * the m-th order statistic of p[0..n) and p[0..m) <= p[m] <= p[m+1..n).  Only
+ * the order statistic (the split value) is pinned; which of several points
+ * tied at it land left is implementation-defined, here as in the reference. */
+static void fr_select(orc_pt *p, int64_t left, int64_t right, int64_t m) {
+    while (right > left) {
+        if (right - left > 600) {
+            const double n = (double)(right - left + 1);
+            const double i = (double)(m - left + 1);
+            const double z = log(n);
+            const double sz = 0.5 * exp(2.0 * z / 3.0);
+            const double sd = 0.5 * sqrt(z * sz * (n - sz) / n) * (i - n / 2 < 0 ? -1.0 : 1.0);
+            int64_t nl = (int64_t)floor((double)m - i * sz / n + sd);
+            int64_t nr = (int64_t)floor((double)m + (n - i) * sz / n + sd);
+            if (nl < left) nl = left;
+            if (nr > right) nr = right;
+            fr_select(p, nl, nr, m);
         }
-        if (m <= j)
-            hi = j;
-        else if (m >= i)
-            lo = i;
-        else
-            return;
+        const float t = p[m].k;
+        int64_t i = left, j = right;
+        swap_pt(&p[left], &p[m]);
+        if (p[right].k > t) swap_pt(&p[right], &p[left]);
+        while (i < j) {
+            swap_pt(&p[i], &p[j]);
+            ++i;
+            --j;
+            while (p[i].k < t) ++i;
+            while (p[j].k > t) --j;
+        }
+        if (p[left].k == t) {
+            swap_pt(&p[left], &p[j]);
+        } else {
+            ++j;
+            swap_pt(&p[j], &p[right]);
+        }
+        if (j <= m) left = j + 1;
+        if (m <= j) right = j - 1;
     }
 }
+
+static void quickselect(orc_pt *p, int64_t n, int64_t m) { fr_select(p, 0, n - 1, m); }
 
 static int push_node(orc_tree *t, orc_node nd) {
     if (t->nnodes == t->cap_nodes) {
