@@ -887,10 +887,13 @@ knn_select_wave_kernel(DevTree t, const float *__restrict__ q, const uint32_t *_
 
 
 // walk ahead to the next leaf while a leaf's staging is in flight (grp_packet
-// AHEAD); NBKD_COLLECT_AHEAD in an experiments build
+// AHEAD, on by default since round 4: collect 49.80 -> 48.28 ms per 1e8
+// queries, profiles/r04c_ab_collect_ahead.txt; every distance row identical
+// at 1e8, only the order inside exact ties changes, profiles/r04e_ahead_rows.json);
+// NBKD_COLLECT_AHEAD=0 in an experiments build restores the walk after the scan
 bool collect_ahead() {
     const char *e = knob("NBKD_COLLECT_AHEAD"); // read per launch: A/B within one process
-    return e && atoi(e) != 0;
+    return !(e && atoi(e) == 0);
 }
 
 // a device-counted pass's fixed grid: 8 blocks of 4 waves per CU
