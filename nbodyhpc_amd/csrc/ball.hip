@@ -73,7 +73,7 @@ __device__ __forceinline__ bool wrap_free(float qx, float qy, float qz, const fl
 // (r03g): spills that stay in L2 cost less than the lost occupancy
 constexpr int BALL_OCC[2][2] = {{8, 8}, {8, 8}};
 
-template <bool PER, bool FILL, bool AHEAD>
+template <bool PER, bool FILL>
 __global__ void __launch_bounds__(TB, BALL_OCC[PER][FILL])
 ball_packet_kernel(DevTree t, const uint32_t *__restrict__ linfo, const float *__restrict__ q,
                    const uint32_t *__restrict__ order, uint32_t m, float r2, PadLeaves pad,
@@ -119,41 +119,14 @@ ball_packet_kernel(DevTree t, const uint32_t *__restrict__ linfo, const float *_
     uint64_t st[1] = {0};
     (void)st;
 
-    // AHEAD (count mode): the leaf's tight box and first chunk are loaded
-    // before the need test (speculatively: a leaf no lane needs costs its
-    // staging bandwidth only) and the walk goes on to the next leaf while they
-    // are in flight, as knn_collect's grp_packet does
-    bool found_n = false;
-    uint32_t lpos_n = 0, lend_n = 0, node_n = 0;
-    if constexpr (AHEAD) {
-        NBKD_GWALK(found_n, lpos_n, lend_n);
-        node_n = node;
-    }
     for (;;) {
         bool found;
-        uint32_t lpos = 0, lend = 0, lnode;
-        if constexpr (AHEAD) {
-            found = found_n;
-            lpos = lpos_n;
-            lend = lend_n;
-            lnode = node_n;
-        } else {
-            NBKD_GWALK(found, lpos, lend);
-            lnode = node;
-        }
+        uint32_t lpos = 0, lend = 0;
+        NBKD_GWALK(found, lpos, lend);
         if (!found) break;
 
         // leaf: tight box first (lanes < 6), then the chunks
-        const uint32_t iw = lane < 6 ? linfo[8 * (size_t)lnode + lane] : 0u;
-        if constexpr (AHEAD) {
-            wave_sync(); // the previous leaf's LDS reads are done
-            const uint32_t cn0 = min((uint32_t)CHUNK, lend - lpos);
-            glds_f32(t.x + lpos, W.pb[0], lane, cn0);
-            glds_f32(t.y + lpos, W.pb[1], lane, cn0);
-            glds_f32(t.z + lpos, W.pb[2], lane, cn0);
-            NBKD_GWALK(found_n, lpos_n, lend_n);
-            node_n = node;
-        }
+        const uint32_t iw = lane < 6 ? linfo[8 * (size_t)node + lane] : 0u;
         const float tb[6] = {rdlane(__uint_as_float(iw), 0), rdlane(__uint_as_float(iw), 3),
                              rdlane(__uint_as_float(iw), 1), rdlane(__uint_as_float(iw), 4),
                              rdlane(__uint_as_float(iw), 2), rdlane(__uint_as_float(iw), 5)};
@@ -162,7 +135,7 @@ ball_packet_kernel(DevTree t, const uint32_t *__restrict__ linfo, const float *_
         // a leaf holding padding points (FLT_MAX, never inside) is always evaluated
         bool padded = false;
 #pragma unroll
-        for (int j = 0; j < NBKD_PAD_LEAVES; ++j) padded |= pad.id[j] == lnode;
+        for (int j = 0; j < NBKD_PAD_LEAVES; ++j) padded |= pad.id[j] == node;
         const bool full = need && !padded && box_ub2<PER>(qx, qy, qz, tb) <= thr;
         const bool part = need && !full;
         if constexpr (!FILL) {
@@ -171,15 +144,13 @@ ball_packet_kernel(DevTree t, const uint32_t *__restrict__ linfo, const float *_
         }
         for (uint32_t c0 = lpos; c0 < lend; c0 += CHUNK) {
             const uint32_t cn = min((uint32_t)CHUNK, lend - c0);
-            if (!AHEAD || c0 != lpos) { // AHEAD: the first chunk is staged already
-                wave_sync();
-                glds_f32(t.x + c0, W.pb[0], lane, cn);
-                glds_f32(t.y + c0, W.pb[1], lane, cn);
-                glds_f32(t.z + c0, W.pb[2], lane, cn);
-                if constexpr (FILL)
-                    glds_f32(reinterpret_cast<const float *>(t.idx) + c0,
-                             reinterpret_cast<float *>(W.pid), lane, cn);
-            }
+            wave_sync();
+            glds_f32(t.x + c0, W.pb[0], lane, cn);
+            glds_f32(t.y + c0, W.pb[1], lane, cn);
+            glds_f32(t.z + c0, W.pb[2], lane, cn);
+            if constexpr (FILL)
+                glds_f32(reinterpret_cast<const float *>(t.idx) + c0,
+                         reinterpret_cast<float *>(W.pid), lane, cn);
             wait_vm0();
             wave_sync();
             if constexpr (FILL) {
@@ -356,24 +327,17 @@ void launch_ball_packet(const Tree &t, const float *q, const uint32_t *order, ui
         const char *e = knob("NBKD_BALL_PLAIN");
         return !(e && atoi(e) == 0);
     }();
-    // NBKD_BALL_AHEAD (experiments build, read per launch): the count walks ahead
-    const char *ea = knob("NBKD_BALL_AHEAD");
-    const bool ahead = ea && atoi(ea) != 0;
     PadLeaves pad;
     for (int j = 0; j < NBKD_PAD_LEAVES; ++j)
         pad.id[j] = t.npad_leaves <= NBKD_PAD_LEAVES ? t.pad_leaves[j] : 0xFFFFFFFFu;
-#define NBKD_BALL(PER, FILL, AH)                                                               \
-    ball_packet_kernel<PER, FILL, AH><<<blocks, TB, 0, s>>>(view(t), t.leafinfo, q, order, m,  \
-                                                            r2, pad, out_count, row_offsets,   \
-                                                            out_idx, tnum, plain_ok)
+#define NBKD_BALL(PER, FILL)                                                                   \
+    ball_packet_kernel<PER, FILL><<<blocks, TB, 0, s>>>(view(t), t.leafinfo, q, order, m, r2,  \
+                                                        pad, out_count, row_offsets, out_idx, \
+                                                        tnum, plain_ok)
     if (t.periodic) {
-        if (out_idx) NBKD_BALL(true, true, false);
-        else if (ahead) NBKD_BALL(true, false, true);
-        else NBKD_BALL(true, false, false);
+        if (out_idx) NBKD_BALL(true, true); else NBKD_BALL(true, false);
     } else {
-        if (out_idx) NBKD_BALL(false, true, false);
-        else if (ahead) NBKD_BALL(false, false, true);
-        else NBKD_BALL(false, false, false);
+        if (out_idx) NBKD_BALL(false, true); else NBKD_BALL(false, false);
     }
 #undef NBKD_BALL
 }
