@@ -48,6 +48,8 @@ void free_tree(Tree &t) {
     tree_free(t.y);
     tree_free(t.z);
     tree_free(t.idx);
+    tree_free(t.p4);
+    t.p4 = nullptr;
     tree_free(t.nodes);
     tree_free(t.splits);
     tree_free(t.shape_c);

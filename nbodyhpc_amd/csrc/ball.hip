@@ -36,8 +36,7 @@ struct PadLeaves {
 };
 
 struct alignas(16) BallLds {
-    float pb[3][CHUNK];
-    uint32_t pid[CHUNK];
+    float4 p4[CHUNK]; // the staged points: x, y, z, original id bits (Tree::p4)
     float4 qs[64]; // the wave's query coordinates, for the transposed count
 };
 
@@ -145,18 +144,14 @@ ball_packet_kernel(DevTree t, const uint32_t *__restrict__ linfo, const float *_
         for (uint32_t c0 = lpos; c0 < lend; c0 += CHUNK) {
             const uint32_t cn = min((uint32_t)CHUNK, lend - c0);
             wave_sync();
-            glds_f32(t.x + c0, W.pb[0], lane, cn);
-            glds_f32(t.y + c0, W.pb[1], lane, cn);
-            glds_f32(t.z + c0, W.pb[2], lane, cn);
-            if constexpr (FILL)
-                glds_f32(reinterpret_cast<const float *>(t.idx) + c0,
-                         reinterpret_cast<float *>(W.pid), lane, cn);
+            glds_f4(t.p4 + c0, W.p4, lane, cn);
             wait_vm0();
             wave_sync();
             if constexpr (FILL) {
                 if (full) {
 #pragma unroll 1
-                    for (uint32_t u = 0; u < cn; ++u) out_idx[wpos + cnt + u] = W.pid[u];
+                    for (uint32_t u = 0; u < cn; ++u)
+                        out_idx[wpos + cnt + u] = __float_as_uint(W.p4[u].w);
                     cnt += cn;
                 }
             }
@@ -172,7 +167,8 @@ ball_packet_kernel(DevTree t, const uint32_t *__restrict__ linfo, const float *_
                 trans = (uint32_t)__popcll(pm) * 8u <= cn * tnum;
                 if (trans) {
                     const bool pv = (uint32_t)lane < cn;
-                    const float px = W.pb[0][lane], py = W.pb[1][lane], pz = W.pb[2][lane];
+                    const float4 pl = W.p4[lane];
+                    const float px = pl.x, py = pl.y, pz = pl.z;
                     uint64_t rem = pm;
                     // periodic leaves no partial query wraps around: the plain d2
                     // has the same bits (wrap_free), 8 VALU instead of 14 a step
@@ -198,23 +194,13 @@ ball_packet_kernel(DevTree t, const uint32_t *__restrict__ linfo, const float *_
                 }
             }
             if (part && !trans) {
-                // 4 staged points per step (float4 LDS reads); slots past cn hold
-                // stale data and are masked
-#pragma unroll 1
-                for (uint32_t u0 = 0; u0 < cn; u0 += 4) {
-                    const float4 xv = *reinterpret_cast<const float4 *>(&W.pb[0][u0]);
-                    const float4 yv = *reinterpret_cast<const float4 *>(&W.pb[1][u0]);
-                    const float4 zv = *reinterpret_cast<const float4 *>(&W.pb[2][u0]);
-                    const float d[4] = {point_d2_fast<PER>(qx, qy, qz, xv.x, yv.x, zv.x, L),
-                                        point_d2_fast<PER>(qx, qy, qz, xv.y, yv.y, zv.y, L),
-                                        point_d2_fast<PER>(qx, qy, qz, xv.z, yv.z, zv.z, L),
-                                        point_d2_fast<PER>(qx, qy, qz, xv.w, yv.w, zv.w, L)};
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        if (u0 + j < cn && d[j] <= thr) {
-                            if constexpr (FILL) out_idx[wpos + cnt] = W.pid[u0 + j];
-                            ++cnt;
-                        }
+                // each lane loops over the staged points (one 16-B LDS read each)
+#pragma unroll 2
+                for (uint32_t u = 0; u < cn; ++u) {
+                    const float4 a = W.p4[u];
+                    if (point_d2_fast<PER>(qx, qy, qz, a.x, a.y, a.z, L) <= thr) {
+                        if constexpr (FILL) out_idx[wpos + cnt] = __float_as_uint(a.w);
+                        ++cnt;
                     }
                 }
             }

@@ -1299,6 +1299,14 @@ struct Carve {
 
 } // namespace
 
+// the points packed per tree position, after group_kernel's final order
+__global__ void __launch_bounds__(256)
+pack4_kernel(const float *__restrict__ x, const float *__restrict__ y, const float *__restrict__ z,
+             const uint32_t *__restrict__ idx, uint64_t n8, float4 *__restrict__ p4) {
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n8; i += (uint64_t)gridDim.x * 256)
+        p4[i] = make_float4(x[i], y[i], z[i], __uint_as_float(idx[i]));
+}
+
 nbkd_status build_tree(Tree &t, const float *xyz, uint64_t n, int32_t leaf_size, bool input_dev,
                        hipStream_t s) {
     const uint64_t n8 = (n + 7) / 8 * 8;
@@ -1577,6 +1585,10 @@ nbkd_status build_tree(Tree &t, const float *xyz, uint64_t n, int32_t leaf_size,
                 group_kernel<NBKD_GBLOCK / 64><<<(unsigned)std::max<uint64_t>(blocks, 1), TB, 0, s>>>(
                     t.nodes, t.nnodes, t.x, t.y, t.z, t.idx, t.n, t.ginfo, t.hinfo,
                     reinterpret_cast<uint32_t *>(t.leafinfo), d_bbox);
+            NBKD_HIP(hipGetLastError());
+            NBKD_HIP(tree_malloc((void **)&t.p4, n8 * sizeof(float4)));
+            pack4_kernel<<<(unsigned)std::min<uint64_t>((n8 + 255) / 256, (uint64_t)cus * 16), 256,
+                           0, s>>>(t.x, t.y, t.z, t.idx, n8, t.p4);
         } else {
             uint64_t blocks = std::min<uint64_t>((t.nnodes + TB - 1) / TB, 16384);
             leafinfo_kernel<<<(unsigned)std::max<uint64_t>(blocks, 1), TB, 0, s>>>(

@@ -104,6 +104,11 @@ struct Tree {
     int depth = 0; // max node depth (root = 0)
     float *x = nullptr, *y = nullptr, *z = nullptr;
     uint32_t *idx = nullptr;
+    // the same points packed (x, y, z, idx bits) per tree position: the packet
+    // kernels stage a leaf with one 16-B-per-lane direct-to-LDS load and carry
+    // the original id with each candidate (build.hip pack4_kernel; nbkd_set_ids
+    // remaps both idx and .w)
+    float4 *p4 = nullptr;
     nbkd_node *nodes = nullptr;
     // descent helpers: split value per node and the shape table
     // (count -> subtree node count, sorted by count) of this (n8, leaf)
@@ -158,6 +163,7 @@ struct DevTree {
     const float *__restrict__ y;
     const float *__restrict__ z;
     const uint32_t *__restrict__ idx;
+    const float4 *__restrict__ p4;
     const nbkd_node *__restrict__ nodes;
     uint32_t n8;
     uint32_t nnodes;
@@ -166,7 +172,8 @@ struct DevTree {
 };
 
 inline DevTree view(const Tree &t) {
-    return DevTree{t.x, t.y, t.z, t.idx, t.nodes, (uint32_t)t.n8, (uint32_t)t.nnodes, t.box, t.nbox};
+    return DevTree{t.x, t.y, t.z, t.idx, t.p4, t.nodes, (uint32_t)t.n8, (uint32_t)t.nnodes, t.box,
+                   t.nbox};
 }
 
 // Tuning.  The production library reads no environment variable: every

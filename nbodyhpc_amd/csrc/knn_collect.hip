@@ -90,7 +90,7 @@ struct CollectLdsG {
     float scl[64]; // per lane: bucket factor (d2_bucket)
     uint32_t cnt[64];
     uint32_t hist[NB / 4][65];  // padded rows: one lane's 4 words sit in 4 banks
-    float pb[3][GCHUNK];
+    float4 p4[GCHUNK];           // the staged points: x, y, z, original id bits
     float gb[6 * GMAX];          // the chunk's group boxes (lo.x, hi.x, lo.y, hi.y, lo.z, hi.z)
     float tb[8];                 // the leaf's tight box (leafinfo words 0..5)
     uint16_t pairs[64 * GMAX];   // (slot, lane, group) pairs: slot | lane << 6 | group << 12
@@ -101,9 +101,7 @@ struct CollectLdsG {
 // words: lo.xyz, hi.xyz)
 #define NBKD_COLLECT_STAGE_G(LPOS, CN, TBOX)                                                       \
     do {                                                                                           \
-        glds_f32(t.x + (LPOS), W.pb[0], lane, (CN));                                               \
-        glds_f32(t.y + (LPOS), W.pb[1], lane, (CN));                                               \
-        glds_f32(t.z + (LPOS), W.pb[2], lane, (CN));                                               \
+        glds_f4(t.p4 + (LPOS), W.p4, lane, (CN));                                                  \
         glds_f32(ginfo + 6 * (size_t)((LPOS) / NBKD_GROUP), W.gb, lane, 6 * ((CN) / NBKD_GROUP));  \
         glds_f32((TBOX), W.tb, lane, 6);                                                           \
     } while (0)
@@ -260,8 +258,8 @@ __device__ __forceinline__ void grp_packet(const DevTree &t, const float *__rest
                         const uint32_t qs = pr & 63u, owner = (pr >> 6) & 63u;
                         const uint32_t pi = (pr >> 12) * NBKD_GROUP + (ti % NBKD_GROUP);
                         const float4 qq = W.sq[qs];
-                        const float d = point_d2_fast<M>(qq.x, qq.y, qq.z, W.pb[0][pi],
-                                                         W.pb[1][pi], W.pb[2][pi], L);
+                        const float4 pp = W.p4[pi];
+                        const float d = point_d2_fast<M>(qq.x, qq.y, qq.z, pp.x, pp.y, pp.z, L);
                         if (d < qq.w) {
                             const uint32_t j = d2_bucket(d, W.scl[qs]);
                             atomicAdd(&W.hist[j >> 2][owner], 1u << (8 * (j & 3)));
@@ -269,8 +267,10 @@ __device__ __forceinline__ void grp_packet(const DevTree &t, const float *__rest
                             // a row past capg is a failure whose column is never read (both
                             // selects): its extra hits overwrite its last slot (no branch)
                             const uint32_t sw = min(sl, capg - 1u);
+                            // the candidate carries the point's original id (p4.w):
+                            // the selects write it without a gather
                             col[((sw >> 4) * qpp + owner) * 16u + (sw & 15u)] =
-                                make_uint2(__float_as_uint(d), c0 + pi);
+                                make_uint2(__float_as_uint(d), __float_as_uint(pp.w));
                         }
                     }
                 }
@@ -571,13 +571,7 @@ knn_select_kernel(DevTree t, const float *__restrict__ q, const uint32_t *__rest
         wave_sync();
         store_rows<CC>(stage, rowq, reinterpret_cast<uint32_t *>(out_d), k, j0 - (KC - k), lane);
     }
-    // tree positions -> original ids: KC independent gathers in flight per lane
-    // (inside store_rows' loop they would be issued one after another)
-#pragma unroll
-    for (int j = 0; j < KC; ++j) { // branch-free: no-neighbour slots gather idx[0] and keep the sentinel
-        const uint32_t v = t.idx[ti[j] == 0xFFFFFFFFu ? 0u : ti[j]];
-        ti[j] = ti[j] == 0xFFFFFFFFu ? ti[j] : v;
-    }
+    // ti holds original ids (the collect kernel stores them with the candidates)
 #pragma unroll
     for (int j0 = 0; j0 < KC; j0 += CC) {
         wave_sync();
@@ -866,7 +860,7 @@ knn_select_wave_kernel(DevTree t, const float *__restrict__ q, const uint32_t *_
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             const int e = r * 64 + lane;
-            gi[r] = (e < k && tp[r] != 0xFFFFFFFFu) ? t.idx[tp[r]] : 0xFFFFFFFFu;
+            gi[r] = e < k ? tp[r] : 0xFFFFFFFFu; // ids, or the no-neighbour sentinel
             if (e < k) out_d[base + e] = sq ? td[r] : sqrtf(td[r]);
         }
         if (pend_q != 0xFFFFFFFFu) {

@@ -17,6 +17,12 @@ __device__ __forceinline__ void glds_f32(const float *src, float *dst, int lane,
         __builtin_amdgcn_global_load_lds((gas_ptr)(src + lane), (las_ptr)dst, 4, 0, 0);
 }
 
+// lanes < n copy the 16-B src[lane] into dst[lane] (LDS), one instruction for 64 points
+__device__ __forceinline__ void glds_f4(const float4 *src, float4 *dst, int lane, uint32_t n) {
+    if ((uint32_t)lane < n)
+        __builtin_amdgcn_global_load_lds((gas_ptr)(src + lane), (las_ptr)dst, 16, 0, 0);
+}
+
 // s_waitcnt vmcnt(0) (expcnt / lgkmcnt untouched): the direct-to-LDS loads have landed
 __device__ __forceinline__ void wait_vm0() { __builtin_amdgcn_s_waitcnt(0x0F70); }
 

@@ -88,12 +88,15 @@ band_scatter_kernel(const float *__restrict__ xyz, const uint32_t *__restrict__ 
     }
 }
 
-__global__ void remap_ids_kernel(uint32_t *__restrict__ idx, uint64_t n8, uint64_t n,
-                                 const uint32_t *__restrict__ ids) {
+__global__ void remap_ids_kernel(uint32_t *__restrict__ idx, float4 *__restrict__ p4, uint64_t n8,
+                                 uint64_t n, const uint32_t *__restrict__ ids) {
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= n8) return;
     const uint32_t p = idx[j];
-    if (p < n) idx[j] = ids[p];
+    if (p < n) {
+        idx[j] = ids[p];
+        if (p4) p4[j].w = __uint_as_float(ids[p]); // the packed copy carries the id too
+    }
 }
 
 // a query's result is exact iff its k-th distance does not reach past the
@@ -287,7 +290,7 @@ nbkd_status nbkd_set_ids(nbkd_tree *tree, const uint32_t *ids, uint32_t flags, v
         dids = tmp.as<uint32_t>();
     }
     const unsigned blocks = (unsigned)((t.n8 + 255) / 256);
-    remap_ids_kernel<<<blocks, 256, 0, s>>>(t.idx, t.n8, t.n, dids);
+    remap_ids_kernel<<<blocks, 256, 0, s>>>(t.idx, t.p4, t.n8, t.n, dids);
     NBKD_HIP(hipGetLastError());
     // every later call on any workspace (any stream) sees the new ids
     NBKD_HIP(hipStreamSynchronize(s));
