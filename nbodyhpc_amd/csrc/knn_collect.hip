@@ -424,19 +424,17 @@ __device__ __forceinline__ void mark_failure(float qx, float qy, float qz, float
 // One 8-KB candidate block (64 rows x 8 pieces of 16 B, row-contiguous) into
 // LDS by direct loads, no VGPR staging: LDS piece x = i*64 + lane takes the
 // block's row r = x/8, piece (x%8) ^ (r%8), so row r's piece j sits at
-// r*8 + (j ^ (r & 7)) and the per-row reads are bank-conflict free.  Only the
-// pieces holding candidates are read (piece j of the block starting at slot
-// s0 holds slots s0 + 2j, s0 + 2j + 1; rown[r] = row r's count, 0 for a row
-// that needs nothing): a row's last block is usually part full, and
-// round 3 read its whole 128-B line.  all_rows: read every piece (A/B).
-__device__ __forceinline__ void issue_block(const uint4 *b4, uint4 *lds4, int lane,
-                                            const uint32_t *rown, uint32_t s0, bool all_rows) {
+// r*8 + (j ^ (r & 7)) and the per-row reads are bank-conflict free.
+__device__ __forceinline__ void issue_block(const uint4 *b4, uint4 *lds4, int lane, uint64_t rows) {
+    // rows: bit r set = row r holds candidates in this block; the other rows'
+    // 128-B lines are not read (their LDS slots keep stale data, masked by count)
     const uint32_t r0 = (uint32_t)lane >> 3, jj = (uint32_t)lane & 7u;
-    const uint32_t pj = jj ^ r0; // the piece this lane moves, for every row r0 + 8 i
-    const uint4 *src = b4 + r0 * 8 + pj;
+    const uint4 *src = b4 + r0 * 8 + (jj ^ r0);
+    // bits r0, r0+8, .., r0+56 of rows -> bits 0..7 of m
+    const uint32_t m = (uint32_t)((((rows >> r0) & 0x0101010101010101ull) * 0x0102040810204080ull) >> 56);
 #pragma unroll
     for (int i = 0; i < 8; ++i)
-        if (all_rows || s0 + 2 * pj < rown[r0 + 8 * i])
+        if (m & (1u << i))
             __builtin_amdgcn_global_load_lds((gas_ptr)(src + 64 * i), (las_ptr)(lds4 + 64 * i), 16, 0, 0);
 }
 
@@ -454,9 +452,8 @@ knn_select_kernel(DevTree t, const float *__restrict__ q, const uint32_t *__rest
     constexpr int SW = CC < 32 ? 32 * 64 : CC * 64; // >= 8 KB: one candidate block
     __shared__ uint32_t stage_all[WPB][SW];
     __shared__ uint32_t rowq_all[WPB][64];
-    __shared__ uint32_t rown_all[WPB][64];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    uint32_t *stage = stage_all[wave], *rowq = rowq_all[wave], *rown = rown_all[wave];
+    uint32_t *stage = stage_all[wave], *rowq = rowq_all[wave];
     // a device-counted pass (retry rounds) is launched for its cap and reads
     // its count here (a loop over blocks made the compiler spill td / ti)
     const uint32_t m = span_m(span);
@@ -506,12 +503,8 @@ knn_select_kernel(DevTree t, const float *__restrict__ q, const uint32_t *__rest
     const uint4 *blk = reinterpret_cast<const uint4 *>(
         cand + (whole ? (size_t)(gq >> 6) * 64u * capg : (size_t)gq * capg));
     uint4 *const lds4 = reinterpret_cast<uint4 *>(stage);
-    // all_rows: read every row's line (A/B of the per-piece masking)
-    if (whole) {
-        rown[lane] = nn;
-        wave_sync();
-    }
-    if (whole && maxn > 0) issue_block(blk, lds4, lane, rown, 0u, all_rows != 0);
+    // all_rows: read every row's line (A/B of the per-row masking)
+    if (whole && maxn > 0) issue_block(blk, lds4, lane, __ballot(nn > 0u) | all_rows);
     for (uint32_t s0 = 0; s0 < maxn; s0 += NS) {
         float bd[NS];
         uint32_t bi[NS];
@@ -545,8 +538,8 @@ knn_select_kernel(DevTree t, const float *__restrict__ q, const uint32_t *__rest
             __builtin_amdgcn_s_waitcnt(0xC07F); // lgkmcnt(0)
             wave_sync();
             if (s0 + NS < maxn)
-                issue_block(blk + (size_t)((s0 + NS) >> 4) * 512u, lds4, lane, rown, s0 + NS,
-                            all_rows != 0);
+                issue_block(blk + (size_t)((s0 + NS) >> 4) * 512u, lds4, lane,
+                            __ballot(nn > s0 + NS) | all_rows);
         }
         // a block with nothing below any lane's current k-th changes nothing
         bool useful = false;

@@ -100,15 +100,9 @@ __global__ void __launch_bounds__(TB)
 leaf_key3_kernel(const float4 *__restrict__ hb, int o, uint32_t n8, uint32_t leaf,
                  const float *__restrict__ q, uint32_t m, uint32_t *__restrict__ keys,
                  uint32_t *__restrict__ vals, float *__restrict__ tg, float mu_c, uint32_t anchor,
-                 float3 box_lo, float3 box_hi, float L, uint32_t *__restrict__ out_list,
-                 uint32_t *__restrict__ out_count) {
+                 float3 box_lo, float3 box_hi) {
     for (uint32_t i = blockIdx.x * TB + threadIdx.x; i < m; i += gridDim.x * TB) {
         const float p[3] = {q[3 * (size_t)i], q[3 * (size_t)i + 1], q[3 * (size_t)i + 2]};
-        // periodic queries outside [0, L]^3 listed here, as outside_box_kernel
-        // would in a separate pass over the queries
-        if (out_list && !(p[0] >= 0.0f && p[0] <= L && p[1] >= 0.0f && p[1] <= L && p[2] >= 0.0f &&
-                          p[2] <= L))
-            out_list[atomicAdd(out_count, 1u)] = i;
         uint32_t left = 0, count = n8;
         int dim = 0;
         float lo[3] = {box_lo.x, box_lo.y, box_lo.z}, hi[3] = {box_hi.x, box_hi.y, box_hi.z};
@@ -837,13 +831,8 @@ SeedParams seed_params(const Tree &t, int k) {
     return p;
 }
 
-// outside_list / outside_count (periodic trees): where the bucketing pass can,
-// it also lists the queries outside [0, L]^3 and sets *outside_done
 nbkd_status sort_queries(const Tree &t, Workspace &ws, const float *dq, uint32_t m, uint32_t *&order,
-                         hipStream_t s, float *tg = nullptr, const SeedParams *sp = nullptr,
-                         uint32_t *outside_list = nullptr, uint32_t *outside_count = nullptr,
-                         bool *outside_done = nullptr) {
-    if (outside_done) *outside_done = false;
+                         hipStream_t s, float *tg = nullptr, const SeedParams *sp = nullptr) {
     order = (uint32_t *)ws.get(WS_ORDER, (size_t)m * 4, s);
     uint32_t *tmp = (uint32_t *)ws.get(WS_TMP, (size_t)m * 4, s);
     uint32_t *keys = (uint32_t *)ws.get(WS_KEYS, (size_t)m * 4, s);
@@ -861,9 +850,7 @@ nbkd_status sort_queries(const Tree &t, Workspace &ws, const float *dq, uint32_t
             leaf_key3_kernel<<<blocks, TB, 0, s>>>((const float4 *)t.hsplit, hblk_offset(t.depth),
                                                    (uint32_t)t.n8, (uint32_t)t.leaf, dq, m,
                                                    keys, order, tg, sp ? sp->mu_c : 0.0f,
-                                                   sp ? sp->anchor : 0u, lo, hi, t.box,
-                                                   outside_list, outside_count);
-            if (outside_done) *outside_done = outside_list != nullptr;
+                                                   sp ? sp->anchor : 0u, lo, hi);
         } else if (t.shape_len <= SHAPE_MAX) {
             const unsigned blocks = (unsigned)std::min<uint64_t>((m + TB - 1) / TB, 8192);
             // periodic: the box; otherwise the real points' bounding box (the
@@ -957,21 +944,8 @@ nbkd_status knn_locked(const Tree &t, Workspace &ws, const float *q, uint64_t m,
         tg = (float *)ws.get(WS_TG, (size_t)mm * 4, s);
         if (!tg) return NBKD_ENOMEM;
     }
-    // queries the packet kernel cannot answer exactly go through the
-    // reference-exact lane-per-query kernel: periodic queries outside [0, L]^3
-    // (listed by the bucketing pass where it can) and queries whose seed radius
-    // held fewer than k points
-    uint32_t *list = nullptr, *count = nullptr;
-    if (packet && (t.periodic || tg)) {
-        list = (uint32_t *)ws.get(WS_LIST, (size_t)mm * 4 + 16, s);
-        if (!list) return NBKD_ENOMEM;
-        count = list + mm;
-        NBKD_HIP(hipMemsetAsync(count, 0, 4, s));
-    }
     uint32_t *ord = nullptr;
-    bool outside_done = false;
-    rc = sort_queries(t, ws, dq, mm, ord, s, tg, &sp, t.periodic ? list : nullptr,
-                      t.periodic ? count : nullptr, &outside_done);
+    rc = sort_queries(t, ws, dq, mm, ord, s, tg, &sp);
     if (rc) return rc;
     float *dd = out_d;
     uint32_t *di = out_i;
@@ -986,10 +960,20 @@ nbkd_status knn_locked(const Tree &t, Workspace &ws, const float *q, uint64_t m,
         if (!stats) return NBKD_ENOMEM;
         NBKD_HIP(hipMemsetAsync(stats, 0, NBKD_NSTATS * 8, s));
     }
-    if (list && t.periodic && !outside_done) {
-        TimedScope ts("knn_outside_box", s);
-        outside_box_kernel<<<(mm + TB - 1) / TB, TB, 0, s>>>(dq, mm, t.box, list, count);
-        NBKD_HIP(hipGetLastError());
+    // queries the packet kernel cannot answer exactly go through the
+    // reference-exact lane-per-query kernel: periodic queries outside [0, L]^3
+    // and queries whose seed radius held fewer than k points
+    uint32_t *list = nullptr, *count = nullptr;
+    if (packet && (t.periodic || tg)) {
+        list = (uint32_t *)ws.get(WS_LIST, (size_t)mm * 4 + 16, s);
+        if (!list) return NBKD_ENOMEM;
+        count = list + mm;
+        NBKD_HIP(hipMemsetAsync(count, 0, 4, s));
+        if (t.periodic) {
+            TimedScope ts("knn_outside_box", s);
+            outside_box_kernel<<<(mm + TB - 1) / TB, TB, 0, s>>>(dq, mm, t.box, list, count);
+            NBKD_HIP(hipGetLastError());
+        }
     }
     if (!packet) { // all queries through the reference-exact lane-per-query kernel
         TimedScope ts("knn_exact", s);
