@@ -27,4 +27,10 @@ rc=$?
 rm -f /tmp/p2e7.f32 /tmp/snap2e7.*
 date
 for f in c5_n1 n2_strong n4_strong c5_n2 redist weak gadget; do echo "== $f"; grep '^{' $O/$f.json 2>/dev/null | cut -c1-300; done
+# (appended) seed-margin A/B at the round-4 head (experiments build knob)
+if [ $rc -eq 0 ] && [ -n "$SEED_AB" ]; then
+  timeout -k 10 900 python3 -u scripts/lib_ab.py --libs "exp@NBKD_KNN_SEED=3.0,exp@NBKD_KNN_SEED=3.5,exp@NBKD_KNN_SEED=4.0" --rounds 2 -- --n 1e8 > $O/seed_ab.log 2>&1
+  rc=$?
+  tail -4 $O/seed_ab.log
+fi
 exit $rc
