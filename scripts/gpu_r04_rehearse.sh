@@ -9,8 +9,9 @@ export TMPDIR=/tmp
 O=gpurun_out/${TAG:-r04r}
 mkdir -p $O
 B="timeout -k 10 600 python3 -u bench.py"
-echo "[rehearse] c5 n1"; date
-$B --workload c5 --steps 3 --warmup 1 > $O/c5_n1.json 2> $O/c5_n1.err \
+echo "[rehearse] suite"; date
+timeout -k 10 900 python3 -u bench.py --suite > $O/suite.json 2> $O/suite.err \
+ && echo "[rehearse] c5 n1" && $B --workload c5 --steps 3 --warmup 1 > $O/c5_n1.json 2> $O/c5_n1.err \
  && echo "[rehearse] n2 strong" && NBKD_BENCH_SAME_DEVICE=1 $B --gpus 2 --steps 3 --warmup 1 --no-cpu-baseline > $O/n2_strong.json 2> $O/n2_strong.err \
  && echo "[rehearse] n4 strong" && NBKD_BENCH_SAME_DEVICE=1 $B --gpus 4 --steps 3 --warmup 1 --no-cpu-baseline > $O/n4_strong.json 2> $O/n4_strong.err \
  && echo "[rehearse] c5 n2" && NBKD_BENCH_SAME_DEVICE=1 $B --workload c5 --gpus 2 --particles 2e7 --steps 3 --warmup 1 > $O/c5_n2.json 2> $O/c5_n2.err \
@@ -26,7 +27,7 @@ io.write_gadget('/tmp/snap2e7', pts[:4_000_000], box=1.0, num_files=2)
 rc=$?
 rm -f /tmp/p2e7.f32 /tmp/snap2e7.*
 date
-for f in c5_n1 n2_strong n4_strong c5_n2 redist weak gadget; do echo "== $f"; grep '^{' $O/$f.json 2>/dev/null | cut -c1-300; done
+for f in suite c5_n1 n2_strong n4_strong c5_n2 redist weak gadget; do echo "== $f"; grep '^{' $O/$f.json 2>/dev/null | cut -c1-300; done
 # (appended) seed-margin A/B at the round-4 head (experiments build knob)
 if [ $rc -eq 0 ] && [ -n "$SEED_AB" ]; then
   timeout -k 10 900 python3 -u scripts/lib_ab.py --libs "exp@NBKD_KNN_SEED=3.0,exp@NBKD_KNN_SEED=3.5,exp@NBKD_KNN_SEED=4.0" --rounds 2 -- --n 1e8 > $O/seed_ab.log 2>&1
