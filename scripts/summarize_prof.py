@@ -32,6 +32,16 @@ def find(d, pat):
     return hits[-1] if hits else None
 
 
+def _stats_instance(name):
+    """knn_collect_grp_kernel<PER, OCC, STATS, LOOP, AHEAD>: STATS is the third
+    template argument (the work-counter instance; its timing and traffic are not
+    the production kernel's)."""
+    if "knn_collect_grp_kernel<" not in name:
+        return False
+    args = name.split("knn_collect_grp_kernel<", 1)[1].split(">", 1)[0].split(",")
+    return len(args) >= 3 and args[2].strip() == "true"
+
+
 def per_dispatch(path, regex):
     """Counter sum per dispatch of the full-size launches of the kernel (the
     work-counter instance and the small retry launches are left out)."""
@@ -40,7 +50,7 @@ def per_dispatch(path, regex):
         for row in csv.DictReader(f):
             if regex not in row["Kernel_Name"]:
                 continue
-            if ", true>(" in row["Kernel_Name"]:  # the work-counter (STATS) instance
+            if _stats_instance(row["Kernel_Name"]):  # the work-counter (STATS) instance
                 continue
             key = row["Dispatch_Id"]
             vals[key] = vals.get(key, 0.0) + float(row["Counter_Value"])
