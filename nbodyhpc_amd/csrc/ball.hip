@@ -51,18 +51,6 @@ __device__ __forceinline__ float box_ub2(float qx, float qy, float qz, const flo
     return (ux * ux + uy * uy) + uz * uz;
 }
 
-// Every point p of the box lies within L/2 of q on every axis: then the
-// periodic per-axis minimum min(d^2, (L - |d|)^2) (the reference's
-// min(d^2, (d-L)^2, (d+L)^2), kdtree.hpp:72-84) is d^2 itself with the same
-// bits, since |fl(p - q)| <= max(|fl(lo - q)|, |fl(hi - q)|) <= L/2 <= fl(L - |d|)
-// (monotone rounding; L/2 is exact).  So the plain formula may replace it.
-template <bool PER>
-__device__ __forceinline__ bool wrap_free(float qx, float qy, float qz, const float b[6], float L) {
-    const float h = 0.5f * L;
-    return fmaxf(fabsf(b[0] - qx), fabsf(b[1] - qx)) <= h &&
-           fmaxf(fabsf(b[2] - qy), fabsf(b[3] - qy)) <= h &&
-           fmaxf(fabsf(b[4] - qz), fabsf(b[5] - qz)) <= h;
-}
 
 // occupancy per variant ([periodic][fill]).  With the node-id stack the
 // periodic count fits 8 waves per SIMD without spills (62 VGPRs); the
@@ -172,7 +160,7 @@ ball_packet_kernel(DevTree t, const uint32_t *__restrict__ linfo, const float *_
                     uint64_t rem = pm;
                     // periodic leaves no partial query wraps around: the plain d2
                     // has the same bits (wrap_free), 8 VALU instead of 14 a step
-                    if (!PER || (plain_ok && __all(!part || wrap_free<PER>(qx, qy, qz, tb, L)))) {
+                    if (!PER || (plain_ok && __all(!part || wrap_free(qx, qy, qz, tb, L)))) {
                         while (rem) {
                             const int j = __builtin_ctzll(rem);
                             rem &= rem - 1;

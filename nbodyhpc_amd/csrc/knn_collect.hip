@@ -27,6 +27,7 @@
 // A query whose ball holds fewer than k points (seed too small) or more than
 // the column capacity is listed for the reference-exact kernel (query.hip).
 #include <algorithm>
+#include <type_traits>
 
 #include "internal.hpp"
 #include "metric.hpp"
@@ -220,60 +221,82 @@ __device__ __forceinline__ void grp_packet(const DevTree &t, const float *__rest
                     W.scl[r] = nb_over_s;
                 }
                 wave_sync();
-                // (needing lane, group) box tests, 8 lanes per needing lane (one
-                // per group); the groups reached become the pair list, entries
-                // slot | owner lane << 6 | group << 12
-                uint32_t np = 0;
-                const uint32_t ntest = nneed * GMAX;
+#if defined(NBKD_CPLAIN)
+                // every needing lane's ball box lies within L/2 of its query on
+                // every axis (wrap_free): the plain d2 and box bounds have the
+                // periodic ones' bits for the chunk's points (8 VALU a pair
+                // instead of 14)
+                const bool plain = M && __all(!need || wrap_free(qx, qy, qz, tb, L));
+#else
+                constexpr bool plain = false;
+#endif
+                // Tried and dropped (r04s): the hit's column slot as the owner's
+                // count plus the hits below it in its run of lanes (the pair list
+                // is slot-major), with no returning LDS atomic and all of a step's
+                // LDS reads issued together: collect 46.7 -> 55.1 ms per 1e8
+                // queries (profiles/r04s_ab_seg_wide.txt); the 64-bit lane-mask
+                // arithmetic costs more issue than the atomics' waits.
+                auto scan_pairs = [&](auto mm) {
+                    constexpr bool MM = decltype(mm)::value;
+                    // (needing lane, group) box tests, 8 lanes per needing lane (one
+                    // per group); the groups reached become the pair list, entries
+                    // slot | owner lane << 6 | group << 12
+                    uint32_t np = 0;
+                    const uint32_t ntest = nneed * GMAX;
 #pragma unroll 1
-                for (uint32_t t0 = 0; t0 < ntest; t0 += 64) {
-                    const uint32_t ti = t0 + lane;
-                    const uint32_t g = ti % GMAX;
-                    const uint32_t sl = ti / GMAX;
-                    uint32_t owner = 0;
-                    bool hit = false;
-                    if (ti < ntest && g < ng) {
-                        owner = W.slot[sl];
-                        const float4 qq = W.sq[sl];
-                        const float gbx[6] = {W.gb[6 * g], W.gb[6 * g + 1], W.gb[6 * g + 2],
-                                              W.gb[6 * g + 3], W.gb[6 * g + 4], W.gb[6 * g + 5]};
-                        hit = box_lb2<M>(qq.x, qq.y, qq.z, gbx, L) <= qq.w;
+                    for (uint32_t t0 = 0; t0 < ntest; t0 += 64) {
+                        const uint32_t ti = t0 + lane;
+                        const uint32_t g = ti % GMAX;
+                        const uint32_t sl = ti / GMAX;
+                        uint32_t owner = 0;
+                        bool hit = false;
+                        if (ti < ntest && g < ng) {
+                            owner = W.slot[sl];
+                            const float4 qq = W.sq[sl];
+                            const float gbx[6] = {W.gb[6 * g], W.gb[6 * g + 1], W.gb[6 * g + 2],
+                                                  W.gb[6 * g + 3], W.gb[6 * g + 4], W.gb[6 * g + 5]};
+                            hit = box_lb2<MM>(qq.x, qq.y, qq.z, gbx, L) <= qq.w;
+                        }
+                        const uint64_t hm = __ballot(hit);
+                        if (hit)
+                            W.pairs[np + mbcnt64(hm)] = (uint16_t)(sl | (owner << 6) | (g << 12));
+                        np += (uint32_t)__popcll(hm);
                     }
-                    const uint64_t hm = __ballot(hit);
-                    if (hit)
-                        W.pairs[np + mbcnt64(hm)] = (uint16_t)(sl | (owner << 6) | (g << 12));
-                    np += (uint32_t)__popcll(hm);
-                }
-                NBKD_PH(2);
-                wave_sync();
-                // each pair's 8 points spread over 8 consecutive lanes
-                const uint32_t ntrip = np * NBKD_GROUP;
-                if constexpr (STATS) st[5] += ntrip;
+                    NBKD_PH(2);
+                    wave_sync();
+                    // each pair's 8 points spread over 8 consecutive lanes
+                    const uint32_t ntrip = np * NBKD_GROUP;
+                    if constexpr (STATS) st[5] += ntrip;
 #pragma unroll 1
-                for (uint32_t t0 = 0; t0 < ntrip; t0 += 64) {
-                    if constexpr (STATS) ++st[4];
-                    const uint32_t ti = t0 + lane;
-                    if (ti < ntrip) {
-                        const uint32_t pr = W.pairs[ti / NBKD_GROUP];
-                        const uint32_t qs = pr & 63u, owner = (pr >> 6) & 63u;
-                        const uint32_t pi = (pr >> 12) * NBKD_GROUP + (ti % NBKD_GROUP);
-                        const float4 qq = W.sq[qs];
-                        const float4 pp = W.p4[pi];
-                        const float d = point_d2_fast<M>(qq.x, qq.y, qq.z, pp.x, pp.y, pp.z, L);
-                        if (d < qq.w) {
-                            const uint32_t j = d2_bucket(d, W.scl[qs]);
-                            atomicAdd(&W.hist[j >> 2][owner], 1u << (8 * (j & 3)));
-                            const uint32_t sl = atomicAdd(&W.cnt[owner], 1u);
-                            // a row past capg is a failure whose column is never read (both
-                            // selects): its extra hits overwrite its last slot (no branch)
-                            const uint32_t sw = min(sl, capg - 1u);
-                            // the candidate carries the point's original id (p4.w):
-                            // the selects write it without a gather
-                            col[((sw >> 4) * qpp + owner) * 16u + (sw & 15u)] =
-                                make_uint2(__float_as_uint(d), __float_as_uint(pp.w));
+                    for (uint32_t t0 = 0; t0 < ntrip; t0 += 64) {
+                        if constexpr (STATS) ++st[4];
+                        const uint32_t ti = t0 + lane;
+                        if (ti < ntrip) {
+                            const uint32_t pr = W.pairs[ti / NBKD_GROUP];
+                            const uint32_t qs = pr & 63u, owner = (pr >> 6) & 63u;
+                            const uint32_t pi = (pr >> 12) * NBKD_GROUP + (ti % NBKD_GROUP);
+                            const float4 qq = W.sq[qs];
+                            const float4 pp = W.p4[pi];
+                            const float d = point_d2_fast<MM>(qq.x, qq.y, qq.z, pp.x, pp.y, pp.z, L);
+                            if (d < qq.w) {
+                                const uint32_t j = d2_bucket(d, W.scl[qs]);
+                                atomicAdd(&W.hist[j >> 2][owner], 1u << (8 * (j & 3)));
+                                const uint32_t sl = atomicAdd(&W.cnt[owner], 1u);
+                                // a row past capg is a failure whose column is never read (both
+                                // selects): its extra hits overwrite its last slot (no branch)
+                                const uint32_t sw = min(sl, capg - 1u);
+                                // the candidate carries the point's original id (p4.w):
+                                // the selects write it without a gather
+                                col[((sw >> 4) * qpp + owner) * 16u + (sw & 15u)] =
+                                    make_uint2(__float_as_uint(d), __float_as_uint(pp.w));
+                            }
                         }
                     }
-                }
+                };
+                if (plain)
+                    scan_pairs(std::false_type{});
+                else
+                    scan_pairs(std::integral_constant<bool, M>{});
                 wave_sync();
                 cnt = W.cnt[lane];
                 NBKD_PH(4);
@@ -346,8 +369,29 @@ __device__ __forceinline__ void collect_packet(
     uint32_t cnt = 0;
     uint64_t st[13] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     float kth = seed;
-    grp_packet<PER, PER, STATS, AHEAD>(t, ginfo, linfo, hinfo, W, lane, qx, qy, qz, kth, s_over_nb,
-                                nb_over_s, col, qpp, capg, kq, cnt, st);
+#if defined(NBKD_PKT_PLAIN)
+    // Every lane's seed ball clears the box faces (a margin r' > sqrt(seed) on
+    // every axis): a point within the ball is then within L/2 of the query on
+    // every axis, where the plain per-axis distance has the periodic minimum's
+    // bits (metric.hpp point_d2_fast), and a point beyond it fails both tests.
+    // So the packet walks with the plain formulas: the same candidates, the
+    // same d2 bits, box bounds that are valid for every point that can be a
+    // candidate.  The bound only shrinks, so the test at the start holds for
+    // the whole walk.
+    bool plain = false;
+    if constexpr (PER) {
+        const float r1 = sqrtf(fmaxf(seed, 0.0f)) * 1.01f + t.box * 1e-6f;
+        const bool wf = !valid || (fin && r1 <= 0.25f * t.box && qx >= r1 && t.box - qx >= r1 &&
+                                   qy >= r1 && t.box - qy >= r1 && qz >= r1 && t.box - qz >= r1);
+        plain = __all(wf);
+    }
+    if (plain)
+        grp_packet<PER, false, STATS, AHEAD>(t, ginfo, linfo, hinfo, W, lane, qx, qy, qz, kth,
+                                             s_over_nb, nb_over_s, col, qpp, capg, kq, cnt, st);
+    else
+#endif
+        grp_packet<PER, PER, STATS, AHEAD>(t, ginfo, linfo, hinfo, W, lane, qx, qy, qz, kth,
+                                           s_over_nb, nb_over_s, col, qpp, capg, kq, cnt, st);
     if (valid) ccount[gq] = cnt;
     // the final bound: at least k candidates lie strictly below it (bound
     // histogram), so none at or above it is among the k smallest

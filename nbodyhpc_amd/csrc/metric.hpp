@@ -113,6 +113,18 @@ __device__ __forceinline__ float box_lb2(float qx, float qy, float qz, const flo
     return r;
 }
 
+// Every point p of the box lies within L/2 of q on every axis: then the
+// periodic per-axis minimum min(d^2, (L - |d|)^2) (the reference's
+// min(d^2, (d-L)^2, (d+L)^2), kdtree.hpp:72-84) is d^2 itself with the same
+// bits, since |fl(p - q)| <= max(|fl(lo - q)|, |fl(hi - q)|) <= L/2 <= fl(L - |d|)
+// (monotone rounding; L/2 is exact).  So the plain formula may replace it.
+__device__ __forceinline__ bool wrap_free(float qx, float qy, float qz, const float b[6], float L) {
+    const float h = 0.5f * L;
+    return fmaxf(fabsf(b[0] - qx), fabsf(b[1] - qx)) <= h &&
+           fmaxf(fabsf(b[2] - qy), fabsf(b[3] - qy)) <= h &&
+           fmaxf(fabsf(b[4] - qz), fabsf(b[5] - qz)) <= h;
+}
+
 // ------------------------------------------------------------------ register sorting networks
 template <int N, bool IDX = true>
 __device__ __forceinline__ void ce(float (&d)[N], uint32_t (&i)[N], int a, int b) {

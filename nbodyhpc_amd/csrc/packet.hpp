@@ -136,6 +136,27 @@ typedef const __attribute__((address_space(4))) NodeBox *cbox_ptr;
 typedef const NodeBox *cbox_ptr;
 #endif
 
+// Tried and dropped (r04s): 64-B node blocks (a node's record and its
+// children's) so a descent waits on one scalar load per two levels: collect
+// 46.7 -> 50.1 ms, radius count 112.3 -> 124.5 ms at 1e8
+// (profiles/r04s_ab_seg_wide.txt).  The node loads mostly hit the scalar
+// cache; four times the bytes per record and 12 more live SGPRs (spilled
+// kernel arguments) cost more than the shorter chains save.
+//
+// Node loads of the walk.  NBKD_POPLOAD: a popped node's record is loaded
+// beside its cell box; the empty asm takes every word as an operand, so the
+// load is not sunk below the box test and both arrive after one scalar-load
+// latency.
+#if defined(NBKD_POPLOAD)
+#define NBKD_WALK_PREFETCH()                                                                       \
+    const nbkd_node wp_ = cnodes[node];                                                            \
+    asm volatile("" ::"s"(wp_.dimension), "s"(wp_.split), "s"(wp_.left), "s"(wp_.right));
+#define NBKD_WALK_TAKE() nd = wp_;
+#else
+#define NBKD_WALK_PREFETCH()
+#define NBKD_WALK_TAKE() nd = cnodes[node];
+#endif
+
 // one internal node with split axis D (compile-time): test both children for
 // every lane; a single wanted child is entered, and only when both are wanted
 // the lanes vote which one is near (entered) and which far (pushed, its seven
@@ -148,8 +169,18 @@ typedef const NodeBox *cbox_ptr;
     {                                                                                              \
         const float split = nd.split;                                                              \
         const float qd = (D) == 0 ? qx : ((D) == 1 ? qy : qz);                                     \
-        const float tl = box_lb_axis<M>(qd, bx[2 * (D)], split, L);                                \
-        const float tr = box_lb_axis<M>(qd, split, bx[2 * (D) + 1], L);                            \
+        float tl, tr;                                                                              \
+        if constexpr (M) {                                                                         \
+            tl = box_lb_axis<M>(qd, bx[2 * (D)], split, L);                                        \
+            tr = box_lb_axis<M>(qd, split, bx[2 * (D) + 1], L);                                    \
+        } else {                                                                                   \
+            /* plain: the child on q's side keeps the slab's bound tm[D] (the   */                 \
+            /* same bits box_lb_axis gives), the other one is (q - split)^2    */                 \
+            const float dd_ = qd - split;                                                          \
+            const float m2_ = dd_ * dd_;                                                           \
+            tl = dd_ > 0.0f ? m2_ : tm[D];                                                         \
+            tr = dd_ > 0.0f ? tm[D] : m2_;                                                         \
+        }                                                                                          \
         const float dl = (((D) == 0 ? tl : tm[0]) + ((D) == 1 ? tl : tm[1])) + ((D) == 2 ? tl : tm[2]); \
         const float dr = (((D) == 0 ? tr : tm[0]) + ((D) == 1 ? tr : tm[1])) + ((D) == 2 ? tr : tm[2]); \
         const uint64_t wl = __ballot(dl <= kth), wr = __ballot(dr <= kth);                         \
@@ -187,12 +218,13 @@ typedef const NodeBox *cbox_ptr;
                 const NodeBox nb_ = cboxes[node];                                                  \
                 _Pragma("unroll") for (int a = 0; a < 6; ++a) bx[a] = nb_.b[a];                    \
             }                                                                                      \
+            NBKD_WALK_PREFETCH();                                                                  \
             tm[0] = box_lb_axis<M>(qx, bx[0], bx[1], L);                                           \
             tm[1] = box_lb_axis<M>(qy, bx[2], bx[3], L);                                           \
             tm[2] = box_lb_axis<M>(qz, bx[4], bx[5], L);                                           \
             wm = __ballot((tm[0] + tm[1]) + tm[2] <= kth);                                         \
             if (wm == 0) continue;                                                                 \
-            nd = cnodes[node];                                                                     \
+            NBKD_WALK_TAKE();                                                                      \
         }                                                                                          \
         have = false;                                                                              \
         if constexpr (STATS) ++st[0];                                                              \

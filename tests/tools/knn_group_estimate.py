@@ -36,7 +36,7 @@ def groups_of(q, size=GSIZE):
         return [q]
     ax = np.argmax(q.max(0) - q.min(0))
     q = q[np.argsort(q[:, ax], kind="stable")]
-    h = (len(q) // 2) // 8 * 8
+    h = (len(q) // 2) // size * size
     return groups_of(q[:h], size) + groups_of(q[h:], size)
 
 
