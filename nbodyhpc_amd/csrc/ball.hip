@@ -60,30 +60,16 @@ __device__ __forceinline__ float box_ub2(float qx, float qy, float qz, const flo
 // (r03g): spills that stay in L2 cost less than the lost occupancy
 constexpr int BALL_OCC[2][2] = {{8, 8}, {8, 8}};
 
-template <bool PER, bool FILL>
-__global__ void __launch_bounds__(TB, BALL_OCC[PER][FILL])
-ball_packet_kernel(DevTree t, const uint32_t *__restrict__ linfo, const float *__restrict__ q,
-                   const uint32_t *__restrict__ order, uint32_t m, float r2, PadLeaves pad,
-                   uint32_t *__restrict__ out_count, const uint64_t *__restrict__ row_offsets,
-                   uint32_t *__restrict__ out_idx, uint32_t tnum, bool plain_ok) {
-    __shared__ BallLds Wl[WPB];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    BallLds &W = Wl[wave];
-    const uint32_t gq = (xcd_block(blockIdx.x, gridDim.x) * WPB + wave) * 64u + lane;
-    const bool valid = gq < m;
-    const uint32_t qo = valid ? order[gq] : 0u;
-    const float qx = valid ? q[3 * (size_t)qo] : 0.0f;
-    const float qy = valid ? q[3 * (size_t)qo + 1] : 0.0f;
-    const float qz = valid ? q[3 * (size_t)qo + 2] : 0.0f;
+// the packet's walk and leaf scans (M: the metric's formulas, plain for a
+// packet whose balls all clear the box faces, ball_packet_kernel)
+template <bool PER, bool M, bool FILL>
+__device__ __forceinline__ void ball_walk(const DevTree &t, const uint32_t *__restrict__ linfo,
+                                          float r2, const PadLeaves &pad,
+                                          uint32_t *__restrict__ out_idx, uint32_t tnum,
+                                          bool plain_ok, BallLds &W, const int lane,
+                                          const float qx, const float qy, const float qz,
+                                          const float thr, const uint64_t wpos, uint32_t &cnt) {
     const float L = t.box;
-    const bool inside =
-        !PER || (qx >= 0.0f && qx <= L && qy >= 0.0f && qy <= L && qz >= 0.0f && qz <= L);
-    const bool active = valid && inside;
-    const float thr = active ? r2 : -INFINITY;
-    uint64_t wpos = (FILL && active) ? row_offsets[qo] : 0;
-    uint32_t cnt = 0;
-    if constexpr (!FILL) W.qs[lane] = make_float4(qx, qy, qz, 0.0f);
-
     uint32_t sk_node = 0;
     int sp = 0;
     const cnode_ptr cnodes = (cnode_ptr)t.nodes;
@@ -95,13 +81,13 @@ ball_packet_kernel(DevTree t, const uint32_t *__restrict__ linfo, const float *_
         bx[2 * a] = PER ? 0.0f : -FLT_MAX;
         bx[2 * a + 1] = PER ? L : FLT_MAX;
     }
-    float tm[3] = {box_lb_axis<PER>(qx, bx[0], bx[1], L), box_lb_axis<PER>(qy, bx[2], bx[3], L),
-                   box_lb_axis<PER>(qz, bx[4], bx[5], L)};
+    float tm[3] = {box_lb_axis<M>(qx, bx[0], bx[1], L), box_lb_axis<M>(qy, bx[2], bx[3], L),
+                   box_lb_axis<M>(qz, bx[4], bx[5], L)};
     uint64_t wm = __ballot((tm[0] + tm[1]) + tm[2] <= thr);
     bool have = wm != 0;
     nbkd_node nd = cnodes[0]; // record of `node` while `have`
     // the shared packet walk (packet.hpp: per-axis steps, node-id stack)
-    constexpr bool M = PER, STATS = false;
+    constexpr bool STATS = false;
     const float kth = thr;
     uint64_t st[1] = {0};
     (void)st;
@@ -117,7 +103,7 @@ ball_packet_kernel(DevTree t, const uint32_t *__restrict__ linfo, const float *_
         const float tb[6] = {rdlane(__uint_as_float(iw), 0), rdlane(__uint_as_float(iw), 3),
                              rdlane(__uint_as_float(iw), 1), rdlane(__uint_as_float(iw), 4),
                              rdlane(__uint_as_float(iw), 2), rdlane(__uint_as_float(iw), 5)};
-        const bool need = box_lb2<PER>(qx, qy, qz, tb, L) <= thr;
+        const bool need = box_lb2<M>(qx, qy, qz, tb, L) <= thr;
         if (!__any(need)) continue;
         // a leaf holding padding points (FLT_MAX, never inside) is always evaluated
         bool padded = false;
@@ -160,7 +146,7 @@ ball_packet_kernel(DevTree t, const uint32_t *__restrict__ linfo, const float *_
                     uint64_t rem = pm;
                     // periodic leaves no partial query wraps around: the plain d2
                     // has the same bits (wrap_free), 8 VALU instead of 14 a step
-                    if (!PER || (plain_ok && __all(!part || wrap_free(qx, qy, qz, tb, L)))) {
+                    if (!M || (plain_ok && __all(!part || wrap_free(qx, qy, qz, tb, L)))) {
                         while (rem) {
                             const int j = __builtin_ctzll(rem);
                             rem &= rem - 1;
@@ -174,7 +160,7 @@ ball_packet_kernel(DevTree t, const uint32_t *__restrict__ linfo, const float *_
                             const int j = __builtin_ctzll(rem);
                             rem &= rem - 1;
                             const float4 sq = W.qs[j]; // LDS broadcast
-                            const float d = point_d2_fast<PER>(sq.x, sq.y, sq.z, px, py, pz, L);
+                            const float d = point_d2_fast<M>(sq.x, sq.y, sq.z, px, py, pz, L);
                             const uint32_t c = (uint32_t)__popcll(__ballot(pv && d <= r2));
                             cnt += lane == j ? c : 0u;
                         }
@@ -186,7 +172,7 @@ ball_packet_kernel(DevTree t, const uint32_t *__restrict__ linfo, const float *_
 #pragma unroll 2
                 for (uint32_t u = 0; u < cn; ++u) {
                     const float4 a = W.p4[u];
-                    if (point_d2_fast<PER>(qx, qy, qz, a.x, a.y, a.z, L) <= thr) {
+                    if (point_d2_fast<M>(qx, qy, qz, a.x, a.y, a.z, L) <= thr) {
                         if constexpr (FILL) out_idx[wpos + cnt] = __float_as_uint(a.w);
                         ++cnt;
                     }
@@ -194,6 +180,49 @@ ball_packet_kernel(DevTree t, const uint32_t *__restrict__ linfo, const float *_
             }
         }
     }
+}
+
+template <bool PER, bool FILL>
+__global__ void __launch_bounds__(TB, BALL_OCC[PER][FILL])
+ball_packet_kernel(DevTree t, const uint32_t *__restrict__ linfo, const float *__restrict__ q,
+                   const uint32_t *__restrict__ order, uint32_t m, float r2, PadLeaves pad,
+                   uint32_t *__restrict__ out_count, const uint64_t *__restrict__ row_offsets,
+                   uint32_t *__restrict__ out_idx, uint32_t tnum, bool plain_ok) {
+    __shared__ BallLds Wl[WPB];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    BallLds &W = Wl[wave];
+    const uint32_t gq = (xcd_block(blockIdx.x, gridDim.x) * WPB + wave) * 64u + lane;
+    const bool valid = gq < m;
+    const uint32_t qo = valid ? order[gq] : 0u;
+    const float qx = valid ? q[3 * (size_t)qo] : 0.0f;
+    const float qy = valid ? q[3 * (size_t)qo + 1] : 0.0f;
+    const float qz = valid ? q[3 * (size_t)qo + 2] : 0.0f;
+    const float L = t.box;
+    const bool inside =
+        !PER || (qx >= 0.0f && qx <= L && qy >= 0.0f && qy <= L && qz >= 0.0f && qz <= L);
+    const bool active = valid && inside;
+    const float thr = active ? r2 : -INFINITY;
+    const uint64_t wpos = (FILL && active) ? row_offsets[qo] : 0;
+    uint32_t cnt = 0;
+    if constexpr (!FILL) W.qs[lane] = make_float4(qx, qy, qz, 0.0f);
+
+    // every active lane's ball clears the box faces by a margin r' > r: the
+    // plain formulas then give the periodic ones' bits for every point within
+    // r and fail the test for every point beyond (knn_collect.hip
+    // collect_packet), so the packet walks and counts with them
+    bool plain = false;
+    if constexpr (PER) {
+        const float r1 = sqrtf(fmaxf(r2, 0.0f)) * 1.01f + L * 1e-6f;
+        const bool wf = !active || (r1 <= 0.25f * L && qx >= r1 && L - qx >= r1 && qy >= r1 &&
+                                    L - qy >= r1 && qz >= r1 && L - qz >= r1);
+        plain = plain_ok && __all(wf);
+    }
+    if (plain)
+        ball_walk<PER, false, FILL>(t, linfo, r2, pad, out_idx, tnum, plain_ok, W, lane, qx, qy, qz,
+                                    thr, wpos, cnt);
+    else
+        ball_walk<PER, PER, FILL>(t, linfo, r2, pad, out_idx, tnum, plain_ok, W, lane, qx, qy, qz,
+                                  thr, wpos, cnt);
     if (active && out_count) out_count[qo] = cnt;
 }
 

@@ -27,7 +27,6 @@
 // A query whose ball holds fewer than k points (seed too small) or more than
 // the column capacity is listed for the reference-exact kernel (query.hip).
 #include <algorithm>
-#include <type_traits>
 
 #include "internal.hpp"
 #include "metric.hpp"
@@ -77,11 +76,16 @@ __device__ __forceinline__ uint32_t d2_bucket(float d, float c) {
 // hinfo) before staging it, so chunks no lane reaches skip the staging and its
 // wait: collect 54.0 -> 54.2 ms (r02as; few staged chunks are unreached).
 //
-// Tried and dropped: running packets whose balls clear the box faces with the
-// non-periodic formulas (4 % fewer VALU instructions).  One kernel holding
-// both variants spills VGPRs at the 8-wave budget; two launches leave the
-// wrap packets (~4 %) as a latency-bound tail (+10.9 ms at 1e8), or, on a side
-// stream beside the main launch, still cost +5 ms (r02f/r02g).
+// Packets whose seed balls all clear the box faces walk with the plain
+// (non-periodic) formulas (collect_packet): round 4, one kernel holding both
+// instances of grp_packet at 56 VGPRs without spills, collect 46.95 -> 44.01
+// ms per 1e8 queries, same rows (profiles/r04t_ab_packet_plain.txt).  In
+// round 2 the same kernel spilled VGPRs at the 8-wave budget, and two launches
+// left the wrap packets (~4 %) as a latency-bound tail (+10.9 ms), or, on a
+// side stream beside the main launch, still cost +5 ms (r02f/r02g).  Round 3
+// tried the plain formulas per chunk instead (the needing lanes within L/2
+// of the chunk's tight box): slower (r03_ab1), and again on top of the packet
+// switch in round 4 (44.01 -> 44.21 ms, r04t).
 //
 constexpr int GCHUNK = 64; // points staged per step (a multiple of NBKD_GROUP)
 constexpr int GMAX = GCHUNK / NBKD_GROUP;
@@ -221,82 +225,66 @@ __device__ __forceinline__ void grp_packet(const DevTree &t, const float *__rest
                     W.scl[r] = nb_over_s;
                 }
                 wave_sync();
-#if defined(NBKD_CPLAIN)
-                // every needing lane's ball box lies within L/2 of its query on
-                // every axis (wrap_free): the plain d2 and box bounds have the
-                // periodic ones' bits for the chunk's points (8 VALU a pair
-                // instead of 14)
-                const bool plain = M && __all(!need || wrap_free(qx, qy, qz, tb, L));
-#else
-                constexpr bool plain = false;
-#endif
+                // (needing lane, group) box tests, 8 lanes per needing lane (one
+                // per group); the groups reached become the pair list, entries
+                // slot | owner lane << 6 | group << 12
+                uint32_t np = 0;
+                const uint32_t ntest = nneed * GMAX;
+#pragma unroll 1
+                for (uint32_t t0 = 0; t0 < ntest; t0 += 64) {
+                    const uint32_t ti = t0 + lane;
+                    const uint32_t g = ti % GMAX;
+                    const uint32_t sl = ti / GMAX;
+                    uint32_t owner = 0;
+                    bool hit = false;
+                    if (ti < ntest && g < ng) {
+                        owner = W.slot[sl];
+                        const float4 qq = W.sq[sl];
+                        const float gbx[6] = {W.gb[6 * g], W.gb[6 * g + 1], W.gb[6 * g + 2],
+                                              W.gb[6 * g + 3], W.gb[6 * g + 4], W.gb[6 * g + 5]};
+                        hit = box_lb2<M>(qq.x, qq.y, qq.z, gbx, L) <= qq.w;
+                    }
+                    const uint64_t hm = __ballot(hit);
+                    if (hit)
+                        W.pairs[np + mbcnt64(hm)] = (uint16_t)(sl | (owner << 6) | (g << 12));
+                    np += (uint32_t)__popcll(hm);
+                }
+                NBKD_PH(2);
+                wave_sync();
                 // Tried and dropped (r04s): the hit's column slot as the owner's
                 // count plus the hits below it in its run of lanes (the pair list
                 // is slot-major), with no returning LDS atomic and all of a step's
                 // LDS reads issued together: collect 46.7 -> 55.1 ms per 1e8
                 // queries (profiles/r04s_ab_seg_wide.txt); the 64-bit lane-mask
                 // arithmetic costs more issue than the atomics' waits.
-                auto scan_pairs = [&](auto mm) {
-                    constexpr bool MM = decltype(mm)::value;
-                    // (needing lane, group) box tests, 8 lanes per needing lane (one
-                    // per group); the groups reached become the pair list, entries
-                    // slot | owner lane << 6 | group << 12
-                    uint32_t np = 0;
-                    const uint32_t ntest = nneed * GMAX;
+                // each pair's 8 points spread over 8 consecutive lanes
+                const uint32_t ntrip = np * NBKD_GROUP;
+                if constexpr (STATS) st[5] += ntrip;
 #pragma unroll 1
-                    for (uint32_t t0 = 0; t0 < ntest; t0 += 64) {
-                        const uint32_t ti = t0 + lane;
-                        const uint32_t g = ti % GMAX;
-                        const uint32_t sl = ti / GMAX;
-                        uint32_t owner = 0;
-                        bool hit = false;
-                        if (ti < ntest && g < ng) {
-                            owner = W.slot[sl];
-                            const float4 qq = W.sq[sl];
-                            const float gbx[6] = {W.gb[6 * g], W.gb[6 * g + 1], W.gb[6 * g + 2],
-                                                  W.gb[6 * g + 3], W.gb[6 * g + 4], W.gb[6 * g + 5]};
-                            hit = box_lb2<MM>(qq.x, qq.y, qq.z, gbx, L) <= qq.w;
-                        }
-                        const uint64_t hm = __ballot(hit);
-                        if (hit)
-                            W.pairs[np + mbcnt64(hm)] = (uint16_t)(sl | (owner << 6) | (g << 12));
-                        np += (uint32_t)__popcll(hm);
-                    }
-                    NBKD_PH(2);
-                    wave_sync();
-                    // each pair's 8 points spread over 8 consecutive lanes
-                    const uint32_t ntrip = np * NBKD_GROUP;
-                    if constexpr (STATS) st[5] += ntrip;
-#pragma unroll 1
-                    for (uint32_t t0 = 0; t0 < ntrip; t0 += 64) {
-                        if constexpr (STATS) ++st[4];
-                        const uint32_t ti = t0 + lane;
-                        if (ti < ntrip) {
-                            const uint32_t pr = W.pairs[ti / NBKD_GROUP];
-                            const uint32_t qs = pr & 63u, owner = (pr >> 6) & 63u;
-                            const uint32_t pi = (pr >> 12) * NBKD_GROUP + (ti % NBKD_GROUP);
-                            const float4 qq = W.sq[qs];
-                            const float4 pp = W.p4[pi];
-                            const float d = point_d2_fast<MM>(qq.x, qq.y, qq.z, pp.x, pp.y, pp.z, L);
-                            if (d < qq.w) {
-                                const uint32_t j = d2_bucket(d, W.scl[qs]);
-                                atomicAdd(&W.hist[j >> 2][owner], 1u << (8 * (j & 3)));
-                                const uint32_t sl = atomicAdd(&W.cnt[owner], 1u);
-                                // a row past capg is a failure whose column is never read (both
-                                // selects): its extra hits overwrite its last slot (no branch)
-                                const uint32_t sw = min(sl, capg - 1u);
-                                // the candidate carries the point's original id (p4.w):
-                                // the selects write it without a gather
-                                col[((sw >> 4) * qpp + owner) * 16u + (sw & 15u)] =
-                                    make_uint2(__float_as_uint(d), __float_as_uint(pp.w));
-                            }
+                for (uint32_t t0 = 0; t0 < ntrip; t0 += 64) {
+                    if constexpr (STATS) ++st[4];
+                    const uint32_t ti = t0 + lane;
+                    if (ti < ntrip) {
+                        const uint32_t pr = W.pairs[ti / NBKD_GROUP];
+                        const uint32_t qs = pr & 63u, owner = (pr >> 6) & 63u;
+                        const uint32_t pi = (pr >> 12) * NBKD_GROUP + (ti % NBKD_GROUP);
+                        const float4 qq = W.sq[qs];
+                        const float4 pp = W.p4[pi];
+                        const float d = point_d2_fast<M>(qq.x, qq.y, qq.z, pp.x, pp.y, pp.z, L);
+                        if (d < qq.w) {
+                            const uint32_t j = d2_bucket(d, W.scl[qs]);
+                            atomicAdd(&W.hist[j >> 2][owner], 1u << (8 * (j & 3)));
+                            const uint32_t sl = atomicAdd(&W.cnt[owner], 1u);
+                            // a row past capg is a failure whose column is never read (both
+                            // selects): its extra hits overwrite its last slot (no branch)
+                            const uint32_t sw = min(sl, capg - 1u);
+                            // the candidate carries the point's original id (p4.w):
+                            // the selects write it without a gather
+                            col[((sw >> 4) * qpp + owner) * 16u + (sw & 15u)] =
+                                make_uint2(__float_as_uint(d), __float_as_uint(pp.w));
                         }
                     }
-                };
-                if (plain)
-                    scan_pairs(std::false_type{});
-                else
-                    scan_pairs(std::integral_constant<bool, M>{});
+                }
                 wave_sync();
                 cnt = W.cnt[lane];
                 NBKD_PH(4);
@@ -369,7 +357,6 @@ __device__ __forceinline__ void collect_packet(
     uint32_t cnt = 0;
     uint64_t st[13] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     float kth = seed;
-#if defined(NBKD_PKT_PLAIN)
     // Every lane's seed ball clears the box faces (a margin r' > sqrt(seed) on
     // every axis): a point within the ball is then within L/2 of the query on
     // every axis, where the plain per-axis distance has the periodic minimum's
@@ -389,7 +376,6 @@ __device__ __forceinline__ void collect_packet(
         grp_packet<PER, false, STATS, AHEAD>(t, ginfo, linfo, hinfo, W, lane, qx, qy, qz, kth,
                                              s_over_nb, nb_over_s, col, qpp, capg, kq, cnt, st);
     else
-#endif
         grp_packet<PER, PER, STATS, AHEAD>(t, ginfo, linfo, hinfo, W, lane, qx, qy, qz, kth,
                                            s_over_nb, nb_over_s, col, qpp, capg, kq, cnt, st);
     if (valid) ccount[gq] = cnt;

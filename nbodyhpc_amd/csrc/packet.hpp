@@ -143,20 +143,6 @@ typedef const NodeBox *cbox_ptr;
 // cache; four times the bytes per record and 12 more live SGPRs (spilled
 // kernel arguments) cost more than the shorter chains save.
 //
-// Node loads of the walk.  NBKD_POPLOAD: a popped node's record is loaded
-// beside its cell box; the empty asm takes every word as an operand, so the
-// load is not sunk below the box test and both arrive after one scalar-load
-// latency.
-#if defined(NBKD_POPLOAD)
-#define NBKD_WALK_PREFETCH()                                                                       \
-    const nbkd_node wp_ = cnodes[node];                                                            \
-    asm volatile("" ::"s"(wp_.dimension), "s"(wp_.split), "s"(wp_.left), "s"(wp_.right));
-#define NBKD_WALK_TAKE() nd = wp_;
-#else
-#define NBKD_WALK_PREFETCH()
-#define NBKD_WALK_TAKE() nd = cnodes[node];
-#endif
-
 // one internal node with split axis D (compile-time): test both children for
 // every lane; a single wanted child is entered, and only when both are wanted
 // the lanes vote which one is near (entered) and which far (pushed, its seven
@@ -218,13 +204,12 @@ typedef const NodeBox *cbox_ptr;
                 const NodeBox nb_ = cboxes[node];                                                  \
                 _Pragma("unroll") for (int a = 0; a < 6; ++a) bx[a] = nb_.b[a];                    \
             }                                                                                      \
-            NBKD_WALK_PREFETCH();                                                                  \
             tm[0] = box_lb_axis<M>(qx, bx[0], bx[1], L);                                           \
             tm[1] = box_lb_axis<M>(qy, bx[2], bx[3], L);                                           \
             tm[2] = box_lb_axis<M>(qz, bx[4], bx[5], L);                                           \
             wm = __ballot((tm[0] + tm[1]) + tm[2] <= kth);                                         \
             if (wm == 0) continue;                                                                 \
-            NBKD_WALK_TAKE();                                                                      \
+            nd = cnodes[node];                                                                     \
         }                                                                                          \
         have = false;                                                                              \
         if constexpr (STATS) ++st[0];                                                              \
