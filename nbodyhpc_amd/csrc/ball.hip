@@ -189,6 +189,8 @@ ball_packet_kernel(DevTree t, const uint32_t *__restrict__ linfo, const float *_
                    uint32_t *__restrict__ out_count, const uint64_t *__restrict__ row_offsets,
                    uint32_t *__restrict__ out_idx, uint32_t tnum, bool plain_ok) {
     __shared__ BallLds Wl[WPB];
+    // (threadIdx.x >> 6 as is: the wave-uniform wave_id() made this kernel slower,
+    // 100.6 -> 104.7 ms at 1e8, profiles/r04v_ab_uniform_wave.txt)
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     BallLds &W = Wl[wave];
     const uint32_t gq = (xcd_block(blockIdx.x, gridDim.x) * WPB + wave) * 64u + lane;

@@ -123,7 +123,7 @@ __device__ __forceinline__ void grp_packet(const DevTree &t, const float *__rest
                                            const float s_over_nb, const float nb_over_s,
                                            uint2 *__restrict__ col, const uint32_t qpp,
                                            const uint32_t capg, const int kq, uint32_t &cnt,
-                                           uint64_t (&st)[13]) {
+                                           uint32_t (&st)[13]) {
     const float L = t.box;
     uint32_t last_cnt = 0;
     uint32_t sk_node = 0;
@@ -147,7 +147,7 @@ __device__ __forceinline__ void grp_packet(const DevTree &t, const float *__rest
     do {                                                                                           \
         if constexpr (STATS) {                                                                     \
             const uint64_t t_ = clock64();                                                         \
-            st[6 + (I)] += t_ - tclk;                                                              \
+            st[6 + (I)] += (uint32_t)(t_ - tclk);                                                              \
             tclk = t_;                                                                             \
         }                                                                                          \
     } while (0)
@@ -280,7 +280,10 @@ __device__ __forceinline__ void grp_packet(const DevTree &t, const float *__rest
                             const uint32_t sw = min(sl, capg - 1u);
                             // the candidate carries the point's original id (p4.w):
                             // the selects write it without a gather
-                            col[((sw >> 4) * qpp + owner) * 16u + (sw & 15u)] =
+                            // a 32-bit byte offset from the packet's (SGPR) column base:
+                            // one saddr store, no 64-bit address arithmetic per hit
+                            const uint32_t off = (((__umul24(sw >> 4, qpp) + owner) << 4) | (sw & 15u)) << 3;
+                            *reinterpret_cast<uint2 *>(reinterpret_cast<char *>(col) + off) =
                                 make_uint2(__float_as_uint(d), __float_as_uint(pp.w));
                         }
                     }
@@ -355,7 +358,9 @@ __device__ __forceinline__ void collect_packet(
     for (int w = 0; w < NB / 4; ++w) W.hist[w][lane] = 0u;
     uint2 *const col = cand + (size_t)pk * qpp * capg;
     uint32_t cnt = 0;
-    uint64_t st[13] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    // per-packet work counters and phase clocks (STATS only): 32 bits each, so
+    // the instrumented instance keeps them in SGPRs without spilling
+    uint32_t st[13] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     float kth = seed;
     // Every lane's seed ball clears the box faces (a margin r' > sqrt(seed) on
     // every axis): a point within the ball is then within L/2 of the query on
@@ -416,7 +421,7 @@ knn_collect_grp_kernel(DevTree t, const float *__restrict__ ginfo,
                        uint32_t *__restrict__ ccount, unsigned long long *__restrict__ stats,
                        bool xcd, float *__restrict__ kbound) {
     __shared__ CollectLdsG Wl[WPB];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, wave = wave_id();
     CollectLdsG &W = Wl[wave];
     const uint32_t m = span_m(span);
     const uint32_t npk = (m + qpp - 1) / qpp;
@@ -482,7 +487,7 @@ knn_select_kernel(DevTree t, const float *__restrict__ q, const uint32_t *__rest
     constexpr int SW = CC < 32 ? 32 * 64 : CC * 64; // >= 8 KB: one candidate block
     __shared__ uint32_t stage_all[WPB][SW];
     __shared__ uint32_t rowq_all[WPB][64];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, wave = wave_id();
     uint32_t *stage = stage_all[wave], *rowq = rowq_all[wave];
     // a device-counted pass (retry rounds) is launched for its cap and reads
     // its count here (a loop over blocks made the compiler spill td / ti)
@@ -735,7 +740,7 @@ knn_select_wave_kernel(DevTree t, const float *__restrict__ q, const uint32_t *_
     // per wave: the query's candidates below its final bound, compacted
     __shared__ uint2 cl_all[WPB][2 * K];
     const int lane = threadIdx.x & 63;
-    uint2 *const cl = cl_all[threadIdx.x >> 6];
+    uint2 *const cl = cl_all[wave_id()];
     const uint32_t m = span_m(span);
     const uint32_t nwaves = gridDim.x * WPB;
     // software pipeline: the next query's count, bound and first 2K slots are
@@ -746,7 +751,7 @@ knn_select_wave_kernel(DevTree t, const float *__restrict__ q, const uint32_t *_
         return WHOLE ? cand + (size_t)(g >> 6) * 64u * capg + ((c >> 4) * 64u + (g & 63u)) * 16u + (c & 15u)
                      : cand + (size_t)g * capg + c;
     };
-    uint32_t gq = blockIdx.x * WPB + (threadIdx.x >> 6);
+    uint32_t gq = blockIdx.x * WPB + wave_id();
     uint32_t n_nx = 0, qo_nx = 0;
     float b_nx = INFINITY;
     uint2 e_nx[2 * R];

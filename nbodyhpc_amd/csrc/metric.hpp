@@ -15,6 +15,11 @@ __device__ __forceinline__ uint32_t mbcnt64(uint64_t mask) {
 
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
+// the wave's index in its block, as a wave-uniform (SGPR) value: the compiler
+// does not know threadIdx.x >> 6 is uniform, and everything derived from it
+// (packet ids, column and LDS bases) would otherwise live in VGPRs
+__device__ __forceinline__ int wave_id() { return (int)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
+
 // Workgroups are dealt round-robin over the 8 XCDs (observed, not promised:
 // MI355X_MICROARCH.md "Workgroup dispatch, XCD placement").  This bijection of
 // [0, nb) gives each XCD a contiguous range of logical blocks instead, so
