@@ -95,7 +95,12 @@ __device__ __forceinline__ float guess_r2(uint32_t count, const float lo[3], con
 // Bucketing descent over the blocked heap of splits (internal.hpp hblk_*,
 // build.hip heap_splits_kernel): same turns, same leaf key and seed as
 // leaf_key2_kernel, one 64-B line (4 levels) per load instead of one dependent
-// load per level.
+// load per level.  The kernel keeps the texture addresser ~80 % busy with
+// these divergent 16-B gathers (profiles/r04w_pmc_sq_tcc.txt), but fewer of
+// them cost more in latency than they save: reading a line's last quarter
+// only after the first three levels' turns (3 gathers a line) 3.15 -> 3.59 ms,
+// block levels 0 and 1 from LDS 3.86 ms, both 3.73 ms at 1e8
+// (profiles/r04x_ab_leaf_key.txt).
 __global__ void __launch_bounds__(TB)
 leaf_key3_kernel(const float4 *__restrict__ hb, int o, uint32_t n8, uint32_t leaf,
                  const float *__restrict__ q, uint32_t m, uint32_t *__restrict__ keys,
