@@ -89,6 +89,23 @@ def pmc_traffic(n_particles, k, q_per_launch, kind="knn"):
     return None, None
 
 
+def pmc_step_traffic(n_particles, k):
+    """(HBM bytes of one whole kNN step, source file) from a committed
+    profiles/r*_pmc_step.json (scripts/step_traffic.sh + summarize_step.py:
+    every kernel of the query, the build and warmup differenced out) measured
+    with this very library build, or (None, None)."""
+    import glob
+    sha = lib_sha256()
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_step.json"))):
+        try:
+            pm = json.load(open(path))
+        except Exception:
+            continue
+        if pm.get("lib_sha256") == sha and pm.get("n_particles") == n_particles and pm.get("k") == k:
+            return pm.get("hbm_bytes_per_step"), os.path.relpath(path, ROOT)
+    return None, None
+
+
 def roofline_entry(traffic, traffic_source, kernel_ms, work_achieved, **extra):
     """The roofline object of one kernel.  `achieved` / `frac` are HBM
     bandwidth as the counters see it: HBM bytes per launch (rocprofv3 PMC of
@@ -910,6 +927,10 @@ def main():
     # x2 (gfx950) + WRITE_SIZE, separate runs) whose recorded libnbkd.so SHA-256
     # equals the loaded library's, for the same workload; else null
     traffic, traffic_source = pmc_traffic(own, k, q_per_launch)
+    # the whole step's HBM bytes (every kernel of the query), same build, one GPU
+    step_traffic, step_source = pmc_step_traffic(own, k) if world == 1 else (None, None)
+    step_sec = elapsed_max / args.steps
+    step_ach = None if step_traffic is None else step_traffic / step_sec / 1e9
     extra = None
     if world == 1 and args.suite:
         extra = suite(args, capi, hip, tree, dev_pts, n, k, L, stream, od, oi)
@@ -953,7 +974,12 @@ def main():
             kernel="knn_collect_grp_kernel<periodic> (nbodyhpc_amd/csrc/knn_collect.hip)",
             step_work_frac=value * bq / (HBM_PEAK_GBS * 1e9 * world),
             launches_per_step=col_launches / args.steps, queries_per_launch=q_per_launch,
-            bytes_per_query=bq),
+            bytes_per_query=bq,
+            # the whole pipeline (bucketing, sort, collect, select, retries):
+            # PMC HBM bytes of one step / the step's wall time
+            step_traffic=step_traffic, step_traffic_source=step_source,
+            step_achieved=step_ach,
+            step_frac=None if step_ach is None else step_ach / HBM_PEAK_GBS),
         "breakdown_ms_per_step": {
             "leaf_key": key_ms / args.steps, "sort": sort_ms / args.steps,
             "knn": knn_ms / args.steps, "knn_collect": col_ms / args.steps,

@@ -77,3 +77,27 @@ def test_gpus_n_with_fewer_gpus_fails_cleanly():
     rc, lines, err = _run_bench(["--gpus", "2", "--steps", "1", "--warmup", "0"])
     assert rc != 0 and not lines
     assert "GPU(s) visible" in err
+
+
+def test_pmc_lookups_match_the_library_sha(tmp_path, monkeypatch):
+    """roofline.traffic / step_traffic come only from a PMC summary whose
+    lib_sha256 is the loaded library's (no GPU: the lookups read files)."""
+    import importlib.util
+    import json
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    prof = tmp_path / "profiles"
+    prof.mkdir()
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    monkeypatch.setattr(bench, "lib_sha256", lambda: "abc")
+    json.dump({"lib_sha256": "abc", "n_particles": 100, "k": 32, "hbm_bytes_per_step": 7.0},
+              open(prof / "r99_pmc_step.json", "w"))
+    json.dump({"lib_sha256": "zzz", "n_particles": 100, "k": 32, "hbm_bytes_per_step": 9.0},
+              open(prof / "r98_pmc_step.json", "w"))
+    assert bench.pmc_step_traffic(100, 32) == (7.0, "profiles/r99_pmc_step.json")
+    assert bench.pmc_step_traffic(100, 16) == (None, None)
+    monkeypatch.setattr(bench, "lib_sha256", lambda: "other")
+    assert bench.pmc_step_traffic(100, 32) == (None, None)
+    r = bench.roofline_entry(8e9, "x", 2.0, 1000.0, step_traffic=1.0)
+    assert abs(r["frac"] - 8e9 / 2e-3 / 1e9 / 8000.0) < 1e-12 and r["frac"] <= 1.0
