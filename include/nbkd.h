@@ -148,7 +148,7 @@ void nbkd_free(nbkd_tree *tree);
  *                      (default 3.5; > 0).  Results never depend on it: a query
  *                      whose seed ball holds fewer than k points is re-walked.
  *   "candidate_bytes"  HBM budget of one collect / select batch's candidate
- *                      columns (default 0 = min(24 GiB, free / 4)).
+ *                      columns (default 0 = min(96 GiB, free / 3)).
  *   "host_batch"       queries per batch of a host-buffer call (default 0 =
  *                      about 1 GiB of queries plus results per batch).
  * NEW (no reference counterpart: kdtree/src/cpp/pybind.cpp:196-216 has no knobs). */

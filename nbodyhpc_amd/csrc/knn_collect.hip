@@ -196,6 +196,10 @@ __device__ __forceinline__ void grp_packet(const DevTree &t, const float *__rest
             node_next = node;
             NBKD_PH(0);
         }
+        // Tried and dropped (r04aa): pulling the next leaf's lines (points,
+        // group boxes, tight box) toward L2 here with one 4-B direct-to-LDS
+        // load per line, waiting vmcnt(1) for this leaf's staging only:
+        // collect 43.68 -> 46.97 ms per 1e8 (profiles/r04aa_ab_prefetch_anchor.txt)
         wait_vm0();
         wave_sync();
         NBKD_PH(1);

@@ -894,20 +894,23 @@ nbkd_status stage_queries(Workspace &ws, const float *q, uint64_t m, uint32_t fl
 } // namespace
 
 // Candidate-column budget per collect/select batch: NBKD_CAND_BYTES, else the
-// smaller of 24 GiB and a quarter of the free device memory.  Fewer, larger
+// smaller of 96 GiB and a third of the free device memory.  Fewer, larger
 // batches shorten the per-launch tails: 9 batches of 11 M queries (8 GiB) ->
-// 3 at 1e8 is 53.9 -> 51.5 ms of collect (r02at).
+// 3 at 1e8 is 53.9 -> 51.5 ms of collect (r02at); 3 (24 GiB, the cap until
+// round 4) -> 1 (80 GiB) is 65.05 -> 63.95 ms per step
+// (profiles/r04z_ab_budget_anchor.txt).  A 1e8 query on an otherwise empty
+// MI355X (288 GB) now takes one batch of 77 GB of columns.
 uint64_t cand_budget() {
     const char *eb = knob("NBKD_CAND_BYTES");
     if (eb) return strtoull(eb, nullptr, 10);
     const double tb = tuning(TUNE_CAND_BYTES); // nbkd_set_tuning("candidate_bytes"), 0 = auto
     if (tb > 0.0) return (uint64_t)tb;
     size_t free_b = 0, total_b = 0;
-    uint64_t b = 24ull << 30;
+    uint64_t b = 96ull << 30;
     if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b > 0)
-        // a quarter of the free memory, never more than what is free (the
+        // a third of the free memory, never more than what is free (the
         // callers' minimum is one 64-query packet's column)
-        b = std::min<uint64_t>(b, free_b / 4);
+        b = std::min<uint64_t>(b, free_b / 3);
     else
         (void)hipGetLastError();
     return b;
