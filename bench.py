@@ -81,10 +81,14 @@ def pmc_traffic(n_particles, k, q_per_launch, kind="knn"):
             pm = json.load(open(path))
         except Exception:
             continue
-        if (pm.get("lib_sha256") == sha and pm.get("n_particles") == n_particles
-                and pm.get("k") == k and str(pm.get("kernel", "")).startswith("knn_collect")
-                and abs(float(pm.get("queries_per_launch") or 0) - q_per_launch)
-                <= 1e-9 * q_per_launch):
+        if (pm.get("lib_sha256") != sha or pm.get("n_particles") != n_particles
+                or pm.get("k") != k or not str(pm.get("kernel", "")).startswith("knn_collect")):
+            continue
+        # per-query HBM bytes over every first-pass launch of the PMC runs x this
+        # run's queries per launch (the batch split follows the free memory)
+        if pm.get("hbm_bytes_per_query"):
+            return pm["hbm_bytes_per_query"] * q_per_launch, os.path.relpath(path, ROOT)
+        if abs(float(pm.get("queries_per_launch") or 0) - q_per_launch) <= 1e-9 * q_per_launch:
             return pm.get("hbm_bytes_per_launch"), os.path.relpath(path, ROOT)
     return None, None
 

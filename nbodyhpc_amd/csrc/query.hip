@@ -1002,7 +1002,10 @@ nbkd_status knn_locked(const Tree &t, Workspace &ws, const float *q, uint64_t m,
         if (tg && !collect_disabled()) {
             // collect + select in batches sized to the candidate-column budget
             const uint32_t capg = collect_capacity(k);
-            const uint64_t budget = cand_budget();
+            // the columns this workspace already holds count as budget: free
+            // memory no longer includes them, and a second call of the same
+            // size must split the same way as the first (one batch at 1e8)
+            const uint64_t budget = std::max<uint64_t>(cand_budget(), ws.cap[WS_CAND]);
             uint64_t batch = budget / ((uint64_t)capg * 8u) / 64u * 64u;
             batch = std::max<uint64_t>(batch, 64);
             batch = std::min<uint64_t>(batch, ((uint64_t)mm + 63) / 64 * 64);

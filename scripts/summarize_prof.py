@@ -59,6 +59,29 @@ def per_dispatch(path, regex):
     return [v for kk, v in vals.items() if grid[kk] == gmax]
 
 
+def per_query(path, regex):
+    """(counter sum, grid sum) over the first-pass launches of the kernel: the
+    production instance (not STATS, not the LOOP retry instance), grids of at
+    least 1 M threads (one query per thread).  The launch split depends on the
+    free memory at the call, so bytes are kept per query."""
+    vals, grid = {}, {}
+    with open(path) as f:
+        for row in csv.DictReader(f):
+            name = row["Kernel_Name"]
+            if regex not in name or _stats_instance(name):
+                continue
+            if "knn_collect_grp_kernel<" in name:
+                args = name.split("knn_collect_grp_kernel<", 1)[1].split(">", 1)[0].split(",")
+                if len(args) >= 4 and args[3].strip() == "true":  # LOOP: retry rounds
+                    continue
+            if int(row["Grid_Size"]) < (1 << 20):
+                continue
+            key = row["Dispatch_Id"]
+            vals[key] = vals.get(key, 0.0) + float(row["Counter_Value"])
+            grid[key] = int(row["Grid_Size"])
+    return sum(vals.values()), sum(grid.values())
+
+
 def main():
     src, tag = sys.argv[1], sys.argv[2]
     regex = sys.argv[3] if len(sys.argv) > 3 else "knn_collect"
@@ -99,6 +122,9 @@ def main():
         f_kib = sum(fv) / len(fv)
         w_kib = sum(wv) / len(wv)
         hbm = 2.0 * 1024.0 * f_kib + 1024.0 * w_kib
+        fs, fg = per_query(fetch, regex)
+        ws_, wg = per_query(write, regex)
+        bpq = (2.0 * 1024.0 * fs / fg + 1024.0 * ws_ / wg) if fg and wg else None
         cfg = (b or {}).get("config", {})
         shaf = os.path.join(src, "lib.sha256")
         lib_sha = open(shaf).read().split()[0] if os.path.exists(shaf) else None
@@ -116,6 +142,10 @@ def main():
             "fetch_bytes_per_launch_corrected": 2.0 * 1024.0 * f_kib,
             "write_bytes_per_launch": 1024.0 * w_kib,
             "hbm_bytes_per_launch": hbm,
+            # over every first-pass launch of the runs (any batch split): bench.py
+            # multiplies it by the queries of its own launches
+            "hbm_bytes_per_query": bpq,
+            "queries_in_passes": [fg, wg],
             "note": "FETCH_SIZE doubled, WRITE_SIZE as reported (calibration: "
                     "profiles/r04a_pmc_calibration.json); Infinity-Cache hits are counted "
                     "by these counters, not excluded",
