@@ -900,11 +900,13 @@ nbkd_status stage_queries(Workspace &ws, const float *q, uint64_t m, uint32_t fl
 // round 4) -> 1 (80 GiB) is 65.05 -> 63.95 ms per step
 // (profiles/r04z_ab_budget_anchor.txt).  A 1e8 query on an otherwise empty
 // MI355X (288 GB) now takes one batch of 77 GB of columns.
-uint64_t cand_budget() {
+uint64_t cand_budget(bool *is_auto) {
+    if (is_auto) *is_auto = false;
     const char *eb = knob("NBKD_CAND_BYTES");
     if (eb) return strtoull(eb, nullptr, 10);
     const double tb = tuning(TUNE_CAND_BYTES); // nbkd_set_tuning("candidate_bytes"), 0 = auto
     if (tb > 0.0) return (uint64_t)tb;
+    if (is_auto) *is_auto = true;
     size_t free_b = 0, total_b = 0;
     uint64_t b = 96ull << 30;
     if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b > 0)
@@ -1002,10 +1004,13 @@ nbkd_status knn_locked(const Tree &t, Workspace &ws, const float *q, uint64_t m,
         if (tg && !collect_disabled()) {
             // collect + select in batches sized to the candidate-column budget
             const uint32_t capg = collect_capacity(k);
-            // the columns this workspace already holds count as budget: free
-            // memory no longer includes them, and a second call of the same
-            // size must split the same way as the first (one batch at 1e8)
-            const uint64_t budget = std::max<uint64_t>(cand_budget(), ws.cap[WS_CAND]);
+            // automatic budget: the columns this workspace already holds count
+            // too (free memory no longer includes them), so a second call of
+            // the same size splits the same way as the first (one batch at
+            // 1e8); an explicit candidate_bytes is taken as given
+            bool auto_budget = false;
+            uint64_t budget = cand_budget(&auto_budget);
+            if (auto_budget) budget = std::max<uint64_t>(budget, ws.cap[WS_CAND]);
             uint64_t batch = budget / ((uint64_t)capg * 8u) / 64u * 64u;
             batch = std::max<uint64_t>(batch, 64);
             batch = std::min<uint64_t>(batch, ((uint64_t)mm + 63) / 64 * 64);
