@@ -300,6 +300,10 @@ __device__ __forceinline__ void grp_packet(const DevTree &t, const float *__rest
             if (c0 >= lend) {
                 if constexpr (STATS) st[1] += any_leaf ? 1 : 0;
                 // tighten: smallest bucket edge with >= k candidates below it
+                // (after every leaf that added candidates; re-tightening only
+                // after 3 or 6 more was slower, 63.66 -> 64.00 / 63.98 ms per
+                // 1e8 step: the staler bound costs the select more than the
+                // skipped passes save, profiles/r04ag_ab_tighten_delta.txt)
                 const bool upd = cnt >= (uint32_t)kq && cnt != last_cnt;
                 if (__any(upd)) {
                     wave_sync();
