@@ -33,6 +33,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+PROFILES = os.path.join(ROOT, "profiles")  # the committed PMC summaries bench.py matches
 METRIC = "kNN queries/sec (k=32, 1e8 periodic particles)"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 # Algorithmic bytes per kNN query: B_q = 16*N + 12*P + 12 + 8k,
@@ -110,7 +111,56 @@ def pmc_step_traffic(n_particles, k):
     return None, None
 
 
-def roofline_entry(traffic, traffic_source, kernel_ms, work_achieved, **extra):
+def pmc_slab(args, world, k):
+    """N > 1: (entry, source) of a committed profiles/r*_pmc_slab.json measured
+    with this very library build for this decomposition, or (None, None).
+    Each entry is one rank's slab (own particles + halo) profiled alone on one
+    GPU by scripts/slab_traffic.sh (scripts/knn_time.py --slab-world N
+    --slab-rank r: the same points, halo and ids the bench's rank builds), with
+    the HBM bytes per own query of the collect kernel and of the whole step."""
+    import glob
+    sha = lib_sha256()
+    want = {"world": world, "scaling": args.scaling, "n_arg": int(args.n), "k": k,
+            "leafsize": args.leafsize, "seed": args.seed}
+    for path in sorted(glob.glob(os.path.join(PROFILES, "r*_pmc_slab.json"))):
+        try:
+            pm = json.load(open(path))
+        except Exception:
+            continue
+        if pm.get("lib_sha256") != sha:
+            continue
+        for e in pm.get("entries", []):
+            if all(e.get(kk) == v for kk, v in want.items()):
+                return e, os.path.relpath(path, ROOT)
+    return None, None
+
+
+def slab_roofline(ent, src, world, bq, q_per_launch, own, col_avg_ms, step_sec, allsum, allmax):
+    """The whole job's roofline terms at N > 1 (a collective: every rank calls
+    it).  Each rank's HBM bytes = its own queries x the bytes per own query of
+    its slab's profile (ent, same build and decomposition); the sums over the
+    ranks go over the slowest rank's collect launch / step time, against N x the
+    per-GPU peak.  Without a profile on every rank the traffic terms are None."""
+    have = allsum(1.0 if ent else 0.0) == world
+    col_max = allmax(col_avg_ms)
+    out = {"kernel_ms": col_max, "peak": HBM_PEAK_GBS * world,
+           "work_achieved": allsum(bq * q_per_launch) / (col_max * 1e-3) / 1e9,
+           "traffic": None, "step_traffic": None, "step_achieved": None, "source": None,
+           "basis": None}
+    if not have:
+        return out
+    out["traffic"] = allsum(ent["collect_bytes_per_query"] * q_per_launch)
+    out["step_traffic"] = allsum(ent["step_bytes_per_query"] * own)
+    out["step_achieved"] = out["step_traffic"] / step_sec / 1e9
+    out["source"] = src
+    out["basis"] = (f"sum over the {world} ranks of own queries x HBM bytes per own query of "
+                    f"rank {ent['rank']}'s slab (own + halo, {ent['n_local']} points) profiled "
+                    f"alone on one GPU (scripts/slab_traffic.sh), over the slowest rank's time, "
+                    f"against {world} x {HBM_PEAK_GBS:.0f} GB/s")
+    return out
+
+
+def roofline_entry(traffic, traffic_source, kernel_ms, work_achieved, peak=HBM_PEAK_GBS, **extra):
     """The roofline object of one kernel.  `achieved` / `frac` are HBM
     bandwidth as the counters see it: HBM bytes per launch (rocprofv3 PMC of
     THIS library build: FETCH_SIZE x2 + WRITE_SIZE, each scaled by the
@@ -122,11 +172,11 @@ def roofline_entry(traffic, traffic_source, kernel_ms, work_achieved, **extra):
     serves 64 queries of a packet."""
     sec = kernel_ms * 1e-3
     ach = None if traffic is None or sec <= 0 else traffic / sec / 1e9
-    out = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-           "frac": None if ach is None else ach / HBM_PEAK_GBS,
+    out = {"bound": "hbm", "achieved": ach, "peak": peak, "unit": "GB/s",
+           "frac": None if ach is None else ach / peak,
            "traffic": traffic, "traffic_source": traffic_source,
            "basis": "PMC HBM bytes per launch (calibrated) / HIP-event launch time",
-           "work_achieved": work_achieved, "work_frac": work_achieved / HBM_PEAK_GBS,
+           "work_achieved": work_achieved, "work_frac": work_achieved / peak,
            "kernel_ms_per_launch": kernel_ms}
     out.update(extra)
     return out
@@ -156,6 +206,8 @@ def parse():
     p.add_argument("--seed", type=int, default=20261015)
     p.add_argument("--cpu-sample", type=int, default=10_000_000,
                    help="queries timed on the CPU baseline (rank 0, N=1)")
+    p.add_argument("--cpu-threads", type=int, default=0,
+                   help="CPU baseline workers (default: every core this process may use)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-parity", action="store_true")
     p.add_argument("--suite", action="store_true",
@@ -199,18 +251,65 @@ def gen_uniform(n, seed, box):
     return out
 
 
-def cpu_baseline(points, k, leafsize, box, sample, gpu_d, gpu_i):
+# port / reference CPU speed ratios measured in the build container, where the
+# compiled reference exists (scripts/cpu_ratio.py -> profiles/r05_cpu_ratio.json,
+# 1e7 points, k = 32, periodic, leafsize 64, interleaved runs, medians): the
+# single-threaded build and the query rate at 1 and 8 threads
+CPU_RATIO_SOURCE = "profiles/r05_cpu_ratio.json"
+
+
+def cpu_ratio():
+    try:
+        r = json.load(open(os.path.join(ROOT, CPU_RATIO_SOURCE)))
+        return {"source": CPU_RATIO_SOURCE,
+                "build_time_port_over_reference": r["build_port_over_reference_time"],
+                "query_rate_port_over_reference": r["query_port_over_reference_rate"]}
+    except (OSError, KeyError, ValueError):
+        return None
+
+
+def host_cpus():
+    """The host cores this process may use: the affinity mask, capped by the
+    cgroup CPU quota (a GPU box shares its machine: nproc and os.cpu_count()
+    show every CPU of it), plus nproc and the CPU model for the report."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = os.cpu_count() or 1
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = float(q) / float(period)
+    except (OSError, ValueError):
+        pass
+    usable = max(1, min(aff, int(math.ceil(quota)) if quota else aff))
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"usable": usable, "nproc": os.cpu_count(), "affinity": aff, "cgroup_quota": quota,
+            "model": model}
+
+
+def cpu_baseline(points, k, leafsize, box, sample, gpu_d, gpu_i, threads=0):
     """The C restatement of the reference (oracle/liborc.so, pinned bit for bit to
     the reference's own compiled C++ by tests/test_oracle.py; same median-split
     tree, 8-wide leaf scan + loser tree, contiguous-block thread pool), timed on
-    this host's cores on a bounded sample.  The reference itself does not travel
-    to the GPU box; the port/reference speed ratio measured in
-    the build container is in BASELINE.md."""
+    this host's cores on a bounded sample: `threads` workers, by default every
+    core this process may use (host_cpus; BASELINE.md "workers = nproc").  The
+    reference itself does not travel to the GPU box; the
+    port/reference speed ratios measured in the build container are reported
+    beside it (cpu_ratio)."""
     from oracle.oracle import Oracle
     kind = "port"
     lib = Oracle()
-    cores = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
-    cores = max(1, min(cores, 64))
+    host = host_cpus()
+    cores = threads if threads > 0 else host["usable"]
     t0 = time.perf_counter()
     tree = lib.tree(points, leafsize, box)
     build_s = time.perf_counter() - t0
@@ -230,8 +329,17 @@ def cpu_baseline(points, k, leafsize, box, sample, gpu_d, gpu_i):
     return {"value": sample / query_s, "unit": "queries/s", "cores": cores, "kind": kind,
             "sample": f"{sample} self-queries (first {sample} particles) of the same "
                       f"{len(points):.0e}-point periodic tree, k={k}, leafsize={leafsize}, "
-                      f"{cores} threads; single-threaded CPU build {build_s:.2f} s",
-            "build_s": build_s}, parity
+                      f"{cores} threads on {host['model']} ({host['usable']} usable of nproc "
+                      f"{host['nproc']}); the port's single-threaded CPU build {build_s:.2f} s",
+            "host": host, "build_s": build_s}, parity
+
+
+def cpu_build_entry(build_s):
+    r = cpu_ratio()
+    out = {"port_ms": build_s * 1e3, "kind": "port", "threads": 1, "ratio": r}
+    if r:
+        out["reference_estimate_ms"] = build_s * 1e3 / r["build_time_port_over_reference"]
+    return out
 
 
 def gloo_halo() -> bool:
@@ -912,8 +1020,6 @@ def main():
         counts = allgather_int(own)
     else:
         counts = [own]
-    if rank != 0:
-        return
     total_q = own_total * args.steps
     value = total_q / elapsed_max
     ms_per_step = elapsed_max / args.steps * 1e3
@@ -935,13 +1041,26 @@ def main():
     step_traffic, step_source = pmc_step_traffic(own, k) if world == 1 else (None, None)
     step_sec = elapsed_max / args.steps
     step_ach = None if step_traffic is None else step_traffic / step_sec / 1e9
+    peak = HBM_PEAK_GBS
+    basis = None
+    if world > 1:
+        ent, src = pmc_slab(args, world, k)
+        sr = slab_roofline(ent, src, world, bq, q_per_launch, own, col_avg_ms, step_sec,
+                           allsum, allmax)
+        traffic, step_traffic = sr["traffic"], sr["step_traffic"]
+        traffic_source = step_source = sr["source"]
+        achieved, col_avg_ms, step_ach = sr["work_achieved"], sr["kernel_ms"], sr["step_achieved"]
+        peak, basis = sr["peak"], sr["basis"]
+    if rank != 0:
+        return
     extra = None
     if world == 1 and args.suite:
         extra = suite(args, capi, hip, tree, dev_pts, n, k, L, stream, od, oi)
     cpu = None
     parity = None
     if world == 1 and not args.no_cpu_baseline:
-        cpu, parity = cpu_baseline(points, k, args.leafsize, L, parity_rows, gpu_d, gpu_i)
+        cpu, parity = cpu_baseline(points, k, args.leafsize, L, parity_rows, gpu_d, gpu_i,
+                                   threads=args.cpu_threads)
     out = {
         "metric": METRIC,
         "value": value,
@@ -974,16 +1093,16 @@ def main():
         "build_ms": build_ms,
         "build_ms_first": build_ms_first,
         "roofline": roofline_entry(
-            traffic, traffic_source, col_avg_ms, achieved,
+            traffic, traffic_source, col_avg_ms, achieved, peak=peak,
             kernel="knn_collect_grp_kernel<periodic> (nbodyhpc_amd/csrc/knn_collect.hip)",
             step_work_frac=value * bq / (HBM_PEAK_GBS * 1e9 * world),
             launches_per_step=col_launches / args.steps, queries_per_launch=q_per_launch,
-            bytes_per_query=bq,
+            bytes_per_query=bq, peak_per_gpu=HBM_PEAK_GBS, traffic_basis=basis,
             # the whole pipeline (bucketing, sort, collect, select, retries):
             # PMC HBM bytes of one step / the step's wall time
             step_traffic=step_traffic, step_traffic_source=step_source,
             step_achieved=step_ach,
-            step_frac=None if step_ach is None else step_ach / HBM_PEAK_GBS),
+            step_frac=None if step_ach is None else step_ach / peak),
         "breakdown_ms_per_step": {
             "leaf_key": key_ms / args.steps, "sort": sort_ms / args.steps,
             "knn": knn_ms / args.steps, "knn_collect": col_ms / args.steps,
@@ -1001,9 +1120,15 @@ def main():
         "fallback_queries": st["fallback_queries"], "retry_queries": st["retry_queries"],
         # where a collect wave's cycles go (work-counter pass, s_memtime clocks)
         "collect_phase_frac": _phase_frac(st),
-        "cpu_baseline": None if cpu is None else {kk: cpu[kk] for kk in
-                                                  ("value", "unit", "cores", "kind", "sample")},
+        "cpu_baseline": None if cpu is None else dict(
+            {kk: cpu[kk] for kk in ("value", "unit", "cores", "kind", "sample")},
+            port_over_reference=cpu_ratio()),
         "cpu_build_ms": None if cpu is None else cpu["build_s"] * 1e3,
+        # the port's build selects with a scalar partition where the reference
+        # runs its AVX2 one: the measured build-time ratio scales it to the
+        # reference's (an estimate; the reference cannot run on the GPU box)
+        "cpu_build": None if cpu is None else cpu_build_entry(cpu["build_s"]),
+        "cpu_host": None if cpu is None else cpu["host"],
         "parity_vs_cpu": parity,
     }
     if extra is not None:

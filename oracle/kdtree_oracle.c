@@ -21,10 +21,13 @@
  *                               kdtree/third_party/misc/thread_pool.hpp:148-183
  *   naive kNN (house KAT)       kdtree/src/cpp/tests/test.cpp:14-37
  *
- * Selection: the reference selects with an AVX2 Floyd-Rivest partition
- * (kdtree_selection.cpp); only the order statistic matters for the node table,
- * so this restatement uses a plain Hoare quickselect.  Leaf membership under
- * exact coordinate ties at a split value is implementation-defined in both.
+ * Selection: the reference selects with Floyd-Rivest (kdtree_selection.cpp:
+ * 322-368) over an AVX2 vectorised partition; fr_select below restates the same
+ * sample-window recursion (integer pivot-side test, truncating window bounds)
+ * over a scalar Hoare partition.  Only the order statistic, i.e. the split
+ * value, is pinned: where several points tie at a split value, which of them
+ * land left depends on the partition, so leaf membership and the descendants'
+ * splits under such ties can differ from the reference.
  *
  * Radius query (query_ball) is NEW capability (no reference code): brute-force
  * semantics are "count points with d2 <= r*r", d2 computed with the same f32
@@ -172,22 +175,27 @@ static inline void swap_pt(orc_pt *a, orc_pt *b) {
     *b = t;
 }
 
-/* Floyd-Rivest selection (the algorithm the reference's AVX2 selection follows,
- * kdtree_selection.cpp:322-368: a sample window when the range exceeds 600,
- * then a Hoare-style partition around the sampled pivot): afterwards p[m].k is
- * the m-th order statistic of p[0..n) and p[0..m) <= p[m] <= p[m+1..n).  Only
- * the order statistic (the split value) is pinned; which of several points
- * tied at it land left is implementation-defined, here as in the reference. */
+/* Floyd-Rivest selection (the recursion of kdtree_selection.cpp:322-368: a
+ * sample window when the range exceeds 600 elements, the pivot side flipped by
+ * the integer test i < n / 2, window bounds truncated to integers), then a
+ * scalar Hoare partition around the sampled pivot where the reference runs its
+ * AVX2 partition (pivot at the right end).  Afterwards p[m].k is the m-th order
+ * statistic of p[0..n) and p[0..m) <= p[m] <= p[m+1..n).  Only that order
+ * statistic (the split value) is pinned to the reference; the order of the
+ * other elements, and so which of several points tied at the split land left,
+ * is this partition's own. */
 static void fr_select(orc_pt *p, int64_t left, int64_t right, int64_t m) {
     while (right > left) {
         if (right - left > 600) {
-            const double n = (double)(right - left + 1);
-            const double i = (double)(m - left + 1);
+            const int64_t ni = right - left + 1, ii = m - left + 1;
+            const double n = (double)ni, i = (double)ii;
             const double z = log(n);
             const double sz = 0.5 * exp(2.0 * z / 3.0);
-            const double sd = 0.5 * sqrt(z * sz * (n - sz) / n) * (i - n / 2 < 0 ? -1.0 : 1.0);
-            int64_t nl = (int64_t)floor((double)m - i * sz / n + sd);
-            int64_t nr = (int64_t)floor((double)m + (n - i) * sz / n + sd);
+            /* the reference's ptrdiff_t test (kdtree_selection.cpp:340) */
+            const double sd = 0.5 * sqrt(z * sz * (n - sz) / n) * (ii < ni / 2 ? -1.0 : 1.0);
+            /* static_cast<ptrdiff_t>: truncation toward zero (:343-344) */
+            int64_t nl = (int64_t)((double)m - i * sz / n + sd);
+            int64_t nr = (int64_t)((double)m + (n - i) * sz / n + sd);
             if (nl < left) nl = left;
             if (nr > right) nr = right;
             fr_select(p, nl, nr, m);

@@ -8,7 +8,7 @@ also from scipy.spatial.KDTree — the reference's own test oracle
 at test time; each fixture stores a SHA-256 of its inputs so a drift in the
 generator is caught.
 
-    PYTHONPATH=. python tests/golden/gen_golden.py
+    PYTHONPATH=. python tests/golden/gen_golden.py [--only g7]
 """
 from __future__ import annotations
 
@@ -24,13 +24,42 @@ sys.path.insert(0, ROOT)
 
 from oracle.oracle import Reference  # noqa: E402
 from tests.golden.inputs import (edge_cases, g1_inputs, g2_inputs, g3_inputs, g4_inputs,  # noqa: E402
-                                 g5_inputs, sha)
+                                 g5_inputs, g7_inputs, node_shape, sha)
 
 OUT = os.path.dirname(os.path.abspath(__file__))
 
 
+def g7(R):
+    """G7: node tables at 1e6-1e7 (gen_golden.py --only g7).  Tie-free sets: the
+    SHA-256 of the reference's whole node table.  The uniform 1e7 set (ties at
+    split values): the SHA of its shape (dim, left, right) and its split values,
+    so a test can measure how many nodes agree."""
+    from oracle.oracle import Oracle
+    O = Oracle()
+    out = {}
+    for key, (gen, leaf, box, tie_free) in g7_inputs().items():
+        pts = gen()
+        t = R.tree(pts, leaf, box)
+        nodes, x, y, z, idx = t.export()
+        out["sha_" + key] = np.array(sha(pts))
+        out["n8_" + key] = np.array(t.n)
+        out["nnodes_" + key] = np.array(t.size)
+        out["table_sha_" + key] = np.array(sha(nodes.view(np.uint32).reshape(-1, 4)))
+        out["shape_sha_" + key] = np.array(sha(node_shape(nodes)))
+        on = O.tree(pts, leaf, box).export()[0]
+        agree = float(np.mean(on["split"].view(np.uint32) == nodes["split"].view(np.uint32)))
+        out["oracle_split_agreement_" + key] = np.array(agree)
+        if not tie_free:
+            out["splits_" + key] = np.ascontiguousarray(nodes["split"])
+        print(key, t.n, t.size, "oracle agreement", agree, flush=True)
+    np.savez_compressed(os.path.join(OUT, "g7_scale_nodes.npz"), **out)
+
+
 def main():
     R = Reference()
+    if "--only" in sys.argv and sys.argv[sys.argv.index("--only") + 1] == "g7":
+        g7(R)
+        return
 
     # G1 / G2: the reference pytest cases (kdtree/tests/test_kdtree.py:6-35), wrapper leafsize 128
     for name, (pts, q, box) in (("g1_basic", g1_inputs()), ("g2_periodic", g2_inputs())):
@@ -91,6 +120,7 @@ def main():
     except RuntimeError:
         out["box_error"] = np.array(1)
     np.savez_compressed(os.path.join(OUT, "g6_edges.npz"), **out)
+    g7(R)
     print("fixtures written to", OUT)
 
 

@@ -64,6 +64,39 @@ def g5_inputs():
     return out
 
 
+def tie_free(n, seed, L=1.0):
+    """n points whose coordinates are distinct on every axis (each axis a random
+    sample without replacement of the 2^24 f32 values k / 2^24 * L), so no
+    split value is tied and the node table is a pure function of the points,
+    whatever partition the build runs (G7)."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    out = np.empty((n, 3), np.float32)
+    for a in range(3):
+        out[:, a] = (rng.choice(1 << 24, size=n, replace=False).astype(np.float64)
+                     * (L / float(1 << 24))).astype(np.float32)
+    return out
+
+
+def g7_inputs():
+    """Node tables at scale: name -> (points, leafsize,
+    boxsize, tie_free).  Tie-free sets must match the reference bit for bit;
+    the plain uniform 1e7 set (the bench generator's seed; ~8.3e6 distinct x
+    values, so split values are tied) is compared for shape and agreement."""
+    return {
+        "tiefree_1e6_leaf64_periodic": (lambda: tie_free(1_000_000, 70), 64, 1.0, True),
+        "tiefree_1e6_leaf32": (lambda: tie_free(1_000_000, 71), 32, None, True),
+        "tiefree_1e7_leaf64_periodic": (lambda: tie_free(10_000_000, 72), 64, 1.0, True),
+        "uniform_1e7_leaf64_periodic": (lambda: uniform(10_000_000, 20261015), 64, 1.0, False),
+    }
+
+
+def node_shape(nodes):
+    """(dim, left, right) of every node: the tree's shape, which depends only on
+    (n8, leafsize) (dims cycle x, y, z: kdtree_impl.hpp:149-169)."""
+    v = np.ascontiguousarray(nodes).view(np.uint32).reshape(-1, 4)
+    return np.ascontiguousarray(v[:, [0, 2, 3]])
+
+
 def edge_cases():
     """name -> (points, queries, k, leafsize, boxsize)"""
     out = {}

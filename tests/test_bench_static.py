@@ -8,7 +8,7 @@ import os
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 COLLECTIVES = {"allsum", "allmax", "allgather_int", "barrier", "all_reduce", "all_gather",
-               "broadcast", "second_round"}
+               "broadcast", "second_round", "slab_roofline"}
 
 
 def _is_rank0_return(node):
@@ -101,3 +101,50 @@ def test_pmc_lookups_match_the_library_sha(tmp_path, monkeypatch):
     assert bench.pmc_step_traffic(100, 32) == (None, None)
     r = bench.roofline_entry(8e9, "x", 2.0, 1000.0, step_traffic=1.0)
     assert abs(r["frac"] - 8e9 / 2e-3 / 1e9 / 8000.0) < 1e-12 and r["frac"] <= 1.0
+
+
+def _bench_module():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def test_n_gt_1_roofline_from_per_rank_slab_profiles(tmp_path, monkeypatch):
+    """an N > 1 line finds the slab profile of its own build
+    and decomposition (library SHA, world, scaling, --particles, k, leafsize,
+    seed), and the roofline sums every rank's own queries x bytes per query over
+    the slowest rank's time against N x 8 TB/s."""
+    import json
+    import types
+    bench = _bench_module()
+    monkeypatch.setattr(bench, "lib_sha256", lambda: "abc")
+    monkeypatch.setattr(bench, "PROFILES", str(tmp_path))
+    entry = {"world": 2, "rank": 0, "scaling": "strong", "n_arg": 100_000_000, "k": 32,
+             "leafsize": 64, "seed": 20261015, "own": 50_000_000, "n_local": 54_000_000,
+             "collect_bytes_per_query": 1000.0, "step_bytes_per_query": 2000.0}
+    other = dict(entry, world=4)
+    json.dump({"lib_sha256": "abc", "entries": [other, entry]},
+              open(tmp_path / "r99_pmc_slab.json", "w"))
+    json.dump({"lib_sha256": "old", "entries": [dict(entry, step_bytes_per_query=1.0)]},
+              open(tmp_path / "r98_pmc_slab.json", "w"))
+    args = types.SimpleNamespace(scaling="strong", n=1e8, leafsize=64, seed=20261015)
+    e, src = bench.pmc_slab(args, 2, 32)
+    assert e == entry and src.endswith("r99_pmc_slab.json")
+    assert bench.pmc_slab(args, 8, 32) == (None, None)
+    assert bench.pmc_slab(types.SimpleNamespace(**dict(vars(args), scaling="weak")), 2, 32) \
+        == (None, None)
+    # two ranks (the reducers stand in for gloo): rank times 10 and 12 ms
+    world = 2
+    allsum = lambda v: v * world  # noqa: E731  (both ranks hold the same values)
+    allmax = lambda v: max(v, 12.0) if v > 1 else v  # noqa: E731
+    r = bench.slab_roofline(e, src, world, 4951.6, 5e7, 5e7, 10.0, 0.025, allsum, allmax)
+    assert r["kernel_ms"] == 12.0 and r["peak"] == 16000.0
+    assert r["traffic"] == 2 * 1000.0 * 5e7 and r["step_traffic"] == 2 * 2000.0 * 5e7
+    assert abs(r["step_achieved"] - 2 * 2000.0 * 5e7 / 0.025 / 1e9) < 1e-6
+    assert "rank 0's slab" in r["basis"]
+    # a rank without a profile: no traffic terms on any rank
+    r0 = bench.slab_roofline(None, None, world, 4951.6, 5e7, 5e7, 10.0, 0.025,
+                             lambda v: v, allmax)
+    assert r0["traffic"] is None and r0["step_traffic"] is None and r0["basis"] is None

@@ -2,10 +2,13 @@
 against the reference's golden vectors and the oracle.  Run on an MI355X:
     python -m pytest tests -m gpu -x -q
 """
+import os
+
 import numpy as np
 import pytest
 
-from tests.golden.inputs import edge_cases, g1_inputs, g2_inputs, g3_inputs, g4_inputs, g5_inputs, sha, uniform
+from tests.golden.inputs import (edge_cases, g1_inputs, g2_inputs, g3_inputs, g4_inputs, g5_inputs,
+                                 g7_inputs, node_shape, sha, uniform)
 from tests.parity import assert_knn_equal, check_tree_structure, d2_ref, leaf_sets
 
 pytestmark = pytest.mark.gpu
@@ -65,6 +68,45 @@ def test_node_tables_match_reference(gpu, golden):
         assert t.size == ref.shape[0], key
         assert np.array_equal(nodes.view(np.uint32).reshape(-1, 4), ref), key
         check_tree_structure(nodes, x, y, z, idx, len(pts), leaf)
+
+
+@pytest.mark.parametrize("key", list(g7_inputs()))
+def test_node_tables_at_scale_match_reference(gpu, golden, key):
+    """G7: node tables at 1e6-1e7 points against the
+    reference's (kdtree_impl.hpp:98-146, split kdtree_selection.cpp:475-494).
+    Tie-free sets (every coordinate distinct on its axis): the whole table bit
+    for bit.  The plain uniform 1e7 set has tied coordinates at split values,
+    where which tied points go left is the partition's choice (the reference's
+    AVX2 Floyd-Rivest, our radix select) and the descendants' splits follow
+    from it: there the shape (n8, node count, dims, every node's range) must be
+    equal and the fraction of equal split values is measured (the C oracle's,
+    over the same set, is in the fixture) and must stay >= 0.99."""
+    g = golden("g7_scale_nodes")
+    gen, leaf, box, tie_free = g7_inputs()[key]
+    pts = gen()
+    assert str(g["sha_" + key]) == sha(pts)
+    t = gpu.Tree(pts, leafsize=leaf, boxsize=box)
+    nodes = t.export()[0]
+    assert t.n == int(g["n8_" + key]) and t.size == int(g["nnodes_" + key]), key
+    assert sha(node_shape(nodes)) == str(g["shape_sha_" + key]), key
+    if tie_free:
+        assert sha(nodes.view(np.uint32).reshape(-1, 4)) == str(g["table_sha_" + key]), key
+        return
+    ref = g["splits_" + key]
+    agree = float(np.mean(nodes["split"].view(np.uint32) == ref.view(np.uint32)))
+    internal = nodes["dim"] >= 0
+    agree_int = float(np.mean(nodes["split"][internal].view(np.uint32)
+                              == ref[internal].view(np.uint32)))
+    report = {"key": key, "nodes": int(t.size), "internal": int(internal.sum()),
+              "split_agreement_all_nodes": agree, "split_agreement_internal": agree_int,
+              "oracle_split_agreement_all_nodes": float(g["oracle_split_agreement_" + key])}
+    print(report)
+    out = os.environ.get("NBKD_TEST_REPORT_DIR")
+    if out:
+        import json
+        with open(os.path.join(out, f"g7_{key}.json"), "w") as f:
+            json.dump(report, f)
+    assert agree >= 0.99, report
 
 
 def test_leaf_membership_matches_oracle(gpu, oracle):

@@ -173,3 +173,21 @@ def test_ball_count_stats_counters(oracle):
     assert np.array_equal(c, c0)
     assert points >= int(c.sum()) and points % 8 == 0
     assert nodes >= points // 32
+
+
+def test_g7_tie_free_node_tables_pin_the_oracle(golden):
+    """G7: on sets with no tied coordinate the C oracle's node table equals the
+    reference's bit for bit at 1e6 and 1e7 points (tests/golden/gen_golden.py
+    --only g7); the GPU tables are checked against the same fixture."""
+    from oracle.oracle import Oracle
+    from tests.golden.inputs import g7_inputs, node_shape, sha
+    g = golden("g7_scale_nodes")
+    O = Oracle()
+    for key, (gen, leaf, box, tie_free) in g7_inputs().items():
+        if not tie_free:
+            continue
+        pts = gen()
+        assert str(g["sha_" + key]) == sha(pts)
+        nodes = O.tree(pts, leaf, box).export()[0]
+        assert sha(nodes.view(np.uint32).reshape(-1, 4)) == str(g["table_sha_" + key]), key
+        assert sha(node_shape(nodes)) == str(g["shape_sha_" + key]), key
