@@ -619,6 +619,9 @@ def run_c5(args, rank, world, local_rank, dist, same_dev, barrier, allmax, allsu
     def kth_pass():
         tree.query_kth_device(dev_pts.ptr, own, k, rk.ptr, stream.handle)
         if rows is not None:
+            # the forward test enqueued behind the pass, its count read behind
+            # an event (no device synchronisation)
+            rows.start(*slab.covered_range(bounds, rank, ds.h))
             st = slab.second_round(rows, rank, world, bounds, L, ds.h, k, dist)
             for kk in ("rows_forwarded", "forwards"):
                 sr_acc[kk] += st[kk]
@@ -926,36 +929,61 @@ def main():
             tree.close()
     build_ms = allmax(min(build_ms))
 
-    od = hip.DeviceArray((own, k), np.float32)
-    oi = hip.DeviceArray((own, k), np.uint32)
+    # N > 1: two row buffers, so a step's second round overlaps the next step
+    bufs = [(hip.DeviceArray((own, k), np.float32), hip.DeviceArray((own, k), np.uint32))
+            for _ in range(1 if ds is None else 2)]
+    od, oi = bufs[0]
 
     # N > 1: rows whose k-th neighbour lies past the halo are forwarded to the
     # neighbours and merged (second-round exchange) inside
     # every step, so every row of every step is exact; no rebuild, no widening
-    rows = None if ds is None else slab.DeviceRows(ds, tree, k, od.ptr, oi.ptr,
-                                                   stream=stream.handle)
-    sr_acc = {"rows_forwarded": 0, "forwards": 0, "hops": 0, "calls": 0}
+    rows_b = None if ds is None else [slab.DeviceRows(ds, tree, k, b[0].ptr, b[1].ptr,
+                                                      stream=stream.handle) for b in bufs]
+    rows = None if rows_b is None else rows_b[0]
+    cover = None if ds is None else slab.covered_range(ds.bounds, rank, ds.h)
+    sr_acc = {"rows_forwarded": 0, "forwards": 0, "hops": 0, "calls": 0, "host_s": 0.0}
 
     counters = {"timing": False, "stats": False}
+    pipe = {"cur": 0, "pending": None, "last": 0}
+
+    def resolve(j):
+        # the second round's small host-in kNN calls stay out of the kernel
+        # timers and work counters (they describe the slab-local pass); its
+        # time is in the step's wall clock
+        capi.timing_enable(False)
+        capi.stats_enable(False)
+        t_r = time.perf_counter()
+        st = slab.second_round(rows_b[j], rank, world, ds.bounds, L, ds.h, k, dist)
+        sr_acc["host_s"] += time.perf_counter() - t_r
+        capi.timing_enable(counters["timing"])
+        capi.stats_enable(counters["stats"])
+        for kk in ("rows_forwarded", "forwards"):
+            sr_acc[kk] += st[kk]
+        sr_acc["hops"] = max(sr_acc["hops"], st["hops"])
+        sr_acc["calls"] += 1
 
     def step():
-        tree.query_device(dev_pts.ptr, own, k, od.ptr, oi.ptr, stream.handle)
-        if rows is not None:
-            # the second round's small host-in kNN calls stay out of the kernel
-            # timers and work counters (they describe the slab-local pass); its
-            # time is in the step's wall clock
-            capi.timing_enable(False)
-            capi.stats_enable(False)
-            st = slab.second_round(rows, rank, world, ds.bounds, L, ds.h, k, dist)
-            capi.timing_enable(counters["timing"])
-            capi.stats_enable(counters["stats"])
-            for kk in ("rows_forwarded", "forwards"):
-                sr_acc[kk] += st[kk]
-            sr_acc["hops"] = max(sr_acc["hops"], st["hops"])
-            sr_acc["calls"] += 1
+        j = pipe["cur"]
+        tree.query_device(dev_pts.ptr, own, k, bufs[j][0].ptr, bufs[j][1].ptr, stream.handle)
+        pipe["last"] = j
+        if ds is None:
+            return
+        # the forward test and its count are enqueued behind this step's kNN;
+        # the previous step's second round (its count agreed over gloo, and
+        # any forwarded rows) runs while this step computes on the device
+        rows_b[j].start(*cover)
+        if pipe["pending"] is not None:
+            resolve(pipe["pending"])
+        pipe["pending"], pipe["cur"] = j, 1 - j
+
+    def drain():
+        if pipe["pending"] is not None:
+            resolve(pipe["pending"])
+            pipe["pending"] = None
 
     for _ in range(args.warmup):
         step()
+    drain()
     stream.synchronize()
     if ds is not None:
         # the slab-local rows before the second round: how many reach past the halo
@@ -964,6 +992,7 @@ def main():
         halo["rows_past_halo_before_second_round"] = int(
             allsum(float(ds.violations(od.ptr, k, stream.handle))))
         step()  # and resolved again, so the checked rows below are the exact ones
+        drain()
         stream.synchronize()
         halo.update({"h": ds.h, "local_points": n_local, "transport": ds.transport})
         for kk in sr_acc:
@@ -976,10 +1005,12 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
+    drain()
     hip.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
     sr_timed = dict(sr_acc)
+    od, oi = bufs[pipe["last"]]  # the last step's (exact) rows
     knn_ms, knn_launches = capi.timing_read("knn")
     sort_ms, _ = capi.timing_read("sort")
     key_ms, _ = capi.timing_read("leaf_key")
@@ -1003,6 +1034,9 @@ def main():
     pts_scanned = st["pair_evals"]
     capi.stats_enable(False)
     counters["stats"] = False
+    drain()  # that step's second round: its rows are the exact ones read below
+    stream.synchronize()
+    od, oi = bufs[pipe["last"]]
 
     gpu_d = gpu_i = None
     parity_rows = min(args.cpu_sample, own)
@@ -1011,11 +1045,27 @@ def main():
         gpu_i = oi.numpy_head(parity_rows)
 
     if ds is not None:
+        # the same steps without the second round (rows then inexact, never
+        # reported): what the round adds to a step, on the same (possibly
+        # shared) device
+        barrier()
+        hip.synchronize()
+        t_k = time.perf_counter()
+        for _ in range(args.steps):
+            tree.query_device(dev_pts.ptr, own, k, bufs[0][0].ptr, bufs[0][1].ptr, stream.handle)
+        hip.synchronize()
+        barrier()
+        knn_only = allmax(time.perf_counter() - t_k) / args.steps
         halo["second_round"] = {
             "transport": rows.transport,
             "rows_forwarded_per_step": allsum(float(sr_timed["rows_forwarded"])) / max(args.steps, 1),
             "forwards_per_step": allsum(float(sr_timed["forwards"])) / max(args.steps, 1),
             "max_hops": int(allmax(float(sr_timed["hops"]))),
+            # overlapped with the next step's kNN (pipelined steps); the host's
+            # time in it, and the step time over the same steps without it
+            "host_ms_per_step": allmax(sr_timed["host_s"]) / args.steps * 1e3,
+            "ms_per_step": (elapsed_max / args.steps - knn_only) * 1e3,
+            "knn_only_ms_per_step": knn_only * 1e3,
         }
         counts = allgather_int(own)
     else:

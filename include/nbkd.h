@@ -23,12 +23,15 @@
  * each call holds one; a call reusing a workspace from another stream first
  * waits for that workspace's previous call on the device.
  *
- * Host buffers of any size: a call with host queries or host outputs runs in
- * batches of "host_batch" queries (nbkd_set_tuning; default ~1 GiB of queries
- * and results per batch) through two device slots, the next batch's queries
- * copied in and the previous batch's results copied out on a second stream
- * while one batch computes, so device scratch stays bounded for any m (the
- * reference streams any m its host memory holds, pybind.cpp:103-104,164-172).
+ * Host buffers of any size: a kNN, k-th distance or radius-count call with
+ * host queries or host outputs runs in batches of "host_batch" queries
+ * (nbkd_set_tuning; default ~1 GiB of queries, results and unbudgeted device
+ * scratch per batch) through two device slots and two pinned host staging
+ * slots: the next batch's queries are copied in and the previous batch's
+ * results copied out (DMA on a second stream, host copies on the library's
+ * copy threads, "host_threads") while one batch computes, so device scratch
+ * stays bounded for any m (the reference streams any m its host memory holds,
+ * pybind.cpp:103-104,164-172).
  * Between batches the call runs the thread's interrupt check
  * (nbkd_set_interrupt; the reference polls PyErr_CheckSignals every 1000
  * queries, pybind.cpp:128-133) and returns NBKD_EINTR when it asks to stop.
@@ -127,6 +130,8 @@ nbkd_status nbkd_query_ball_count(const nbkd_tree *tree, const float *q, uint64_
  * (always host memory); out_idx receives offsets[m] original point indices,
  * each row in tree traversal order (unsorted; sort per row if needed).  Call with out_idx == NULL first to get
  * offsets[m] (the required capacity), then again with a buffer of that size.
+ * Not batched: the call holds the m queries, their counts and the offsets[m]
+ * indices in device scratch at once (split a very large m into several calls).
  */
 nbkd_status nbkd_query_ball_csr(const nbkd_tree *tree, const float *q, uint64_t m, float r,
                                 uint64_t *out_offsets, uint32_t *out_idx, uint64_t capacity,
@@ -151,6 +156,8 @@ void nbkd_free(nbkd_tree *tree);
  *                      columns (default 0 = min(96 GiB, free / 3)).
  *   "host_batch"       queries per batch of a host-buffer call (default 0 =
  *                      about 1 GiB of queries plus results per batch).
+ *   "host_threads"     threads copying between the caller's host arrays and
+ *                      pinned staging (default 0 = the usable cores, <= 16).
  * NEW (no reference counterpart: kdtree/src/cpp/pybind.cpp:196-216 has no knobs). */
 nbkd_status nbkd_set_tuning(const char *name, double value);
 nbkd_status nbkd_get_tuning(const char *name, double *value);
@@ -226,6 +233,15 @@ nbkd_status nbkd_slab_violations(const float *q, const float *dist, uint64_t m, 
 nbkd_status nbkd_slab_forward(const float *q, const float *dist, uint64_t m, int32_t k, float cl,
                               float ch, uint32_t *out_list, uint8_t *out_sides, uint64_t capacity,
                               uint64_t *count, int32_t device, void *stream);
+
+/* nbkd_slab_forward without waiting: `count` is a device word (8 B) that the
+ * call zeroes and the kernel fills on `stream`; nothing is read back, so a
+ * caller can queue its next work before it copies the count out (the bench's
+ * N > 1 step overlaps the second round's agreement with the next step). */
+nbkd_status nbkd_slab_forward_async(const float *q, const float *dist, uint64_t m, int32_t k,
+                                    float cl, float ch, uint32_t *out_list, uint8_t *out_sides,
+                                    uint64_t capacity, uint64_t *count, int32_t device,
+                                    void *stream);
 
 /* Row gather / scatter of device arrays: dst[i] = src[idx[i]] (gather) or
  * dst[idx[i]] = src[i] (scatter) for n rows of row_bytes (a multiple of 4)

@@ -64,6 +64,8 @@ _PROTOS = {
                                     ctypes.c_float, ctypes.POINTER(_u64), _i32, _c_p]),
     "nbkd_slab_forward": (_i32, [_c_p, _c_p, _u64, _i32, ctypes.c_float, ctypes.c_float, _c_p,
                                  _c_p, _u64, ctypes.POINTER(_u64), _i32, _c_p]),
+    "nbkd_slab_forward_async": (_i32, [_c_p, _c_p, _u64, _i32, ctypes.c_float, ctypes.c_float,
+                                       _c_p, _c_p, _u64, _c_p, _i32, _c_p]),
     "nbkd_rows_gather": (_i32, [_c_p, _u64, _c_p, _u64, _c_p, _i32, _c_p]),
     "nbkd_rows_scatter": (_i32, [_c_p, _u64, _c_p, _u64, _c_p, _i32, _c_p]),
     "nbkd_set_tuning": (_i32, [ctypes.c_char_p, ctypes.c_double]),
@@ -329,6 +331,15 @@ def slab_violations(q_ptr, dist_ptr, m, k, lo, hi, h, device=0, stream=None):
     _check(lib().nbkd_slab_violations(q_ptr, dist_ptr, int(m), int(k), float(lo), float(hi),
                                       float(h), ctypes.byref(c), int(device), stream))
     return c.value
+
+
+def slab_forward_async(q_ptr, dist_ptr, m, k, cl, ch, count_ptr, list_ptr=None, sides_ptr=None,
+                       capacity=0, device=0, stream=None):
+    """nbkd_slab_forward_async: the same test, its total in the device word
+    count_ptr when the stream gets there (nothing is waited for)."""
+    _check(lib().nbkd_slab_forward_async(q_ptr, dist_ptr, int(m), int(k), float(cl), float(ch),
+                                         list_ptr, sides_ptr, int(capacity), count_ptr,
+                                         int(device), stream))
 
 
 def slab_forward(q_ptr, dist_ptr, m, k, cl, ch, list_ptr=None, sides_ptr=None, capacity=0,

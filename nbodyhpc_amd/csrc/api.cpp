@@ -2,13 +2,18 @@
 // build.hip / query.hip.  No exception crosses the boundary.
 #include <hip/hip_runtime.h>
 
+#include <sched.h>
+
 #include <atomic>
 #include <cmath>
+#include <condition_variable>
+#include <cstdio>
 #include <cstring>
 #include <map>
 #include <mutex>
 #include <new>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "internal.hpp"
@@ -216,8 +221,9 @@ void tree_free(void *p) {
 
 namespace {
 // nbkd_set_tuning knobs (process-wide); defaults are the measured optima
-std::atomic<double> g_tune[TUNE_N] = {{3.5}, {0.0}, {0.0}};
-const char *const g_tune_names[TUNE_N] = {"knn_seed_margin", "candidate_bytes", "host_batch"};
+std::atomic<double> g_tune[TUNE_N] = {{3.5}, {0.0}, {0.0}, {0.0}};
+const char *const g_tune_names[TUNE_N] = {"knn_seed_margin", "candidate_bytes", "host_batch",
+                                          "host_threads"};
 thread_local nbkd_interrupt_fn t_intr = nullptr;
 thread_local void *t_intr_user = nullptr;
 } // namespace
@@ -246,12 +252,118 @@ Workspace &acquire_ws(const Tree &t) {
 AllWs::AllWs(const Tree &t_, hipStream_t s) : t(t_), pool(t_.ws_mu) {
     locks.emplace_back(t.ws.mu);
     for (auto &w : t.ws_extra) locks.emplace_back(w->mu);
+    // held by this thread: an out-of-memory retry under this lock (malloc_or_release
+    // -> trim_idle_workspaces) must not try_lock them
+    hold_mark(&t.ws);
+    for (auto &w : t.ws_extra) hold_mark(w.get());
     // the stream waits for every workspace's last call
     auto wait = [&](Workspace &w) {
         if (w.used && w.done) (void)hipStreamWaitEvent(s, w.done, 0);
     };
     wait(t.ws);
     for (auto &w : t.ws_extra) wait(*w);
+}
+
+AllWs::~AllWs() {
+    for (auto &w : t.ws_extra) hold_unmark(w.get());
+    hold_unmark(&t.ws);
+}
+
+// ------------------------------------------------------------ host copy threads
+// The host-buffer pipeline moves every batch between the caller's (pageable)
+// arrays and pinned staging: a ~1 GiB batch of k = 32 rows is one memcpy per
+// output, and its first touch of fresh numpy pages faults them in.  One thread
+// does ~5-10 GB/s of that, under the ~50 GB/s of pinned PCIe DMA, so the copy is
+// split into 8 MiB chunks over a few threads (the usable cores: the affinity
+// mask capped by the cgroup quota, at most 16; nbkd_set_tuning("host_threads")).
+namespace {
+int usable_cpus() {
+    int n = 1;
+    cpu_set_t set;
+    if (sched_getaffinity(0, sizeof(set), &set) == 0) n = CPU_COUNT(&set);
+    if (FILE *f = std::fopen("/sys/fs/cgroup/cpu.max", "r")) {
+        char q[32] = {0};
+        double period = 0.0;
+        if (std::fscanf(f, "%31s %lf", q, &period) == 2 && std::strcmp(q, "max") != 0 && period > 0)
+            n = std::min(n, std::max(1, (int)std::ceil(std::atof(q) / period)));
+        std::fclose(f);
+    }
+    return std::max(n, 1);
+}
+
+struct CopyPool {
+    std::mutex job_mu; // one job at a time
+    std::mutex mu;
+    std::condition_variable cv, done_cv;
+    int nthreads = 0;
+    char *dst = nullptr;
+    const char *src = nullptr;
+    size_t bytes = 0;
+    std::atomic<size_t> next{0};
+    int busy = 0;
+    uint64_t gen = 0;
+    static constexpr size_t CHUNK = 8u << 20;
+
+    void work() {
+        for (size_t i; (i = next.fetch_add(1)) * CHUNK < bytes;) {
+            const size_t o = i * CHUNK;
+            std::memcpy(dst + o, src + o, std::min(CHUNK, bytes - o));
+        }
+    }
+    void loop() {
+        uint64_t seen = 0;
+        std::unique_lock<std::mutex> lk(mu);
+        for (;;) {
+            cv.wait(lk, [&] { return gen != seen; });
+            seen = gen;
+            lk.unlock();
+            work();
+            lk.lock();
+            if (--busy == 0) done_cv.notify_all();
+        }
+    }
+    // workers are created on first use and never joined (detached, the pool
+    // is never destroyed): a process may exit with them waiting
+    void grow(int want) {
+        while (nthreads < want) {
+            std::thread(&CopyPool::loop, this).detach();
+            ++nthreads;
+        }
+    }
+    void run(void *d, const void *s, size_t n, int workers) {
+        std::lock_guard<std::mutex> job(job_mu);
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            grow(workers - 1);
+            dst = (char *)d;
+            src = (const char *)s;
+            bytes = n;
+            next.store(0);
+            busy = nthreads;
+            ++gen;
+        }
+        cv.notify_all();
+        work(); // the calling thread takes chunks too
+        std::unique_lock<std::mutex> lk(mu);
+        done_cv.wait(lk, [&] { return busy == 0; });
+    }
+};
+CopyPool &copy_pool() {
+    static CopyPool *p = new CopyPool(); // never destroyed (see grow)
+    return *p;
+}
+} // namespace
+
+void host_copy(void *dst, const void *src, size_t bytes) {
+    if (bytes == 0) return;
+    static const int cpus = usable_cpus();
+    const double tw = tuning(TUNE_HOST_THREADS);
+    const int workers = tw >= 1.0 ? (int)std::min(tw, 256.0) : std::min(cpus, 16);
+    if (workers <= 1 || bytes < (16u << 20)) {
+        std::memcpy(dst, src, bytes);
+        return;
+    }
+    copy_pool().run(dst, src, bytes, workers);
 }
 
 void set_error(const std::string &msg) { g_err = msg; }
@@ -265,8 +377,11 @@ nbkd_status hip_fail(hipError_t e, const char *what) {
 
 bool timing_enabled() { return g_timing; }
 bool stats_enabled() { return g_stats_on; }
-void stats_store(const uint64_t *v) {
-    for (int i = 0; i < NBKD_NSTATS; ++i) g_stats[i] = v[i];
+void stats_reset() {
+    for (int i = 0; i < NBKD_NSTATS; ++i) g_stats[i] = 0;
+}
+void stats_add(const uint64_t *v) {
+    for (int i = 0; i < NBKD_NSTATS; ++i) g_stats[i] += v[i];
 }
 
 TimedScope::TimedScope(const char *name, hipStream_t s) : name_(name), s_(s) {
@@ -655,6 +770,31 @@ void Workspace::release() {
     }
     if (copy) (void)hipStreamDestroy(copy);
     copy = nullptr;
+    for (int b = 0; b < 2; ++b) {
+        if (hpin[b]) (void)hipHostFree(hpin[b]);
+        hpin[b] = nullptr;
+        hpin_cap[b] = 0;
+    }
+}
+
+void *Workspace::host_pinned(int slot, size_t bytes) {
+    if (bytes == 0) bytes = 16;
+    if (hpin_cap[slot] >= bytes) return hpin[slot];
+    if (hpin[slot]) {
+        // the slot's last DMA belongs to a finished call (every call drains
+        // its copies before returning)
+        (void)hipHostFree(hpin[slot]);
+        hpin[slot] = nullptr;
+        hpin_cap[slot] = 0;
+    }
+    hipError_t e = hipHostMalloc(&hpin[slot], bytes, hipHostMallocDefault);
+    if (e != hipSuccess) {
+        (void)hip_fail(e, "hipHostMalloc(pipeline staging)");
+        hpin[slot] = nullptr;
+        return nullptr;
+    }
+    hpin_cap[slot] = bytes;
+    return hpin[slot];
 }
 
 hipError_t Workspace::pipe_init() {

@@ -40,10 +40,15 @@ struct Workspace {
     hipEvent_t done = nullptr;
     bool used = false;
     // the host-buffer pipeline's copy stream (non-blocking) and its events:
-    // [0..1] queries in, [2..3] batch computed, per slot
+    // [0..1] queries in, [2..3] batch computed, [4..5] results out, per slot
     hipStream_t copy = nullptr;
-    hipEvent_t pev[4] = {};
+    hipEvent_t pev[6] = {};
     hipError_t pipe_init(); // creates copy / pev once
+    // the pipeline's two pinned host staging slots (hipHostMalloc, grow-only,
+    // kept across calls: pinning is paid once per workspace, not per call)
+    void *hpin[2] = {};
+    size_t hpin_cap[2] = {};
+    void *host_pinned(int slot, size_t bytes); // nullptr on failure (error recorded)
     // returns nullptr on failure (hip error recorded via set_error)
     void *get(int slot, size_t bytes, hipStream_t s);
     void release();
@@ -155,6 +160,7 @@ struct AllWs {
     std::unique_lock<std::mutex> pool;
     std::vector<std::unique_lock<std::mutex>> locks;
     AllWs(const Tree &t_, hipStream_t s);
+    ~AllWs();
 };
 
 // plain-value view passed to kernels
@@ -187,7 +193,11 @@ inline const char *knob(const char *env) { return getenv(env); }
 #else
 inline const char *knob(const char *) { return nullptr; }
 #endif
-enum TuneId { TUNE_KNN_SEED = 0, TUNE_CAND_BYTES, TUNE_HOST_BATCH, TUNE_N };
+enum TuneId { TUNE_KNN_SEED = 0, TUNE_CAND_BYTES, TUNE_HOST_BATCH, TUNE_HOST_THREADS, TUNE_N };
+// host memcpy split over the library's copy threads (api.cpp): the host-buffer
+// pipeline's pinned staging <-> the caller's arrays; small copies stay on the
+// calling thread
+void host_copy(void *dst, const void *src, size_t bytes);
 // the calling thread's interrupt check (nbkd_set_interrupt): true = abandon
 // the call (host-buffer calls check it between batches)
 bool interrupted();
@@ -214,7 +224,10 @@ struct TimedScope {
 bool timing_enabled();
 bool stats_enabled();
 constexpr int NBKD_NSTATS = 17; // see capi.STATS_NAMES (collect kernel) + exact-kernel and retried queries
-void stats_store(const uint64_t *v);
+// the calling thread's counters of its last query call: zeroed when a call
+// starts, summed over the call's batches (a host-buffer call runs several)
+void stats_reset();
+void stats_add(const uint64_t *v);
 
 // hipMalloc that, when the device is out of memory, first returns what the
 // device holds idle -- the cached tree blocks (api.cpp, tree_malloc), the build

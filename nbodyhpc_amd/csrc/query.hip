@@ -1017,17 +1017,23 @@ nbkd_status knn_locked(const Tree &t, Workspace &ws, const float *q, uint64_t m,
             // the re-walk rounds' columns: 8 capg (packets of 64 or one query
             // per wave), then 64 capg (one query per wave)
             const uint32_t capr = capg * 8u, capr2 = capg * 64u;
-            // A round-1 batch holds at most rb queries (the 8 capg columns' budget)
-            // and round 1 takes up to ~10 % of the queries; round 2 rb2 per batch,
-            // up to ~1 %.  The columns are sized for THAT, not for every query
-            // failing: at m = 1e5, k = 32 sizing them for m held ~5.7 GB of
-            // scratch where the first pass needs ~90 MB.  What a round cannot
-            // take (never on the benchmark sets) spills to the next round, the
-            // last to the exact kernel.
+            // A round-1 batch holds at most rb queries: the larger of ~10 % of
+            // the queries and what the first pass's columns hold at 8 capg per
+            // query (memory the call has anyway), within the columns' budget.
+            // Round 1 runs up to RB1_MAX such batches, so it takes every
+            // failure of any first pass with rb >= m / RB1_MAX (ADVICE r04:
+            // round 4 took ~10 % and sent the rest to round 2 and the exact
+            // kernel); the batches past the failure count exit at once on the
+            // device.  Round 2: rb2 per batch, up to ~1 %.  The columns are
+            // sized for THAT, not for every query failing at 64 capg: at
+            // m = 1e5, k = 32 sizing them for m held ~5.7 GB of scratch where
+            // the first pass needs ~90 MB.  What a round cannot take spills to
+            // the next round, the last to the exact kernel.
             const uint64_t mm64 = ((uint64_t)mm + 63) / 64 * 64;
             const uint64_t rb = std::min<uint64_t>(
                 std::max<uint64_t>(budget / ((uint64_t)capr * 8u) / 64u * 64u, 64),
-                std::max<uint64_t>(64, ((uint64_t)mm / 10 + 63) / 64 * 64));
+                std::max<uint64_t>({64, ((uint64_t)mm / 10 + 63) / 64 * 64,
+                                    batch * capg / capr / 64u * 64u}));
             const uint64_t rb2 = std::min<uint64_t>(
                 std::max<uint64_t>(budget / ((uint64_t)capr2 * 8u), 64),
                 std::max<uint64_t>(64, (uint64_t)mm / 100 + 1));
@@ -1083,10 +1089,12 @@ nbkd_status knn_locked(const Tree &t, Workspace &ws, const float *q, uint64_t m,
             // are dense (>= 1/512 of the queries, as on clustered inputs: a
             // coherent walk) and one query per wave where they are sparse
             // (uniform 1e8, r02bi: 82 k failures 1.1 ms one per wave vs 1.9 ms
-            // as packets); batches of rb up to ~10 % of the queries, the rest
-            // (never reached on the benchmark sets) straight to round 2
+            // as packets); up to RB1_MAX batches of rb, enough for every
+            // failure when rb >= m / RB1_MAX (the later batches exit at once
+            // on the device); what remains goes straight to round 2
+            constexpr uint64_t RB1_MAX = 10;
             const uint32_t nb1 =
-                (uint32_t)std::min<uint64_t>(8, std::max<uint64_t>(1, ((uint64_t)mm / 10 + rb - 1) / rb));
+                (uint32_t)std::min<uint64_t>(RB1_MAX, std::max<uint64_t>(1, (mm64 + rb - 1) / rb));
             for (uint32_t bi = 0; bi < nb1; ++bi) {
                 for (int mode = 1; mode <= 2; ++mode) {
                     const QSpan sp{(uint32_t)cap1, rq_count, (uint32_t)(bi * rb), mm, mode};
@@ -1147,7 +1155,7 @@ nbkd_status knn_locked(const Tree &t, Workspace &ws, const float *q, uint64_t m,
         uint64_t h[NBKD_NSTATS];
         NBKD_HIP(hipMemcpyAsync(h, stats, NBKD_NSTATS * 8, hipMemcpyDeviceToHost, s));
         NBKD_HIP(hipStreamSynchronize(s));
-        stats_store(h);
+        stats_add(h);
     }
     if (!(flags & NBKD_OUTPUT_DEVICE)) {
         NBKD_HIP(hipMemcpyAsync(out_d, dd, m * row_words * 4, hipMemcpyDeviceToHost, s));
@@ -1181,12 +1189,21 @@ kth_column_kernel(const float *__restrict__ rows, uint32_t m, int k, float *__re
 
 // Host-buffer calls of any size (a 1e9-query host call needed
 // ~256 GB of device row scratch).  The m queries run in batches of hb through
-// two device slots: while batch i computes on `s`, the copy stream `cp` brings
-// batch i+1's queries in and takes batch i-1's results out (pageable copies,
-// staged by the runtime), so device scratch is bounded by hb whatever m is.
-// run(dq, nb, outs, s) enqueues one batch with device inputs and outputs.
-// Inputs or outputs already on the device are used in place.  The thread's
-// interrupt check (nbkd_set_interrupt) runs between batches.
+// two device slots and two pinned host staging slots (Workspace::host_pinned,
+// kept across calls): the host copies batch i's queries from the caller's
+// array into pinned slot i % 2 (host_copy: a few threads), the copy stream
+// `cp` moves them to the device, batch i computes on `s`, `cp` DMAs its results
+// into the same pinned slot, and while batch i computes and moves, the host
+// copies batch i-1's results from pinned memory into the caller's arrays.
+// Each hop waits on events only.  Until round 4 the copies went straight
+// between pageable memory and the device (the runtime stages those through
+// its own small pinned buffers) with a stream synchronisation per batch:
+// 8.8e7 queries/s host to host at 1e8, k = 32 (profiles/r04ar_suite.json).
+// Device scratch is bounded by hb whatever m is: hb counts the caller's bytes
+// per query plus the per-query device scratch a batch call allocates that no
+// budget bounds (scratch_per_q).  Inputs or outputs already on the device are
+// used in place.  The thread's interrupt check (nbkd_set_interrupt) runs
+// between batches.
 uint64_t host_batch(size_t bytes_per_query, uint64_t m) {
     const double tb = tuning(TUNE_HOST_BATCH);
     uint64_t hb = tb > 0.0 ? (uint64_t)tb
@@ -1197,20 +1214,25 @@ uint64_t host_batch(size_t bytes_per_query, uint64_t m) {
 
 template <typename Run>
 nbkd_status host_pipeline(Workspace &ws, const float *q, uint64_t m, uint32_t flags, int nout,
-                          const size_t *obytes, void *const *outs, Run run, hipStream_t s) {
+                          const size_t *obytes, void *const *outs, size_t scratch_per_q, Run run,
+                          hipStream_t s) {
     const bool in_dev = (flags & NBKD_INPUT_DEVICE) != 0, out_dev = (flags & NBKD_OUTPUT_DEVICE) != 0;
     size_t per_q = in_dev ? 0 : 12;
     for (int j = 0; j < nout; ++j) per_q += out_dev ? 0 : obytes[j];
-    const uint64_t hb = host_batch(per_q, m);
+    const uint64_t hb = host_batch(per_q + scratch_per_q, m);
     NBKD_HIP(ws.pipe_init());
     hipStream_t cp = ws.copy;
-    hipEvent_t *ev_in = ws.pev, *ev_comp = ws.pev + 2;
-    // the previous call of this workspace may still use the slots
+    hipEvent_t *ev_in = ws.pev, *ev_comp = ws.pev + 2, *ev_out = ws.pev + 4;
+    // the previous call of this workspace may still use the device slots
     if (ws.used && ws.done) NBKD_HIP(hipStreamWaitEvent(cp, ws.done, 0));
-    const int nbat_slots = m > hb ? 2 : 1;
+    const int nslots = m > hb ? 2 : 1;
     float *qslot[2] = {nullptr, nullptr};
     void *oslot[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
-    for (int b = 0; b < nbat_slots; ++b) {
+    char *hp[2] = {nullptr, nullptr};
+    // pinned slot layout: [queries hb x 12 B][output 0][output 1]
+    size_t ooff[2] = {in_dev ? 0 : hb * 12, 0};
+    if (nout > 1) ooff[1] = ooff[0] + (out_dev ? 0 : hb * obytes[0]);
+    for (int b = 0; b < nslots; ++b) {
         if (!in_dev) {
             qslot[b] = (float *)ws.get(WS_HQ0 + b, hb * 12, s);
             if (!qslot[b]) return NBKD_ENOMEM;
@@ -1220,13 +1242,29 @@ nbkd_status host_pipeline(Workspace &ws, const float *q, uint64_t m, uint32_t fl
                 oslot[b][j] = ws.get(WS_HO00 + 2 * b + j, hb * obytes[j], s);
                 if (!oslot[b][j]) return NBKD_ENOMEM;
             }
+        if (per_q) {
+            hp[b] = (char *)ws.host_pinned(b, hb * per_q);
+            if (!hp[b]) return NBKD_ENOMEM;
+        }
     }
     nbkd_status rc = NBKD_OK;
-    bool comp_rec[2] = {false, false};
+    bool in_rec[2] = {false, false}, comp_rec[2] = {false, false}, out_rec[2] = {false, false};
     const uint64_t nbat = (m + hb - 1) / hb;
-    for (uint64_t i = 0; i <= nbat && rc == NBKD_OK; ++i) {
+    auto fail = [&](hipError_t e, const char *what) {
+        rc = hip_fail(e, what);
+        return rc;
+    };
+#define NBKD_PIPE(call)                                                                            \
+    do {                                                                                           \
+        hipError_t e_ = (call);                                                                    \
+        if (e_ != hipSuccess) {                                                                    \
+            fail(e_, #call);                                                                       \
+            goto drain;                                                                            \
+        }                                                                                          \
+    } while (0)
+    for (uint64_t i = 0; i <= nbat; ++i) {
         if (i < nbat) {
-            const int b = (int)(i & 1) % nbat_slots;
+            const int b = (int)(i & 1) % nslots;
             const uint64_t b0 = i * hb, nb = std::min<uint64_t>(hb, m - b0);
             if (i > 0 && interrupted()) {
                 set_error("interrupted");
@@ -1235,48 +1273,75 @@ nbkd_status host_pipeline(Workspace &ws, const float *q, uint64_t m, uint32_t fl
             }
             const float *dq = q + 3 * b0;
             if (!in_dev) {
-                // the slot's previous batch has finished reading it
-                if (comp_rec[b]) NBKD_HIP(hipStreamWaitEvent(cp, ev_comp[b], 0));
-                NBKD_HIP(hipMemcpyAsync(qslot[b], q + 3 * b0, nb * 12, hipMemcpyHostToDevice, cp));
-                NBKD_HIP(hipEventRecord(ev_in[b], cp));
-                NBKD_HIP(hipStreamWaitEvent(s, ev_in[b], 0));
+                // pinned slot b's previous queries (batch i-2) have left for the device
+                if (in_rec[b]) NBKD_PIPE(hipEventSynchronize(ev_in[b]));
+                host_copy(hp[b], q + 3 * b0, nb * 12);
+                // device slot b is free once batch i-2 finished reading it
+                if (comp_rec[b]) NBKD_PIPE(hipStreamWaitEvent(cp, ev_comp[b], 0));
+                NBKD_PIPE(hipMemcpyAsync(qslot[b], hp[b], nb * 12, hipMemcpyHostToDevice, cp));
+                NBKD_PIPE(hipEventRecord(ev_in[b], cp));
+                in_rec[b] = true;
+                NBKD_PIPE(hipStreamWaitEvent(s, ev_in[b], 0));
                 dq = qslot[b];
             }
             void *o[2] = {nullptr, nullptr};
             for (int j = 0; j < nout; ++j)
                 o[j] = out_dev ? (void *)((char *)outs[j] + b0 * obytes[j]) : oslot[b][j];
+            // device output slot b is free once batch i-2's results left it
+            if (!out_dev && out_rec[b]) NBKD_PIPE(hipStreamWaitEvent(s, ev_out[b], 0));
             rc = run(dq, nb, o, s);
             if (rc) break;
-            NBKD_HIP(hipEventRecord(ev_comp[b], s));
+            NBKD_PIPE(hipEventRecord(ev_comp[b], s));
             comp_rec[b] = true;
+            if (!out_dev) {
+                NBKD_PIPE(hipStreamWaitEvent(cp, ev_comp[b], 0));
+                for (int j = 0; j < nout; ++j)
+                    NBKD_PIPE(hipMemcpyAsync(hp[b] + ooff[j], oslot[b][j], nb * obytes[j],
+                                             hipMemcpyDeviceToHost, cp));
+                NBKD_PIPE(hipEventRecord(ev_out[b], cp));
+                out_rec[b] = true;
+            }
         }
         if (i >= 1 && !out_dev) {
-            // batch i-1's results (computed on s) out on cp, into the caller's
-            // memory; returns once they have landed, so its slot is free again
-            const int pb = (int)((i - 1) & 1) % nbat_slots;
+            // batch i-1's results: pinned -> the caller's arrays, while batch i
+            // computes and moves
+            const int pb = (int)((i - 1) & 1) % nslots;
             const uint64_t p0 = (i - 1) * hb, pn = std::min<uint64_t>(hb, m - p0);
-            NBKD_HIP(hipStreamWaitEvent(cp, ev_comp[pb], 0));
+            NBKD_PIPE(hipEventSynchronize(ev_out[pb]));
             for (int j = 0; j < nout; ++j)
-                NBKD_HIP(hipMemcpyAsync((char *)outs[j] + p0 * obytes[j], oslot[pb][j],
-                                        pn * obytes[j], hipMemcpyDeviceToHost, cp));
-            NBKD_HIP(hipStreamSynchronize(cp));
+                host_copy((char *)outs[j] + p0 * obytes[j], hp[pb] + ooff[j], pn * obytes[j]);
         }
     }
+#undef NBKD_PIPE
+drain:
     if (rc) {
         // nothing of this call may still touch the slots or the caller's memory
         (void)hipStreamSynchronize(s);
         (void)hipStreamSynchronize(cp);
         return rc;
     }
-    // host queries: the caller may free them once the call returns
+    // the pinned query slots are free for the next call once their DMA is done
     if (!in_dev) NBKD_HIP(hipStreamSynchronize(cp));
     return NBKD_OK;
+}
+
+// device scratch per query of one batch call that no budget bounds: the
+// order / seed / list / failure buffers (~40 B), plus the full rows the k-th
+// distance takes where the collect / select path does not run (k > 1024, the
+// empty tree): kth_locked.  The candidate columns are budgeted
+// (cand_budget) and not counted here.
+static size_t knn_scratch_per_query(const Tree &t, int k, bool kth) {
+    size_t b = 40;
+    if (kth && !(k <= KNN_PACKET_KMAX && t.ginfo && seed_params(t, k).on && !collect_disabled()))
+        b += (size_t)k * 8;
+    return b;
 }
 
 nbkd_status query_knn(const Tree &t, const float *q, uint64_t m, int k, float *out_d,
                       uint32_t *out_i, uint32_t flags, hipStream_t s) {
     nbkd_status rc = knn_args(k, m);
     if (rc || m == 0) return rc;
+    if (stats_enabled()) stats_reset(); // this call's counters, summed over its batches
     Workspace &ws = acquire_ws(t);
     WsCall call(ws, s, std::adopt_lock);
     NBKD_HIP(call.err);
@@ -1284,7 +1349,7 @@ nbkd_status query_knn(const Tree &t, const float *q, uint64_t m, int k, float *o
     if ((flags & dev_io) == dev_io) return knn_locked(t, ws, q, m, k, out_d, out_i, flags, s);
     const size_t ob[2] = {(size_t)k * 4, (size_t)k * 4};
     void *const outs[2] = {out_d, out_i};
-    return host_pipeline(ws, q, m, flags, 2, ob, outs,
+    return host_pipeline(ws, q, m, flags, 2, ob, outs, knn_scratch_per_query(t, k, false),
                          [&](const float *dq, uint64_t nb, void *const *o, hipStream_t st) {
                              return knn_locked(t, ws, dq, nb, k, (float *)o[0], (uint32_t *)o[1],
                                                flags | dev_io, st);
@@ -1312,6 +1377,7 @@ nbkd_status query_kth(const Tree &t, const float *q, uint64_t m, int k, float *o
                       uint32_t flags, hipStream_t s) {
     nbkd_status rc = knn_args(k, m);
     if (rc || m == 0) return rc;
+    if (stats_enabled()) stats_reset(); // this call's counters, summed over its batches
     Workspace &ws = acquire_ws(t);
     WsCall call(ws, s, std::adopt_lock);
     NBKD_HIP(call.err);
@@ -1319,7 +1385,7 @@ nbkd_status query_kth(const Tree &t, const float *q, uint64_t m, int k, float *o
     if ((flags & dev_io) == dev_io) return kth_locked(t, ws, q, m, k, out_d, flags, s);
     const size_t ob[1] = {4};
     void *const outs[1] = {out_d};
-    return host_pipeline(ws, q, m, flags, 1, ob, outs,
+    return host_pipeline(ws, q, m, flags, 1, ob, outs, knn_scratch_per_query(t, k, true),
                          [&](const float *dq, uint64_t nb, void *const *o, hipStream_t st) {
                              return kth_locked(t, ws, dq, nb, k, (float *)o[0], flags | dev_io, st);
                          }, s);
@@ -1433,7 +1499,7 @@ nbkd_status query_ball_count(const Tree &t, const float *q, uint64_t m, float r,
         return ball_common(t, ws, q, m, r, out_count, nullptr, nullptr, 0, flags, s);
     const size_t ob[1] = {4};
     void *const outs[1] = {out_count};
-    return host_pipeline(ws, q, m, flags, 1, ob, outs,
+    return host_pipeline(ws, q, m, flags, 1, ob, outs, 40,
                          [&](const float *dq, uint64_t nb, void *const *o, hipStream_t st) {
                              return ball_common(t, ws, dq, nb, r, (uint32_t *)o[0], nullptr,
                                                 nullptr, 0, flags | dev_io, st);

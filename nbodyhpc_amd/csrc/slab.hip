@@ -399,6 +399,31 @@ nbkd_status nbkd_slab_forward(const float *q, const float *dist, uint64_t m, int
     SLAB_CATCH
 }
 
+nbkd_status nbkd_slab_forward_async(const float *q, const float *dist, uint64_t m, int32_t k,
+                                    float cl, float ch, uint32_t *out_list, uint8_t *out_sides,
+                                    uint64_t capacity, uint64_t *count, int32_t device,
+                                    void *stream) {
+    SLAB_TRY
+    if (!count || k <= 0 || (m > 0 && (!q || !dist)) || (capacity > 0 && (!out_list || !out_sides))) {
+        set_error("nbkd_slab_forward_async: bad argument");
+        return NBKD_EINVAL;
+    }
+    DevGuard g(device);
+    hipStream_t s = (hipStream_t)stream;
+    // the count lives in device memory the caller owns: no allocation, no
+    // wait (nbkd_slab_forward's scratch word costs a hipFree, a device sync)
+    NBKD_HIP(hipMemsetAsync(count, 0, 8, s));
+    if (m == 0) return NBKD_OK;
+    const float mag = std::fmax(std::fabs(cl), std::fabs(ch));
+    const float slack = 4.0f * (std::nextafter(mag, INFINITY) - mag);
+    const unsigned blocks = (unsigned)std::min<uint64_t>((m + 255) / 256, 65536);
+    forward_kernel<<<blocks, 256, 0, s>>>(q, dist, m, k, cl, ch, slack, out_list, out_sides,
+                                          capacity, (unsigned long long *)count);
+    NBKD_HIP(hipGetLastError());
+    return NBKD_OK;
+    SLAB_CATCH
+}
+
 static nbkd_status rows_common(const void *src, uint64_t row_bytes, const uint32_t *idx, uint64_t n,
                                void *dst, int32_t device, void *stream, bool scatter) {
     if (row_bytes == 0 || row_bytes % 4 != 0 || (n > 0 && (!src || !idx || !dst))) {

@@ -28,6 +28,9 @@ def _hip():
         L.hipMalloc.argtypes = [ctypes.POINTER(vp), sz]
         L.hipFree.argtypes = [vp]
         L.hipMemcpy.argtypes = [vp, vp, sz, ctypes.c_int]
+        L.hipMemcpyAsync.argtypes = [vp, vp, sz, ctypes.c_int, vp]
+        L.hipHostMalloc.argtypes = [ctypes.POINTER(vp), sz, ctypes.c_uint]
+        L.hipHostFree.argtypes = [vp]
         L.hipMemset.argtypes = [vp, ctypes.c_int, sz]
         L.hipMemGetInfo.argtypes = [ctypes.POINTER(sz), ctypes.POINTER(sz)]
         L.hipDeviceSynchronize.argtypes = []
@@ -145,6 +148,36 @@ def memcpy(dst_ptr, src_ptr, nbytes, kind=D2D):
         _ok(_hip().hipMemcpy(dst_ptr, src_ptr, int(nbytes), int(kind)), "hipMemcpy")
 
 
+def memcpy_async(dst_ptr, src_ptr, nbytes, kind, stream_handle):
+    """hipMemcpyAsync on a stream (with pinned host memory a true async copy)."""
+    if nbytes:
+        _ok(_hip().hipMemcpyAsync(dst_ptr, src_ptr, int(nbytes), int(kind), stream_handle),
+            "hipMemcpyAsync")
+
+
+class HostBuffer:
+    """Pinned host memory (hipHostMalloc) viewed as a numpy array."""
+
+    def __init__(self, shape, dtype):
+        self.dtype = np.dtype(dtype)
+        self.shape = tuple(int(s) for s in np.atleast_1d(shape))
+        self.nbytes = int(np.prod(self.shape)) * self.dtype.itemsize
+        p = ctypes.c_void_p()
+        _ok(_hip().hipHostMalloc(ctypes.byref(p), max(self.nbytes, 16), 0), "hipHostMalloc")
+        self.ptr = p.value
+        buf = (ctypes.c_char * max(self.nbytes, 16)).from_address(self.ptr)
+        self.array = np.frombuffer(buf, self.dtype, count=int(np.prod(self.shape))).reshape(
+            self.shape)
+
+    def free(self):
+        if getattr(self, "ptr", None):
+            self.array = None
+            _hip().hipHostFree(self.ptr)
+            self.ptr = None
+
+    __del__ = free
+
+
 class Stream:
     def __init__(self):
         s = ctypes.c_void_p()
@@ -170,7 +203,11 @@ class Event:
         self.handle = e.value
 
     def record(self, stream=None):
-        _ok(_hip().hipEventRecord(self.handle, stream.handle if stream else None), "hipEventRecord")
+        h = stream.handle if isinstance(stream, Stream) else stream
+        _ok(_hip().hipEventRecord(self.handle, h), "hipEventRecord")
+
+    def synchronize(self):
+        _ok(_hip().hipEventSynchronize(self.handle), "hipEventSynchronize")
 
     def elapsed_ms(self, end: "Event") -> float:
         _ok(_hip().hipEventSynchronize(end.handle), "hipEventSynchronize")

@@ -49,13 +49,14 @@ pass() { # dir counter knn_time args...  (every kernel, no regex)
 }
 steps4() { # dir knn_time args...: the 1- and 3-step FETCH / WRITE passes
   local d=$1; shift
+  mkdir -p $O/$d
   pass $d/f1 FETCH_SIZE "$@" --steps 1 && pass $d/f3 FETCH_SIZE "$@" --steps 3 \
     && pass $d/w1 WRITE_SIZE "$@" --steps 1 && pass $d/w3 WRITE_SIZE "$@" --steps 3
 }
 
 step_tests() {
   say tests
-  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+  NBKD_TEST_REPORT_DIR=$O timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
     > $O/tests.log 2>&1
   local rc=$?
   tail -3 $O/tests.log
@@ -100,6 +101,9 @@ step_slab() {
     IFS=: read w sc n <<< "$s"
     steps4 slab_${w}_${sc} --n ${n:-1e8} --k 32 --slab-world $w --slab-rank 0 --scaling $sc || return $?
   done
+  # summarised on the box too, so a later `rehearse` step of this call finds
+  # the profile of this very build (profiles/ is not merged back: copy it)
+  python3 scripts/summarize_slab.py $O $TAG && cp profiles/${TAG}_pmc_slab.json $O/
 }
 step_rehearse() {
   local w

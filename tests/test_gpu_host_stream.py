@@ -153,3 +153,30 @@ def test_concurrent_queries_on_one_tree(gpu):
     assert not errs, errs
     for j in range(len(qs)):
         assert_knn_equal(out[j][0], out[j][1], serial[j][0], serial[j][1], pts, qs[j], 1.0)
+
+
+def test_stats_sum_over_host_batches(gpu, small_host_batch):
+    """A host-buffer call's work counters cover every batch (each
+    batch used to overwrite the last), equal to one device-buffer call's."""
+    from nbodyhpc_amd import hip, synth
+    pts = synth.uniform(200_000, 71, 1.0)
+    m, k = 40_000, 16  # 10 batches of 4096
+    q = synth.uniform(m, 72, 1.0)
+    t = gpu.Tree(pts, leafsize=64, boxsize=1.0)
+    gpu.stats_enable(True)
+    try:
+        t.query(q, k)
+        host = gpu.stats_read_all()
+        dq = hip.DeviceArray.from_numpy(q)
+        od = hip.DeviceArray((m, k), np.float32)
+        oi = hip.DeviceArray((m, k), np.uint32)
+        gpu.set_tuning("host_batch", 0)
+        t.query_device(dq.ptr, m, k, od.ptr, oi.ptr)
+        hip.synchronize()
+        dev = gpu.stats_read_all()
+    finally:
+        gpu.stats_enable(False)
+    # packets of 64 kd-ordered queries: every batch's, at least m / 64 in all
+    assert host["packets"] >= m // 64 and dev["packets"] >= m // 64
+    assert abs(host["candidates"] - dev["candidates"]) < 0.1 * dev["candidates"]
+    t.close()

@@ -308,6 +308,27 @@ def test_knn_seed_retry(gpu, oracle, tuning, box):
     assert_knn_equal(d, i, dr, ir, pts, q, box)
 
 
+def test_retry_rounds_take_failures_past_ten_percent(gpu, oracle, tuning):
+    """with more than 10 % of the first pass failing (a small seed
+    margin), round 1 takes them all in its batches, so the exact lane-per-query
+    kernel sees few queries (round 4 sent everything past ~10 % + ~1 % there)."""
+    tuning("knn_seed_margin", 0.5)
+    pts = uniform(400_000, 33)
+    q = pts[:200_000]
+    t = gpu.Tree(pts, leafsize=64, boxsize=1.0)
+    gpu.stats_enable(True)
+    try:
+        d, i = t.query(q, 32)
+        st = gpu.stats_read_all()
+    finally:
+        gpu.stats_enable(False)
+    assert st["retry_queries"] > 0.1 * len(q), st  # the case the advice names
+    assert st["fallback_queries"] < 0.001 * len(q), st
+    sel = np.arange(0, len(q), 97)
+    dr, ir = oracle.tree(pts, 64, 1.0).query(q[sel], 32, workers=16)
+    assert_knn_equal(d[sel], i[sel], dr, ir, pts, q[sel], 1.0)
+
+
 def test_squared_output(gpu, oracle):
     """NBKD_SQUARED: the d2 the rows are sorted by (kdtree.cpp:149-151), whose
     sqrtf is the plain output, bit for bit (collect/select, exact and k > 64)."""
