@@ -310,6 +310,19 @@ STATS_NAMES = ("node_visits", "pair_evals", "leaves_reached", "sparse_iters", "p
                "chunk_lanes")
 
 
+# the same slots after a radius count with stats enabled (ball.hip STATS instance)
+BALL_STATS_NAMES = ("node_visits", "points_evaluated", "leaves_needed", "transposed_steps",
+                    "points_staged", "packets", "full_lane_leaves", "partial_lane_leaves",
+                    "lane_loop_chunks", "unused9", "clk_walk", "clk_leaf_test", "clk_wait",
+                    "clk_transposed", "clk_lane_loop", "unused15", "unused16")
+
+
+def ball_stats_read_all():
+    arr = (_u64 * len(BALL_STATS_NAMES))()
+    _check(lib().nbkd_stats_read_all(arr, len(BALL_STATS_NAMES)))
+    return dict(zip(BALL_STATS_NAMES, [int(v) for v in arr]))
+
+
 def stats_read_all():
     arr = (_u64 * len(STATS_NAMES))()
     _check(lib().nbkd_stats_read_all(arr, len(STATS_NAMES)))

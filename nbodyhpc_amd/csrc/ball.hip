@@ -69,13 +69,19 @@ constexpr int BALL_OCC[2][2] = {{8, 8}, {8, 8}};
 
 // the packet's walk and leaf scans (M: the metric's formulas, plain for a
 // packet whose balls all clear the box faces, ball_packet_kernel)
-template <bool PER, bool M, bool FILL>
+// STATS (count mode, the instrumented instance): bst = node visits, points
+// evaluated, leaves needed, transposed steps, points staged, full (lane, leaf)
+// pairs, partial (lane, leaf) pairs, per-lane-loop chunks, then the s_memtime
+// phase clocks walk / leaf test / staging wait / transposed steps / per-lane loop
+constexpr int BALL_NST = 13;
+template <bool PER, bool M, bool FILL, bool STATS>
 __device__ __forceinline__ void ball_walk(const DevTree &t, const uint32_t *__restrict__ linfo,
                                           float r2, const PadLeaves &pad,
                                           uint32_t *__restrict__ out_idx, uint32_t tnum,
                                           bool plain_ok, BallLds &W, const int lane,
                                           const float qx, const float qy, const float qz,
-                                          const float thr, const uint64_t wpos, uint32_t &cnt) {
+                                          const float thr, const uint64_t wpos, uint32_t &cnt,
+                                          uint32_t (&bst)[BALL_NST]) {
     const float L = t.box;
     uint32_t sk_node = 0;
     int sp = 0;
@@ -93,16 +99,25 @@ __device__ __forceinline__ void ball_walk(const DevTree &t, const uint32_t *__re
     uint64_t wm = __ballot((tm[0] + tm[1]) + tm[2] <= thr);
     bool have = wm != 0;
     nbkd_node nd = cnodes[0]; // record of `node` while `have`
-    // the shared packet walk (packet.hpp: per-axis steps, node-id stack)
-    constexpr bool STATS = false;
+    // the shared packet walk (packet.hpp: per-axis steps, node-id stack);
+    // NBKD_GWALK counts node visits in st[0]
     const float kth = thr;
-    uint64_t st[1] = {0};
-    (void)st;
+    uint32_t (&st)[BALL_NST] = bst;
+    uint64_t tclk = STATS ? clock64() : 0;
+#define NBKD_BPH(I)                                                                                \
+    do {                                                                                           \
+        if constexpr (STATS) {                                                                     \
+            const uint64_t t_ = clock64();                                                         \
+            bst[8 + (I)] += (uint32_t)(t_ - tclk);                                                 \
+            tclk = t_;                                                                             \
+        }                                                                                          \
+    } while (0)
 
     for (;;) {
         bool found;
         uint32_t lpos = 0, lend = 0;
         NBKD_GWALK(found, lpos, lend);
+        NBKD_BPH(0);
         if (!found) break;
 
         // leaf: tight box first (lanes < 6), then the chunks
@@ -118,6 +133,12 @@ __device__ __forceinline__ void ball_walk(const DevTree &t, const uint32_t *__re
         for (int j = 0; j < NBKD_PAD_LEAVES; ++j) padded |= pad.id[j] == node;
         const bool full = need && !padded && box_ub2<PER>(qx, qy, qz, tb) <= thr;
         const bool part = need && !full;
+        if constexpr (STATS) {
+            ++bst[2];
+            bst[5] += (uint32_t)__popcll(__ballot(full));
+            bst[6] += (uint32_t)__popcll(__ballot(part));
+        }
+        NBKD_BPH(1);
         if constexpr (!FILL) {
             if (full) cnt += lend - lpos;
             if (!__any(part)) continue;
@@ -128,6 +149,8 @@ __device__ __forceinline__ void ball_walk(const DevTree &t, const uint32_t *__re
             glds_f4(t.p4 + c0, W.p4, lane, cn);
             wait_vm0();
             wave_sync();
+            if constexpr (STATS) bst[4] += cn;
+            NBKD_BPH(2);
             if constexpr (FILL) {
                 if (full) {
 #pragma unroll 1
@@ -178,6 +201,12 @@ __device__ __forceinline__ void ball_walk(const DevTree &t, const uint32_t *__re
                         }
                     }
                     cnt += tc;
+                    if constexpr (STATS) {
+                        const uint32_t nst = (uint32_t)__popcll(pm);
+                        bst[3] += nst;
+                        bst[1] += nst * cn;
+                    }
+                    NBKD_BPH(3);
                     // (round 4: before, each step added its count with
                     // cnt += lane == j ? c : 0 and ballotted pv && d <= r2: 5 more
                     // VALU a step; 100.9 -> 98.3 ms at 1e8, r = 0.01, same counts,
@@ -195,16 +224,25 @@ __device__ __forceinline__ void ball_walk(const DevTree &t, const uint32_t *__re
                     }
                 }
             }
+            if constexpr (STATS) {
+                if (__any(part && !trans)) {
+                    ++bst[7];
+                    bst[1] += (uint32_t)__popcll(__ballot(part)) * cn;
+                }
+            }
+            NBKD_BPH(4);
         }
     }
+#undef NBKD_BPH
 }
 
-template <bool PER, bool FILL>
+template <bool PER, bool FILL, bool STATS>
 __global__ void __launch_bounds__(TB, BALL_OCC[PER][FILL])
 ball_packet_kernel(DevTree t, const uint32_t *__restrict__ linfo, const float *__restrict__ q,
                    const uint32_t *__restrict__ order, uint32_t m, float r2, PadLeaves pad,
                    uint32_t *__restrict__ out_count, const uint64_t *__restrict__ row_offsets,
-                   uint32_t *__restrict__ out_idx, uint32_t tnum, bool plain_ok) {
+                   uint32_t *__restrict__ out_idx, uint32_t tnum, bool plain_ok,
+                   unsigned long long *__restrict__ stats) {
     __shared__ BallLds Wl[WPB];
     // (threadIdx.x >> 6 as is: the wave-uniform wave_id() made this kernel slower,
     // 100.6 -> 104.7 ms at 1e8, profiles/r04v_ab_uniform_wave.txt)
@@ -236,13 +274,24 @@ ball_packet_kernel(DevTree t, const uint32_t *__restrict__ linfo, const float *_
                                     L - qy >= r1 && qz >= r1 && L - qz >= r1);
         plain = plain_ok && __all(wf);
     }
+    uint32_t bst[BALL_NST] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     if (plain)
-        ball_walk<PER, false, FILL>(t, linfo, r2, pad, out_idx, tnum, plain_ok, W, lane, qx, qy, qz,
-                                    thr, wpos, cnt);
+        ball_walk<PER, false, FILL, STATS>(t, linfo, r2, pad, out_idx, tnum, plain_ok, W, lane, qx,
+                                           qy, qz, thr, wpos, cnt, bst);
     else
-        ball_walk<PER, PER, FILL>(t, linfo, r2, pad, out_idx, tnum, plain_ok, W, lane, qx, qy, qz,
-                                  thr, wpos, cnt);
+        ball_walk<PER, PER, FILL, STATS>(t, linfo, r2, pad, out_idx, tnum, plain_ok, W, lane, qx,
+                                         qy, qz, thr, wpos, cnt, bst);
     if (active && out_count) out_count[qo] = cnt;
+    if constexpr (STATS) {
+        // the nbkd_stats_read_all slots of a radius count (capi.BALL_STATS_NAMES)
+        constexpr int slot[BALL_NST] = {0, 1, 2, 3, 4, 6, 7, 8, 10, 11, 12, 13, 14};
+        if (lane == 0) {
+#pragma unroll
+            for (int i = 0; i < BALL_NST; ++i)
+                atomicAdd(&stats[slot[i]], (unsigned long long)bst[i]);
+            atomicAdd(&stats[5], 1ull);
+        }
+    }
 }
 
 // Periodic queries outside [0, L]^3 (unvalidated input, as in the reference's
@@ -337,7 +386,7 @@ void launch_ball_outside(const Tree &t, const float *q, const uint32_t *list, ui
 
 void launch_ball_packet(const Tree &t, const float *q, const uint32_t *order, uint32_t m, float r2,
                         uint32_t *out_count, const uint64_t *row_offsets, uint32_t *out_idx,
-                        hipStream_t s) {
+                        unsigned long long *stats, hipStream_t s) {
     const unsigned blocks = (unsigned)((m + TB - 1) / TB);
     // transposed count threshold (x/8 partial lanes per staged point); 0 = off
     static const uint32_t tnum = [] {
@@ -352,14 +401,18 @@ void launch_ball_packet(const Tree &t, const float *q, const uint32_t *order, ui
     PadLeaves pad;
     for (int j = 0; j < NBKD_PAD_LEAVES; ++j)
         pad.id[j] = t.npad_leaves <= NBKD_PAD_LEAVES ? t.pad_leaves[j] : 0xFFFFFFFFu;
-#define NBKD_BALL(PER, FILL)                                                                   \
-    ball_packet_kernel<PER, FILL><<<blocks, TB, 0, s>>>(view(t), t.leafinfo, q, order, m, r2,  \
-                                                        pad, out_count, row_offsets, out_idx, \
-                                                        tnum, plain_ok)
+#define NBKD_BALL(PER, FILL, STATS)                                                            \
+    ball_packet_kernel<PER, FILL, STATS><<<blocks, TB, 0, s>>>(                                \
+        view(t), t.leafinfo, q, order, m, r2, pad, out_count, row_offsets, out_idx, tnum,      \
+        plain_ok, stats)
     if (t.periodic) {
-        if (out_idx) NBKD_BALL(true, true); else NBKD_BALL(true, false);
+        if (out_idx) NBKD_BALL(true, true, false);
+        else if (stats) NBKD_BALL(true, false, true);
+        else NBKD_BALL(true, false, false);
     } else {
-        if (out_idx) NBKD_BALL(false, true); else NBKD_BALL(false, false);
+        if (out_idx) NBKD_BALL(false, true, false);
+        else if (stats) NBKD_BALL(false, false, true);
+        else NBKD_BALL(false, false, false);
     }
 #undef NBKD_BALL
 }

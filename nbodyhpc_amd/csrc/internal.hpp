@@ -315,9 +315,11 @@ nbkd_status launch_knn_collect(const Tree &t, const float *q, const uint32_t *or
 
 // ball.hip: radius count (out_idx == nullptr) or CSR fill over m kd-ordered
 // queries (periodic queries outside [0, L]^3 are skipped: query.hip answers them)
+// (stats != nullptr, count mode: the instrumented instance adds its work
+// counters and phase clocks there, capi.BALL_STATS_NAMES)
 void launch_ball_packet(const Tree &t, const float *q, const uint32_t *order, uint32_t m, float r2,
                         uint32_t *out_count, const uint64_t *row_offsets, uint32_t *out_idx,
-                        hipStream_t s);
+                        unsigned long long *stats, hipStream_t s);
 // the listed periodic queries outside [0, L]^3, every point tested (fill: nout
 // zeroed scratch words when out_idx is set)
 // count mode with the list's length in device memory (no host read)

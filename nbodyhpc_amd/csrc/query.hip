@@ -1425,8 +1425,14 @@ static nbkd_status ball_common(const Tree &t, Workspace &ws, const float *q, uin
             NBKD_HIP(hipStreamSynchronize(s));
         }
     }
+    unsigned long long *stats = nullptr;
+    if (count_only && stats_enabled()) {
+        stats = (unsigned long long *)ws.get(WS_STATS, NBKD_NSTATS * 8, s);
+        if (!stats) return NBKD_ENOMEM;
+        NBKD_HIP(hipMemsetAsync(stats, 0, NBKD_NSTATS * 8, s));
+    }
     auto run = [&](uint32_t *c, const uint64_t *off, uint32_t *idx) -> nbkd_status {
-        launch_ball_packet(t, dq, ord, mm, r2, c, off, idx, s);
+        launch_ball_packet(t, dq, ord, mm, r2, c, off, idx, idx ? nullptr : stats, s);
         if (count_only && list)
             launch_ball_outside_dev(t, dq, list, list + mm, r2, c, s);
         else
@@ -1444,6 +1450,12 @@ static nbkd_status ball_common(const Tree &t, Workspace &ws, const float *q, uin
         TimedScope ts("ball_count", s);
         rc = run(cnt, nullptr, nullptr);
         if (rc) return rc;
+    }
+    if (stats) {
+        uint64_t h[NBKD_NSTATS];
+        NBKD_HIP(hipMemcpyAsync(h, stats, NBKD_NSTATS * 8, hipMemcpyDeviceToHost, s));
+        NBKD_HIP(hipStreamSynchronize(s));
+        stats_add(h);
     }
     if (!offsets) { // count-only
         if (!dev_out) {
@@ -1491,6 +1503,7 @@ nbkd_status query_ball_count(const Tree &t, const float *q, uint64_t m, float r,
         return NBKD_EINVAL;
     }
     if (m == 0) return NBKD_OK;
+    if (stats_enabled()) stats_reset();
     Workspace &ws = acquire_ws(t);
     WsCall call(ws, s, std::adopt_lock);
     NBKD_HIP(call.err);

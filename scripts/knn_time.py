@@ -22,7 +22,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from nbodyhpc_amd import capi, hip, synth  # noqa: E402
 
 PHASES = ("leaf_key", "sort", "knn_collect", "knn_select", "knn_retry", "knn_retry_order",
-          "knn_fallback", "knn")
+          "knn_fallback", "knn", "ball_count")
 
 
 def slab_points(a, k):
@@ -70,6 +70,8 @@ def main():
     ap.add_argument("--slab-rank", type=int, default=0)
     ap.add_argument("--scaling", choices=("strong", "weak"), default="strong")
     ap.add_argument("--seed", type=int, default=20261015)
+    ap.add_argument("--stats", action="store_true",
+                    help="one more (untimed) pass with the work counters and phase clocks on")
     a = ap.parse_args()
     hip.preload()
     hip.set_device(0)
@@ -115,6 +117,13 @@ def main():
         ms, cnt = capi.timing_read(p)
         ph[p] = round(ms / a.steps, 3)
     capi.timing_enable(False)
+    st = None
+    if a.stats:
+        capi.stats_enable(True)
+        run()
+        s.synchronize()
+        st = capi.ball_stats_read_all() if a.ball > 0 else capi.stats_read_all()
+        capi.stats_enable(False)
     h = hashlib.sha256(od.numpy().tobytes())
     if oi is not None:
         h.update(oi.numpy().tobytes())
@@ -123,7 +132,7 @@ def main():
                       "slab_rank": a.slab_rank, "scaling": a.scaling, "n_arg": int(a.n),
                       "seed": a.seed, "k": k, "leaf": a.leaf, "lognormal": a.lognormal,
                       "kth": a.kth, "ball": a.ball, "wall_ms": round(wall, 3), "qps": n / wall * 1e3,
-                      "phases_ms": ph, "sha": h.hexdigest()[:16]}), flush=True)
+                      "phases_ms": ph, "sha": h.hexdigest()[:16], "stats": st}), flush=True)
 
 
 if __name__ == "__main__":
