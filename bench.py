@@ -952,6 +952,7 @@ def main():
         # time is in the step's wall clock
         capi.timing_enable(False)
         capi.stats_enable(False)
+        rows_b[j].wait()  # the count is behind that step's kNN: not the round's own time
         t_r = time.perf_counter()
         st = slab.second_round(rows_b[j], rank, world, ds.bounds, L, ds.h, k, dist)
         sr_acc["host_s"] += time.perf_counter() - t_r
@@ -1062,7 +1063,8 @@ def main():
             "forwards_per_step": allsum(float(sr_timed["forwards"])) / max(args.steps, 1),
             "max_hops": int(allmax(float(sr_timed["hops"]))),
             # overlapped with the next step's kNN (pipelined steps); the host's
-            # time in it, and the step time over the same steps without it
+            # time in it once the count is known (agreement over gloo, any
+            # forwarded rows), and the step time over the same steps without it
             "host_ms_per_step": allmax(sr_timed["host_s"]) / args.steps * 1e3,
             "ms_per_step": (elapsed_max / args.steps - knn_only) * 1e3,
             "knn_only_ms_per_step": knn_only * 1e3,

@@ -482,26 +482,22 @@ __device__ __forceinline__ void issue_block(const uint4 *b4, uint4 *lds4, int la
 }
 
 // One lane per query: the k smallest of its candidate column, sorted, as rows.
+template <int KC> constexpr int select_stage_words() {
+    return (KC < 32 ? KC : 32) < 32 ? 32 * 64 : (KC < 32 ? KC : 32) * 64; // >= 8 KB: one block
+}
+
+// the 64 queries of wave-block wb (m: the pass's query count)
 template <int KC, bool PER, bool WHOLE>
-__global__ void __launch_bounds__(TB, KC <= 32 ? 4 : 2)
-knn_select_kernel(DevTree t, const float *__restrict__ q, const uint32_t *__restrict__ order,
-                  QSpan span, int k, uint32_t qpp, const uint2 *__restrict__ cand, uint32_t capg,
-                  const uint32_t *__restrict__ ccount, float *__restrict__ out_d,
-                  uint32_t *__restrict__ out_i, uint32_t *__restrict__ fail_list,
-                  uint32_t *__restrict__ fail_count, uint32_t pos_base, uint64_t all_rows,
-                  float *__restrict__ tg_fix, float mu, bool sq, uint32_t *__restrict__ fail_bits) {
+__device__ __forceinline__ void
+select_block(const DevTree &t, const float *__restrict__ q, const uint32_t *__restrict__ order,
+             uint32_t m, uint32_t wb, int k, const uint2 *__restrict__ cand, uint32_t capg,
+             const uint32_t *__restrict__ ccount, float *__restrict__ out_d,
+             uint32_t *__restrict__ out_i, uint32_t *__restrict__ fail_list,
+             uint32_t *__restrict__ fail_count, uint32_t pos_base, uint64_t all_rows,
+             float *__restrict__ tg_fix, float mu, bool sq, uint32_t *__restrict__ fail_bits,
+             uint32_t *stage, uint32_t *rowq, const int lane) {
     constexpr int NS = 16;                  // candidates merged per pass
     constexpr int CC = KC < 32 ? KC : 32;   // top-k registers staged per output pass
-    constexpr int SW = CC < 32 ? 32 * 64 : CC * 64; // >= 8 KB: one candidate block
-    __shared__ uint32_t stage_all[WPB][SW];
-    __shared__ uint32_t rowq_all[WPB][64];
-    const int lane = threadIdx.x & 63, wave = wave_id();
-    uint32_t *stage = stage_all[wave], *rowq = rowq_all[wave];
-    // a device-counted pass (retry rounds) is launched for its cap and reads
-    // its count here (a loop over blocks made the compiler spill td / ti)
-    const uint32_t m = span_m(span);
-    const uint32_t wb = blockIdx.x * WPB + wave;
-    if (wb * 64u >= m) return;
     // lane = one query gq; its candidates: packet gq / qpp, row gq % qpp
     const uint32_t gq = wb * 64u + lane;
     const bool valid = gq < m;
@@ -622,6 +618,43 @@ knn_select_kernel(DevTree t, const float *__restrict__ q, const uint32_t *__rest
         for (int j = 0; j < CC; ++j) stage[j * 64 + (lane ^ j)] = ti[j0 + j];
         wave_sync();
         store_rows<CC>(stage, rowq, out_i, k, j0 - (KC - k), lane);
+    }
+}
+
+// A static pass launches one wave per 64 queries; a device-counted pass (the
+// retry rounds: LOOP) a grid of at most resident_blocks() blocks that strides
+// over its wave-blocks, so a pass whose count is zero (round 1 is launched in
+// batches enough for every query failing) costs one short launch,
+// not its cap's worth of workgroups.  Only the LOOP instance carries the loop,
+// at half the occupancy: at the static instance's 128 VGPRs (k <= 32) the
+// loop spilled ~300 B per lane; the static instance keeps 4 waves per SIMD.
+template <int KC, bool PER, bool WHOLE, bool LOOP>
+__global__ void __launch_bounds__(TB, (KC <= 32 ? 4 : 2) / (LOOP ? 2 : 1))
+knn_select_kernel(DevTree t, const float *__restrict__ q, const uint32_t *__restrict__ order,
+                  QSpan span, int k, uint32_t qpp, const uint2 *__restrict__ cand, uint32_t capg,
+                  const uint32_t *__restrict__ ccount, float *__restrict__ out_d,
+                  uint32_t *__restrict__ out_i, uint32_t *__restrict__ fail_list,
+                  uint32_t *__restrict__ fail_count, uint32_t pos_base, uint64_t all_rows,
+                  float *__restrict__ tg_fix, float mu, bool sq, uint32_t *__restrict__ fail_bits) {
+    constexpr int SW = select_stage_words<KC>();
+    __shared__ uint32_t stage_all[WPB][SW];
+    __shared__ uint32_t rowq_all[WPB][64];
+    const int lane = threadIdx.x & 63, wave = wave_id();
+    uint32_t *stage = stage_all[wave], *rowq = rowq_all[wave];
+    const uint32_t m = span_m(span);
+    if constexpr (LOOP) {
+        for (uint32_t wb = blockIdx.x * WPB + wave; wb * 64u < m; wb += gridDim.x * WPB) {
+            wave_sync(); // the previous wave-block's LDS reads are done
+            select_block<KC, PER, WHOLE>(t, q, order, m, wb, k, cand, capg, ccount, out_d, out_i,
+                                         fail_list, fail_count, pos_base, all_rows, tg_fix, mu,
+                                         sq, fail_bits, stage, rowq, lane);
+        }
+    } else {
+        const uint32_t wb = blockIdx.x * WPB + wave;
+        if (wb * 64u >= m) return;
+        select_block<KC, PER, WHOLE>(t, q, order, m, wb, k, cand, capg, ccount, out_d, out_i,
+                                     fail_list, fail_count, pos_base, all_rows, tg_fix, mu, sq,
+                                     fail_bits, stage, rowq, lane);
     }
 }
 
@@ -1015,20 +1048,32 @@ void launch_select(const Tree &t, const float *q, const uint32_t *order, QSpan s
                    float *od, uint32_t *oi, uint32_t *fail_list, uint32_t *fail_count,
                    uint32_t *fail_bits, uint32_t pos_base, float *tg_fix, float mu, bool sq,
                    hipStream_t s) {
-    const unsigned blocks = (span.m + TB - 1) / TB; // device-counted: sized by the cap
+    // a device-counted pass: at most resident_blocks() blocks striding over
+    // its wave-blocks (LOOP); a static one: one wave per 64 queries
+    const unsigned blocks =
+        span.count ? (unsigned)std::min<uint64_t>((span.m + TB - 1) / TB, resident_blocks())
+                   : (span.m + TB - 1) / TB;
     static const uint64_t all_rows = [] { // NBKD_SELECT_ROWMASK=0: read whole blocks
         const char *e = knob("NBKD_SELECT_ROWMASK");
         return (e && atoi(e) == 0) ? ~0ull : 0ull;
     }();
-#define NBKD_SELECT(PER, WH)                                                                       \
-    knn_select_kernel<KC, PER, WH><<<blocks, TB, 0, s>>>(view(t), q, order, span, k, qpp, cand,    \
-                                                        capg, ccount, od, oi, fail_list,           \
-                                                        fail_count, pos_base, all_rows, tg_fix,    \
-                                                        mu, sq, fail_bits)
-    if (t.periodic) {
-        if (qpp == 64) NBKD_SELECT(true, true); else NBKD_SELECT(true, false);
+#define NBKD_SELECT(PER, WH, LP)                                                                   \
+    knn_select_kernel<KC, PER, WH, LP><<<blocks, TB, 0, s>>>(view(t), q, order, span, k, qpp,     \
+                                                            cand, capg, ccount, od, oi, fail_list, \
+                                                            fail_count, pos_base, all_rows,        \
+                                                            tg_fix, mu, sq, fail_bits)
+    if (span.count) {
+        if (t.periodic) {
+            if (qpp == 64) NBKD_SELECT(true, true, true); else NBKD_SELECT(true, false, true);
+        } else {
+            if (qpp == 64) NBKD_SELECT(false, true, true); else NBKD_SELECT(false, false, true);
+        }
     } else {
-        if (qpp == 64) NBKD_SELECT(false, true); else NBKD_SELECT(false, false);
+        if (t.periodic) {
+            if (qpp == 64) NBKD_SELECT(true, true, false); else NBKD_SELECT(true, false, false);
+        } else {
+            if (qpp == 64) NBKD_SELECT(false, true, false); else NBKD_SELECT(false, false, false);
+        }
     }
 #undef NBKD_SELECT
 }

@@ -853,8 +853,13 @@ class DeviceRows:
         self._ev.record(self.stream)
         self._pending = (float(np.float32(cl)), float(np.float32(ch)))
 
+    def wait(self):
+        """Block until the count of the last start() is in host memory."""
+        if self._pending is not None:
+            self._ev.synchronize()
+
     def forward(self, cl, ch):
-        from . import capi, hip
+        from . import capi
 
         ds = self.ds
         dptr, kk = (self.kth_ptr, 1) if self.kth_ptr is not None else (self.od_ptr, self.k)

@@ -17,6 +17,7 @@
 #   rehearse  N > 1 bench lines with every rank on this GPU (NBKD_BENCH_SAME_DEVICE=1)
 #   ab        scripts/gpu_ab.sh with LIBS / BALL_LIBS / ARGS / ROUNDS
 #   final     smoke() + the default bench line
+#   probe     each command of PROBE ("cmd1; cmd2; ..."), 600 s each, into probe.log
 # Afterwards, in the build container:
 #   python scripts/summarize_prof.py gpurun_out/$TAG $TAG     (trace, pmc)
 #   python scripts/summarize_step.py gpurun_out/$TAG $TAG     (step)
@@ -126,6 +127,17 @@ step_final() {
   local rc=$?
   tail -2 $O/final_smoke.log; tail -c 1500 $O/final_bench.json
   return $rc
+}
+
+step_probe() {
+  local c
+  IFS=';' read -ra cmds <<< "$PROBE"
+  for c in "${cmds[@]}"; do
+    say "probe: $c"
+    echo "### $c" >> $O/probe.log
+    timeout -k 10 600 $c >> $O/probe.log 2>&1 || return $?
+  done
+  tail -c 3000 $O/probe.log
 }
 
 rc=0
