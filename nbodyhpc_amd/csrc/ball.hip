@@ -120,11 +120,13 @@ __device__ __forceinline__ void ball_walk(const DevTree &t, const uint32_t *__re
         NBKD_BPH(0);
         if (!found) break;
 
-        // leaf: tight box first (lanes < 6), then the chunks
-        const uint32_t iw = lane < 6 ? linfo[8 * (size_t)node + lane] : 0u;
-        const float tb[6] = {rdlane(__uint_as_float(iw), 0), rdlane(__uint_as_float(iw), 3),
-                             rdlane(__uint_as_float(iw), 1), rdlane(__uint_as_float(iw), 4),
-                             rdlane(__uint_as_float(iw), 2), rdlane(__uint_as_float(iw), 5)};
+        // leaf: its tight box first (leafinfo words lo.xyz, hi.xyz: one
+        // s_load_dwordx8 through the scalar cache, straight into SGPRs), then
+        // the chunks.  Round 4 loaded it per lane (lanes < 6, a vector load
+        // and six v_readlane): the leaf test was 23 % of the kernel's wave
+        // clocks at 1e8, r = 0.01 (profiles/r05c_probes.txt, stats pass)
+        const NodeBox lb_ = ((cbox_ptr)linfo)[node];
+        const float tb[6] = {lb_.b[0], lb_.b[3], lb_.b[1], lb_.b[4], lb_.b[2], lb_.b[5]};
         const bool need = box_lb2<M>(qx, qy, qz, tb, L) <= thr;
         if (!__any(need)) continue;
         // a leaf holding padding points (FLT_MAX, never inside) is always evaluated
@@ -182,6 +184,29 @@ __device__ __forceinline__ void ball_walk(const DevTree &t, const uint32_t *__re
                     // periodic leaves no partial query wraps around: the plain d2
                     // has the same bits (wrap_free), 8 VALU instead of 14 a step
                     if (!M || (plain_ok && __all(!part || wrap_free(qx, qy, qz, tb, L)))) {
+#if NBKD_BALL_PAIR
+                        // two queries a step: two independent chains in flight
+                        while (rem) {
+                            const int j = __builtin_ctzll(rem);
+                            rem &= rem - 1;
+                            const float4 sq = W.qs[j]; // LDS broadcast
+                            if (rem) {
+                                const int j2 = __builtin_ctzll(rem);
+                                rem &= rem - 1;
+                                const float4 sq2 = W.qs[j2];
+                                const float d = point_d2_fast<false>(sq.x, sq.y, sq.z, px, py, pz, L);
+                                const float d2 = point_d2_fast<false>(sq2.x, sq2.y, sq2.z, px, py, pz, L);
+                                const uint32_t c = (uint32_t)__popcll(__ballot(d <= r2) & pvm);
+                                const uint32_t c2 = (uint32_t)__popcll(__ballot(d2 <= r2) & pvm);
+                                lane_write(tc, c, j);
+                                lane_write(tc, c2, j2);
+                            } else {
+                                const float d = point_d2_fast<false>(sq.x, sq.y, sq.z, px, py, pz, L);
+                                const uint32_t c = (uint32_t)__popcll(__ballot(d <= r2) & pvm);
+                                lane_write(tc, c, j);
+                            }
+                        }
+#else
                         while (rem) {
                             const int j = __builtin_ctzll(rem);
                             rem &= rem - 1;
@@ -190,6 +215,7 @@ __device__ __forceinline__ void ball_walk(const DevTree &t, const uint32_t *__re
                             const uint32_t c = (uint32_t)__popcll(__ballot(d <= r2) & pvm);
                             lane_write(tc, c, j);
                         }
+#endif
                     } else {
                         while (rem) {
                             const int j = __builtin_ctzll(rem);

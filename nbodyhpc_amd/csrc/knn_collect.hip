@@ -1102,6 +1102,18 @@ nbkd_status launch_knn_collect(const Tree &t, const float *q, const uint32_t *or
                                uint32_t *fail_list, uint32_t *fail_count, uint32_t *fail_bits,
                                uint32_t pos_base, bool retry, bool fix_seed, bool sq, float *kb,
                                unsigned long long *stats, hipStream_t s) {
+    nbkd_status rc = launch_collect_pass(t, q, order, span, k, tg, seed_mul, qpp, cand, capg,
+                                         ccount, retry, kb, stats, s);
+    if (rc) return rc;
+    return launch_select_pass(t, q, order, span, k, tg, qpp, cand, capg, ccount, od, oi,
+                              fail_list, fail_count, fail_bits, pos_base, retry, fix_seed, sq, kb,
+                              s);
+}
+
+nbkd_status launch_collect_pass(const Tree &t, const float *q, const uint32_t *order, QSpan span,
+                                int k, const float *tg, float seed_mul, uint32_t qpp, uint2 *cand,
+                                uint32_t capg, uint32_t *ccount, bool retry, float *kb,
+                                unsigned long long *stats, hipStream_t s) {
     if (span.m == 0) return NBKD_OK;
     // k > 64: the collect kernel hands each query's final bound to the wave select
     float *kbound = k > 64 ? kb : nullptr;
@@ -1112,6 +1124,17 @@ nbkd_status launch_knn_collect(const Tree &t, const float *q, const uint32_t *or
         launch_collect<false>(t, q, order, span, k, tg, seed_mul, qpp, cand, capg, ccount, stats,
                               retry, kbound, s);
     NBKD_HIP(hipGetLastError());
+    return NBKD_OK;
+}
+
+nbkd_status launch_select_pass(const Tree &t, const float *q, const uint32_t *order, QSpan span,
+                               int k, const float *tg, uint32_t qpp, const uint2 *cand,
+                               uint32_t capg, const uint32_t *ccount, float *od, uint32_t *oi,
+                               uint32_t *fail_list, uint32_t *fail_count, uint32_t *fail_bits,
+                               uint32_t pos_base, bool retry, bool fix_seed, bool sq, float *kb,
+                               hipStream_t s) {
+    if (span.m == 0) return NBKD_OK;
+    float *kbound = k > 64 ? kb : nullptr;
     {
         TimedScope ts(retry ? "knn_retry" : "knn_select", s);
         // a retry round follows: failures rewrite their seed for it
