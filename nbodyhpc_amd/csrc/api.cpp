@@ -1,6 +1,5 @@
 // C ABI of libnbkd.so (include/nbkd.h).  Host code only; kernels live in
 // build.hip / query.hip.  No exception crosses the boundary.
-#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <sched.h>
@@ -222,10 +221,9 @@ void tree_free(void *p) {
 
 namespace {
 // nbkd_set_tuning knobs (process-wide); defaults are the measured optima
-std::atomic<double> g_tune[TUNE_N] = {{3.5}, {0.0}, {0.0}, {0.0}, {0.0}, {0.0}};
+std::atomic<double> g_tune[TUNE_N] = {{3.5}, {0.0}, {0.0}, {0.0}};
 const char *const g_tune_names[TUNE_N] = {"knn_seed_margin", "candidate_bytes", "host_batch",
-                                          "host_threads", "overlap_batches",
-                                          "overlap_select_cus"};
+                                          "host_threads"};
 thread_local nbkd_interrupt_fn t_intr = nullptr;
 thread_local void *t_intr_user = nullptr;
 } // namespace
@@ -274,10 +272,12 @@ AllWs::~AllWs() {
 // ------------------------------------------------------------ host copy threads
 // The host-buffer pipeline moves every batch between the caller's (pageable)
 // arrays and pinned staging: a ~1 GiB batch of k = 32 rows is one memcpy per
-// output, and its first touch of fresh numpy pages faults them in.  One thread
-// does ~5-10 GB/s of that, under the ~50 GB/s of pinned PCIe DMA, so the copy is
-// split into 8 MiB chunks over a few threads (the usable cores: the affinity
-// mask capped by the cgroup quota, at most 16; nbkd_set_tuning("host_threads")).
+// output, and its first touch of fresh numpy pages faults them in.  With one
+// copy thread the whole 1e8-query host call ran at 4.6e7 queries/s (12 GB/s of
+// rows), with 4 at 1.53e8 and with 16 at 1.56e8 (40 GB/s, the DMA's rate:
+// profiles/r05c_probes.txt), so the copy is split into 8 MiB chunks over the
+// usable cores (the affinity mask capped by the cgroup quota, at most 16;
+// nbkd_set_tuning("host_threads")).
 namespace {
 int usable_cpus() {
     int n = 1;
@@ -772,15 +772,6 @@ void Workspace::release() {
     }
     if (copy) (void)hipStreamDestroy(copy);
     copy = nullptr;
-    for (hipStream_t &o : ovl) {
-        if (o) (void)hipStreamDestroy(o);
-        o = nullptr;
-    }
-    for (hipEvent_t &e : oev) {
-        if (e) (void)hipEventDestroy(e);
-        e = nullptr;
-    }
-    ovl_sel_cus = -1;
     for (int b = 0; b < 2; ++b) {
         if (hpin[b]) (void)hipHostFree(hpin[b]);
         hpin[b] = nullptr;
@@ -806,42 +797,6 @@ void *Workspace::host_pinned(int slot, size_t bytes) {
     }
     hpin_cap[slot] = bytes;
     return hpin[slot];
-}
-
-// The select side takes mask bits [0, sel_cus), the collect side the others.
-// Mask bit i is a CU of XCD i % 8 (scripts/calib/cumask_probe.hip on MI355X:
-// bits 0..7 are one CU on each of the 8 XCDs, bits 0..31 four per XCD), so the
-// low bits spread the select over every XCD's memory path: a streaming read
-// reaches 1.8 TB/s on bits 0..31 and 3.3 TB/s on bits 0..63, against 5.7 TB/s on
-// all 256 CUs (profiles/r05c_cumask_probe.txt).  A mask that leaves an XCD
-// without CUs is not honoured as given (every 8th bit ran on all 256 CUs).
-hipError_t Workspace::overlap_init(int sel_cus) {
-    if (ovl[0] && ovl_sel_cus == sel_cus) return hipSuccess;
-    for (hipStream_t &o : ovl) {
-        if (o) (void)hipStreamDestroy(o);
-        o = nullptr;
-    }
-    int dev = 0, cus = 0;
-    hipError_t e = hipGetDevice(&dev);
-    if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (e != hipSuccess) return e;
-    if (sel_cus < 1 || sel_cus >= cus) return hipErrorInvalidValue;
-    const int words = (cus + 31) / 32;
-    std::vector<uint32_t> mc(words, 0u), ms(words, 0u);
-    for (int i = 0; i < cus; ++i) (i < sel_cus ? ms : mc)[i / 32] |= 1u << (i % 32);
-    e = hipExtStreamCreateWithCUMask(&ovl[0], (uint32_t)words, mc.data());
-    if (e == hipSuccess) e = hipExtStreamCreateWithCUMask(&ovl[1], (uint32_t)words, ms.data());
-    for (hipEvent_t &ev : oev)
-        if (e == hipSuccess && !ev) e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
-    if (e != hipSuccess) {
-        for (hipStream_t &o : ovl) {
-            if (o) (void)hipStreamDestroy(o);
-            o = nullptr;
-        }
-        return e;
-    }
-    ovl_sel_cus = sel_cus;
-    return hipSuccess;
 }
 
 hipError_t Workspace::pipe_init() {

@@ -184,8 +184,9 @@ __device__ __forceinline__ void ball_walk(const DevTree &t, const uint32_t *__re
                     // periodic leaves no partial query wraps around: the plain d2
                     // has the same bits (wrap_free), 8 VALU instead of 14 a step
                     if (!M || (plain_ok && __all(!part || wrap_free(qx, qy, qz, tb, L)))) {
-#if NBKD_BALL_PAIR
                         // two queries a step: two independent chains in flight
+                        // (one a step: 91.87 -> 89.41 ms per 1e8 count at r = 0.01,
+                        // same count SHA, profiles/r05d_ab.txt)
                         while (rem) {
                             const int j = __builtin_ctzll(rem);
                             rem &= rem - 1;
@@ -206,16 +207,6 @@ __device__ __forceinline__ void ball_walk(const DevTree &t, const uint32_t *__re
                                 lane_write(tc, c, j);
                             }
                         }
-#else
-                        while (rem) {
-                            const int j = __builtin_ctzll(rem);
-                            rem &= rem - 1;
-                            const float4 sq = W.qs[j]; // LDS broadcast
-                            const float d = point_d2_fast<false>(sq.x, sq.y, sq.z, px, py, pz, L);
-                            const uint32_t c = (uint32_t)__popcll(__ballot(d <= r2) & pvm);
-                            lane_write(tc, c, j);
-                        }
-#endif
                     } else {
                         while (rem) {
                             const int j = __builtin_ctzll(rem);

@@ -49,13 +49,6 @@ struct Workspace {
     void *hpin[2] = {};
     size_t hpin_cap[2] = {};
     void *host_pinned(int slot, size_t bytes); // nullptr on failure (error recorded)
-    // the first pass's overlapped batches (query.hip): [0] a stream on the
-    // collect CUs, [1] one on the select CUs (hipExtStreamCreateWithCUMask),
-    // and their events: [0..1] collect done, [2..3] select done, [4] entry
-    hipStream_t ovl[2] = {};
-    hipEvent_t oev[5] = {};
-    int ovl_sel_cus = -1; // the select side's CU count the streams were made for
-    hipError_t overlap_init(int sel_cus);
     // returns nullptr on failure (hip error recorded via set_error)
     void *get(int slot, size_t bytes, hipStream_t s);
     void release();
@@ -200,10 +193,7 @@ inline const char *knob(const char *env) { return getenv(env); }
 #else
 inline const char *knob(const char *) { return nullptr; }
 #endif
-enum TuneId {
-    TUNE_KNN_SEED = 0, TUNE_CAND_BYTES, TUNE_HOST_BATCH, TUNE_HOST_THREADS, TUNE_OVL_BATCHES,
-    TUNE_OVL_SELECT_CUS, TUNE_N
-};
+enum TuneId { TUNE_KNN_SEED = 0, TUNE_CAND_BYTES, TUNE_HOST_BATCH, TUNE_HOST_THREADS, TUNE_N };
 // host memcpy split over the library's copy threads (api.cpp): the host-buffer
 // pipeline's pinned staging <-> the caller's arrays; small copies stay on the
 // calling thread
@@ -323,8 +313,7 @@ nbkd_status launch_knn_collect(const Tree &t, const float *q, const uint32_t *or
                                uint32_t pos_base, bool retry, bool fix_seed, bool sq, float *kb,
                                unsigned long long *stats, hipStream_t s);
 
-// the same pass as its two halves (the first-pass batches may run their
-// selects on another stream, overlapped with the next batch's collect)
+// the same pass as its two halves
 nbkd_status launch_collect_pass(const Tree &t, const float *q, const uint32_t *order, QSpan span,
                                 int k, const float *tg, float seed_mul, uint32_t qpp, uint2 *cand,
                                 uint32_t capg, uint32_t *ccount, bool retry, float *kb,

@@ -926,19 +926,6 @@ nbkd_status sort_pairs(Workspace &ws, uint32_t *k0, uint32_t *v0, uint32_t *k1, 
 
 namespace {
 
-// overlapped first pass: batches (0 = off) and the select side's CUs
-// (nbkd_set_tuning "overlap_batches" / "overlap_select_cus"; experiments
-// builds: NBKD_OVL_B / NBKD_OVL_CUS)
-int overlap_batches() {
-    const char *e = knob("NBKD_OVL_B");
-    return e ? atoi(e) : (int)tuning(TUNE_OVL_BATCHES);
-}
-int overlap_select_cus() {
-    const char *e = knob("NBKD_OVL_CUS");
-    const int v = e ? atoi(e) : (int)tuning(TUNE_OVL_SELECT_CUS);
-    return v > 0 ? v : 32;
-}
-
 bool collect_disabled() {
     static const bool off = [] {
         const char *e = knob("NBKD_KNN_COLLECT");
@@ -1027,20 +1014,6 @@ nbkd_status knn_locked(const Tree &t, Workspace &ws, const float *q, uint64_t m,
             uint64_t batch = budget / ((uint64_t)capg * 8u) / 64u * 64u;
             batch = std::max<uint64_t>(batch, 64);
             batch = std::min<uint64_t>(batch, ((uint64_t)mm + 63) / 64 * 64);
-            // Overlapped first pass (overlap_batches B >= 2, k <= 64, large
-            // calls): B batches whose selects run on a stream confined to a few
-            // CUs (overlap_select_cus) while the next batch's collect runs on
-            // the others, the last select on the caller's stream (every CU);
-            // two column buffers.  The collect is bound by instruction issue
-            // and the select by memory, so the select's traffic hides under the
-            // collect's compute.
-            const int ovl_b = overlap_batches();
-            const int ovl_cus = overlap_select_cus();
-            const bool ovl = ovl_b >= 2 && ovl_cus > 0 && k <= 64 &&
-                             (uint64_t)mm >= (uint64_t)ovl_b * 65536u &&
-                             2u * ((((uint64_t)mm + ovl_b - 1) / ovl_b + 63) / 64 * 64) <= batch;
-            const uint64_t nbuf = ovl ? 2 : 1;
-            if (ovl) batch = (((uint64_t)mm + ovl_b - 1) / ovl_b + 63) / 64 * 64;
             // the re-walk rounds' columns: 8 capg (packets of 64 or one query
             // per wave), then 64 capg (one query per wave)
             const uint32_t capr = capg * 8u, capr2 = capg * 64u;
@@ -1060,15 +1033,15 @@ nbkd_status knn_locked(const Tree &t, Workspace &ws, const float *q, uint64_t m,
             const uint64_t rb = std::min<uint64_t>(
                 std::max<uint64_t>(budget / ((uint64_t)capr * 8u) / 64u * 64u, 64),
                 std::max<uint64_t>({64, ((uint64_t)mm / 10 + 63) / 64 * 64,
-                                    nbuf * batch * capg / capr / 64u * 64u}));
+                                    batch * capg / capr / 64u * 64u}));
             const uint64_t rb2 = std::min<uint64_t>(
                 std::max<uint64_t>(budget / ((uint64_t)capr2 * 8u), 64),
                 std::max<uint64_t>(64, (uint64_t)mm / 100 + 1));
             // a round's pass covers at most min(cap, mm) queries, in packets of 64
             const uint64_t cap1 = std::min<uint64_t>(rb, mm64), cap2 = std::min<uint64_t>(rb2, mm);
             const uint64_t cand_bytes =
-                std::max<uint64_t>({nbuf * batch * capg * 8u, cap1 * capr * 8u, cap2 * capr2 * 8u});
-            const uint64_t cc_words = std::max<uint64_t>(nbuf * batch, cap1);
+                std::max<uint64_t>({batch * capg * 8u, cap1 * capr * 8u, cap2 * capr2 * 8u});
+            const uint64_t cc_words = std::max<uint64_t>(batch, cap1);
             uint2 *cand = (uint2 *)ws.get(WS_CAND, cand_bytes, s);
             uint32_t *ccount = (uint32_t *)ws.get(WS_CCOUNT, cc_words * 4u, s);
             // k > 64: per-query final bounds, collect -> wave select (any batch
@@ -1096,40 +1069,7 @@ nbkd_status knn_locked(const Tree &t, Workspace &ws, const float *q, uint64_t m,
             NBKD_HIP(hipMemsetAsync(rq_count, 0, 4, s));
             NBKD_HIP(hipMemsetAsync(r2_count, 0, 4, s));
             const bool adaptive = retry_adaptive();
-            if (ovl) {
-                TimedScope ts("knn", s);
-                NBKD_HIP(ws.overlap_init(ovl_cus));
-                hipStream_t sc = ws.ovl[0], ss = ws.ovl[1];
-                hipEvent_t *ec = ws.oev, *es = ws.oev + 2;
-                NBKD_HIP(hipEventRecord(ws.oev[4], s));
-                NBKD_HIP(hipStreamWaitEvent(sc, ws.oev[4], 0));
-                NBKD_HIP(hipStreamWaitEvent(ss, ws.oev[4], 0));
-                const uint64_t nbt = ((uint64_t)mm + batch - 1) / batch;
-                for (uint64_t bi = 0; bi < nbt; ++bi) {
-                    const uint64_t b0 = bi * batch;
-                    const uint32_t nb = (uint32_t)std::min<uint64_t>(batch, mm - b0);
-                    const int buf = (int)(bi & 1);
-                    uint2 *cb = cand + (size_t)buf * batch * capg;
-                    uint32_t *ccb = ccount + (size_t)buf * batch;
-                    // buffer `buf` is free once batch bi-2's select has read it
-                    if (bi >= 2) NBKD_HIP(hipStreamWaitEvent(sc, es[buf], 0));
-                    rc = launch_collect_pass(t, dq, ord + b0, static_span(nb), k, tg, 1.0f, 64u, cb,
-                                             capg, ccb, false, kb, stats, sc);
-                    if (rc) return rc;
-                    NBKD_HIP(hipEventRecord(ec[buf], sc));
-                    const bool last = bi + 1 == nbt;
-                    hipStream_t sx = last ? s : ss;
-                    NBKD_HIP(hipStreamWaitEvent(sx, ec[buf], 0));
-                    rc = launch_select_pass(t, dq, ord + b0, static_span(nb), k, tg, 64u, cb, capg,
-                                            ccb, dd, di, nullptr, nullptr, bits, (uint32_t)b0,
-                                            false, adaptive, sq, kb, sx);
-                    if (rc) return rc;
-                    if (!last) NBKD_HIP(hipEventRecord(es[buf], ss));
-                }
-                // every select on the select stream before what follows on s
-                NBKD_HIP(hipEventRecord(es[0], ss));
-                NBKD_HIP(hipStreamWaitEvent(s, es[0], 0));
-            } else {
+            {
                 TimedScope ts("knn", s);
                 for (uint64_t b0 = 0; b0 < mm; b0 += batch) {
                     const uint32_t nb = (uint32_t)std::min<uint64_t>(batch, mm - b0);

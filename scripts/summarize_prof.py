@@ -1,4 +1,4 @@
-"""Turn one gpu_round.sh output directory into the committed profile summaries.
+"""Turn one gpu_run.sh output directory (steps trace, pmc) into the committed profile summaries.
 
     python scripts/summarize_prof.py gpurun_out/<tag> <round-tag>
 

@@ -1,4 +1,4 @@
-"""Per-step HBM bytes of the whole kNN query (scripts/step_traffic.sh output):
+"""Per-step HBM bytes of the whole kNN query (scripts/gpu_run.sh STEPS=step output):
 
     python scripts/summarize_step.py gpurun_out/<tag> <round-tag>
 
