@@ -38,6 +38,9 @@ struct PadLeaves {
 struct alignas(16) BallLds {
     float4 p4[CHUNK]; // the staged points: x, y, z, original id bits (Tree::p4)
     float4 qs[64]; // the wave's query coordinates, for the transposed count
+#if NBKD_BALL_V4
+    float qsx[64], qsy[64], qsz[64]; // the same, one array per axis (two queries a step)
+#endif
 };
 
 // upper bound of the f32 d2 of point_d2_fast over every point of the box: per
@@ -187,6 +190,75 @@ __device__ __forceinline__ void ball_walk(const DevTree &t, const uint32_t *__re
                         // two queries a step: two independent chains in flight
                         // (one a step: 91.87 -> 89.41 ms per 1e8 count at r = 0.01,
                         // same count SHA, profiles/r05d_ab.txt)
+#if NBKD_BALL_V4
+                        // lanes past the chunk hold FLT_MAX (d2 = inf): no mask AND;
+                        // the pair's coordinates per axis as float2, so each axis
+                        // term is one packed op for both queries
+                        typedef float f2 __attribute__((ext_vector_type(2)));
+                        const float ux = pv ? px : FLT_MAX, uy = pv ? py : FLT_MAX,
+                                    uz = pv ? pz : FLT_MAX;
+                        const f2 px2 = {ux, ux}, py2 = {uy, uy}, pz2 = {uz, uz};
+                        while (rem) {
+                            const int j = __builtin_ctzll(rem);
+                            rem &= ~(1ull << j);
+                            asm volatile("s_mov_b32 m0, %0" : : "s"(j) : "m0");
+                            if (rem) {
+                                const int j2 = __builtin_ctzll(rem);
+                                rem &= ~(1ull << j2);
+                                const f2 qx2 = {W.qsx[j], W.qsx[j2]}, qy2 = {W.qsy[j], W.qsy[j2]},
+                                         qz2 = {W.qsz[j], W.qsz[j2]};
+                                const f2 dx = px2 - qx2, dy = py2 - qy2, dz = pz2 - qz2;
+                                const f2 d = (dx * dx + dy * dy) + dz * dz;
+                                const uint32_t c = (uint32_t)__popcll(__ballot(d.x <= r2));
+                                const uint32_t c2 = (uint32_t)__popcll(__ballot(d.y <= r2));
+                                asm volatile("v_writelane_b32 %0, %1, m0\n\ts_mov_b32 m0, %2\n\ts_nop 1\n\t"
+                                             "v_writelane_b32 %0, %3, m0"
+                                             : "+v"(tc) : "s"(c), "s"(j2), "s"(c2) : "m0");
+                            } else {
+                                const float d = point_d2_fast<false>(W.qsx[j], W.qsy[j], W.qsz[j],
+                                                                     ux, uy, uz, L);
+                                const uint32_t c = (uint32_t)__popcll(__ballot(d <= r2));
+                                asm volatile("v_writelane_b32 %0, %1, m0" : "+v"(tc) : "s"(c));
+                            }
+                        }
+#elif NBKD_BALL_V2
+                        // lanes past the chunk hold FLT_MAX (d2 = inf): no mask AND
+                        const float ux = pv ? px : FLT_MAX, uy = pv ? py : FLT_MAX,
+                                    uz = pv ? pz : FLT_MAX;
+                        while (rem) {
+                            const int j = __builtin_ctzll(rem);
+                            rem &= ~(1ull << j);
+#if NBKD_BALL_M0EARLY
+                            asm volatile("s_mov_b32 m0, %0" : : "s"(j) : "m0");
+#endif
+                            const float4 sq = W.qs[j]; // LDS broadcast
+                            if (rem) {
+                                const int j2 = __builtin_ctzll(rem);
+                                rem &= ~(1ull << j2);
+                                const float4 sq2 = W.qs[j2];
+                                const float d = point_d2_fast<false>(sq.x, sq.y, sq.z, ux, uy, uz, L);
+                                const float d2 = point_d2_fast<false>(sq2.x, sq2.y, sq2.z, ux, uy, uz, L);
+                                const uint32_t c = (uint32_t)__popcll(__ballot(d <= r2));
+                                const uint32_t c2 = (uint32_t)__popcll(__ballot(d2 <= r2));
+#if NBKD_BALL_M0EARLY
+                                asm volatile("v_writelane_b32 %0, %1, m0\n\ts_mov_b32 m0, %2\n\ts_nop 1\n\t"
+                                             "v_writelane_b32 %0, %3, m0"
+                                             : "+v"(tc) : "s"(c), "s"(j2), "s"(c2) : "m0");
+#else
+                                lane_write(tc, c, j);
+                                lane_write(tc, c2, j2);
+#endif
+                            } else {
+                                const float d = point_d2_fast<false>(sq.x, sq.y, sq.z, ux, uy, uz, L);
+                                const uint32_t c = (uint32_t)__popcll(__ballot(d <= r2));
+#if NBKD_BALL_M0EARLY
+                                asm volatile("v_writelane_b32 %0, %1, m0" : "+v"(tc) : "s"(c));
+#else
+                                lane_write(tc, c, j);
+#endif
+                            }
+                        }
+#else
                         while (rem) {
                             const int j = __builtin_ctzll(rem);
                             rem &= rem - 1;
@@ -207,6 +279,7 @@ __device__ __forceinline__ void ball_walk(const DevTree &t, const uint32_t *__re
                                 lane_write(tc, c, j);
                             }
                         }
+#endif
                     } else {
                         while (rem) {
                             const int j = __builtin_ctzll(rem);
@@ -279,6 +352,13 @@ ball_packet_kernel(DevTree t, const uint32_t *__restrict__ linfo, const float *_
     const uint64_t wpos = (FILL && active) ? row_offsets[qo] : 0;
     uint32_t cnt = 0;
     if constexpr (!FILL) W.qs[lane] = make_float4(qx, qy, qz, 0.0f);
+#if NBKD_BALL_V4
+    if constexpr (!FILL) {
+        W.qsx[lane] = qx;
+        W.qsy[lane] = qy;
+        W.qsz[lane] = qz;
+    }
+#endif
 
     // every active lane's ball clears the box faces by a margin r' > r: the
     // plain formulas then give the periodic ones' bits for every point within
