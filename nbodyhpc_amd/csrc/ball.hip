@@ -391,6 +391,316 @@ ball_packet_kernel(DevTree t, const uint32_t *__restrict__ linfo, const float *_
     }
 }
 
+// ------------------------------------------------------ 128-query packets (count)
+// Two queries per lane: A = sorted position 128 p + lane, B = A + 64.  One walk
+// and one leaf test serve 128 spatially adjacent queries, so their walk cost
+// (31.7 % of the 64-query kernel's wave clocks at 1e8, r = 0.01, with 309 node
+// visits and 104 leaves per packet; the leaf test 22.9 %; profiles/r05c_probes.txt)
+// spreads over twice the queries, while the per-(query, leaf) work -- the
+// transposed steps and the per-lane loop -- stays what it was.  The packet's
+// balls cover a region only ~1.3x the volume of a 64-query packet's, so far
+// fewer than twice the nodes and leaves are visited.
+struct alignas(16) BallLds2 {
+    float4 p4[CHUNK]; // the staged points
+    float4 qs[128];   // the packet's query coordinates (A at lane, B at 64 + lane)
+};
+
+// one internal node with split axis D for both query sets (NBKD_GSTEP's logic)
+#define NBKD_GSTEP2(D)                                                                             \
+    {                                                                                              \
+        const float split = nd.split;                                                              \
+        const float qa = (D) == 0 ? ax : ((D) == 1 ? ay : az);                                     \
+        const float qb = (D) == 0 ? bx_ : ((D) == 1 ? by : bz);                                    \
+        float tlA, trA, tlB, trB;                                                                  \
+        if constexpr (M) {                                                                         \
+            tlA = box_lb_axis<M>(qa, bx[2 * (D)], split, L);                                       \
+            trA = box_lb_axis<M>(qa, split, bx[2 * (D) + 1], L);                                   \
+            tlB = box_lb_axis<M>(qb, bx[2 * (D)], split, L);                                       \
+            trB = box_lb_axis<M>(qb, split, bx[2 * (D) + 1], L);                                   \
+        } else {                                                                                   \
+            const float da_ = qa - split, ma_ = da_ * da_;                                         \
+            const float db_ = qb - split, mb_ = db_ * db_;                                         \
+            tlA = da_ > 0.0f ? ma_ : tmA[D];                                                       \
+            trA = da_ > 0.0f ? tmA[D] : ma_;                                                       \
+            tlB = db_ > 0.0f ? mb_ : tmB[D];                                                       \
+            trB = db_ > 0.0f ? tmB[D] : mb_;                                                       \
+        }                                                                                          \
+        const float dlA = (((D) == 0 ? tlA : tmA[0]) + ((D) == 1 ? tlA : tmA[1])) + ((D) == 2 ? tlA : tmA[2]); \
+        const float drA = (((D) == 0 ? trA : tmA[0]) + ((D) == 1 ? trA : tmA[1])) + ((D) == 2 ? trA : tmA[2]); \
+        const float dlB = (((D) == 0 ? tlB : tmB[0]) + ((D) == 1 ? tlB : tmB[1])) + ((D) == 2 ? tlB : tmB[2]); \
+        const float drB = (((D) == 0 ? trB : tmB[0]) + ((D) == 1 ? trB : tmB[1])) + ((D) == 2 ? trB : tmB[2]); \
+        const uint64_t wlA = __ballot(dlA <= thrA), wrA = __ballot(drA <= thrA);                  \
+        const uint64_t wlB = __ballot(dlB <= thrB), wrB = __ballot(drB <= thrB);                  \
+        const bool wl = (wlA | wlB) != 0, wr = (wrA | wrB) != 0;                                   \
+        bool go_right = wr;                                                                        \
+        if (wl && wr) {                                                                            \
+            const uint32_t votes = (uint32_t)__popcll(wmA & __ballot(qa > split)) +               \
+                                   (uint32_t)__popcll(wmB & __ballot(qb > split));                \
+            const bool right_first = 2 * votes > (uint32_t)(__popcll(wmA) + __popcll(wmB));        \
+            const uint64_t pmask = 1ull << sp;                                                     \
+            sk_node = lane_set(sk_node, right_first ? nd.left : nd.right, pmask);                  \
+            ++sp;                                                                                  \
+            go_right = right_first;                                                                \
+        } else if (!wl && !wr) {                                                                   \
+            continue;                                                                              \
+        }                                                                                          \
+        node = go_right ? nd.right : nd.left;                                                      \
+        nd = cnodes[node];                                                                         \
+        tmA[D] = go_right ? trA : tlA;                                                             \
+        tmB[D] = go_right ? trB : tlB;                                                             \
+        if (go_right)                                                                              \
+            bx[2 * (D)] = unif(split);                                                             \
+        else                                                                                       \
+            bx[2 * (D) + 1] = unif(split);                                                         \
+        wmA = go_right ? wrA : wlA;                                                                \
+        wmB = go_right ? wrB : wlB;                                                                \
+        have = true;                                                                               \
+    }
+
+// advance the walk to the next leaf a query of either set wants
+#define NBKD_GWALK2(FOUND, LPOS, LEND)                                                             \
+    FOUND = false;                                                                                 \
+    for (;;) {                                                                                     \
+        if (!have) {                                                                               \
+            if (sp == 0) break;                                                                    \
+            --sp;                                                                                  \
+            node = (uint32_t)__builtin_amdgcn_readlane((int)sk_node, sp);                          \
+            {                                                                                      \
+                const NodeBox nb_ = cboxes[node];                                                  \
+                _Pragma("unroll") for (int a = 0; a < 6; ++a) bx[a] = nb_.b[a];                    \
+            }                                                                                      \
+            tmA[0] = box_lb_axis<M>(ax, bx[0], bx[1], L);                                          \
+            tmA[1] = box_lb_axis<M>(ay, bx[2], bx[3], L);                                          \
+            tmA[2] = box_lb_axis<M>(az, bx[4], bx[5], L);                                          \
+            tmB[0] = box_lb_axis<M>(bx_, bx[0], bx[1], L);                                         \
+            tmB[1] = box_lb_axis<M>(by, bx[2], bx[3], L);                                          \
+            tmB[2] = box_lb_axis<M>(bz, bx[4], bx[5], L);                                          \
+            wmA = __ballot((tmA[0] + tmA[1]) + tmA[2] <= thrA);                                    \
+            wmB = __ballot((tmB[0] + tmB[1]) + tmB[2] <= thrB);                                    \
+            if ((wmA | wmB) == 0) continue;                                                        \
+            nd = cnodes[node];                                                                     \
+        }                                                                                          \
+        have = false;                                                                              \
+        if constexpr (STATS) ++bst[0];                                                             \
+        if (nd.dimension < 0) {                                                                    \
+            LPOS = nd.left;                                                                        \
+            LEND = nd.right;                                                                       \
+            FOUND = true;                                                                          \
+            break;                                                                                 \
+        }                                                                                          \
+        if (nd.dimension == 0)                                                                     \
+            NBKD_GSTEP2(0)                                                                         \
+        else if (nd.dimension == 1)                                                                \
+            NBKD_GSTEP2(1)                                                                         \
+        else                                                                                       \
+            NBKD_GSTEP2(2)                                                                         \
+    }
+
+// transposed count of the partial queries in rem (query j of the set at
+// W.qs[base + j]) against the staged points (lanes past the chunk hold FLT_MAX,
+// so their d2 is inf and no mask is needed): two queries a step, each one's
+// count written into lane j of the returned register (v_writelane, lane select
+// in M0, written early)
+template <bool M>
+__device__ __forceinline__ uint32_t ball_tcount(uint64_t rem, const float4 *qs, float ux, float uy,
+                                                float uz, float r2, float L) {
+    uint32_t tc = 0;
+    while (rem) {
+        const int j = __builtin_ctzll(rem);
+        rem &= ~(1ull << j);
+        asm volatile("s_mov_b32 m0, %0" : : "s"(j) : "m0");
+        const float4 sq = qs[j]; // LDS broadcast
+        if (rem) {
+            const int j2 = __builtin_ctzll(rem);
+            rem &= ~(1ull << j2);
+            const float4 sq2 = qs[j2];
+            const float d = point_d2_fast<M>(sq.x, sq.y, sq.z, ux, uy, uz, L);
+            const float d2 = point_d2_fast<M>(sq2.x, sq2.y, sq2.z, ux, uy, uz, L);
+            const uint32_t c = (uint32_t)__popcll(__ballot(d <= r2));
+            const uint32_t c2 = (uint32_t)__popcll(__ballot(d2 <= r2));
+            asm volatile("v_writelane_b32 %0, %1, m0\n\ts_mov_b32 m0, %2\n\ts_nop 1\n\t"
+                         "v_writelane_b32 %0, %3, m0"
+                         : "+v"(tc) : "s"(c), "s"(j2), "s"(c2) : "m0");
+        } else {
+            const float d = point_d2_fast<M>(sq.x, sq.y, sq.z, ux, uy, uz, L);
+            const uint32_t c = (uint32_t)__popcll(__ballot(d <= r2));
+            asm volatile("v_writelane_b32 %0, %1, m0" : "+v"(tc) : "s"(c));
+        }
+    }
+    return tc;
+}
+
+template <bool PER, bool M, bool STATS>
+__device__ __forceinline__ void ball_walk2(const DevTree &t, const uint32_t *__restrict__ linfo,
+                                           float r2, const PadLeaves &pad, uint32_t tnum,
+                                           bool plain_ok, BallLds2 &W, const int lane,
+                                           const float ax, const float ay, const float az,
+                                           const float bx_, const float by, const float bz,
+                                           const float thrA, const float thrB, uint32_t &cntA,
+                                           uint32_t &cntB, uint32_t (&bst)[BALL_NST]) {
+    const float L = t.box;
+    uint32_t sk_node = 0;
+    int sp = 0;
+    const cnode_ptr cnodes = (cnode_ptr)t.nodes;
+    const cbox_ptr cboxes = (cbox_ptr)t.nbox;
+    uint32_t node = 0;
+    float bx[6];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        bx[2 * a] = PER ? 0.0f : -FLT_MAX;
+        bx[2 * a + 1] = PER ? L : FLT_MAX;
+    }
+    float tmA[3] = {box_lb_axis<M>(ax, bx[0], bx[1], L), box_lb_axis<M>(ay, bx[2], bx[3], L),
+                    box_lb_axis<M>(az, bx[4], bx[5], L)};
+    float tmB[3] = {box_lb_axis<M>(bx_, bx[0], bx[1], L), box_lb_axis<M>(by, bx[2], bx[3], L),
+                    box_lb_axis<M>(bz, bx[4], bx[5], L)};
+    uint64_t wmA = __ballot((tmA[0] + tmA[1]) + tmA[2] <= thrA);
+    uint64_t wmB = __ballot((tmB[0] + tmB[1]) + tmB[2] <= thrB);
+    bool have = (wmA | wmB) != 0;
+    nbkd_node nd = cnodes[0];
+    uint64_t tclk = STATS ? clock64() : 0;
+#define NBKD_BPH(I)                                                                                \
+    do {                                                                                           \
+        if constexpr (STATS) {                                                                     \
+            const uint64_t t_ = clock64();                                                         \
+            bst[8 + (I)] += (uint32_t)(t_ - tclk);                                                 \
+            tclk = t_;                                                                             \
+        }                                                                                          \
+    } while (0)
+    for (;;) {
+        bool found;
+        uint32_t lpos = 0, lend = 0;
+        NBKD_GWALK2(found, lpos, lend);
+        NBKD_BPH(0);
+        if (!found) break;
+        const NodeBox lb_ = ((cbox_ptr)linfo)[node];
+        const float tb[6] = {lb_.b[0], lb_.b[3], lb_.b[1], lb_.b[4], lb_.b[2], lb_.b[5]};
+        const bool needA = box_lb2<M>(ax, ay, az, tb, L) <= thrA;
+        const bool needB = box_lb2<M>(bx_, by, bz, tb, L) <= thrB;
+        if (!__any(needA || needB)) continue;
+        bool padded = false;
+#pragma unroll
+        for (int j = 0; j < NBKD_PAD_LEAVES; ++j) padded |= pad.id[j] == node;
+        const bool fullA = needA && !padded && box_ub2<PER>(ax, ay, az, tb) <= thrA;
+        const bool fullB = needB && !padded && box_ub2<PER>(bx_, by, bz, tb) <= thrB;
+        const bool partA = needA && !fullA, partB = needB && !fullB;
+        if (fullA) cntA += lend - lpos;
+        if (fullB) cntB += lend - lpos;
+        const uint64_t pmA = __ballot(partA), pmB = __ballot(partB);
+        if constexpr (STATS) {
+            ++bst[2];
+            bst[5] += (uint32_t)(__popcll(__ballot(fullA)) + __popcll(__ballot(fullB)));
+            bst[6] += (uint32_t)(__popcll(pmA) + __popcll(pmB));
+        }
+        NBKD_BPH(1);
+        if ((pmA | pmB) == 0) continue;
+        const uint32_t np = (uint32_t)(__popcll(pmA) + __popcll(pmB));
+        // the plain d2 where no partial query wraps around (wrap_free)
+        const bool plain_leaf =
+            !M || (plain_ok && __all((!partA || wrap_free(ax, ay, az, tb, L)) &&
+                                     (!partB || wrap_free(bx_, by, bz, tb, L))));
+        for (uint32_t c0 = lpos; c0 < lend; c0 += CHUNK) {
+            const uint32_t cn = min((uint32_t)CHUNK, lend - c0);
+            wave_sync();
+            glds_f4(t.p4 + c0, W.p4, lane, cn);
+            wait_vm0();
+            wave_sync();
+            if constexpr (STATS) bst[4] += cn;
+            NBKD_BPH(2);
+            if (np * 8u <= cn * tnum) {
+                const bool pv = (uint32_t)lane < cn;
+                const float4 pl = W.p4[lane];
+                const float ux = pv ? pl.x : FLT_MAX, uy = pv ? pl.y : FLT_MAX,
+                            uz = pv ? pl.z : FLT_MAX;
+                if (plain_leaf) {
+                    cntA += ball_tcount<false>(pmA, W.qs, ux, uy, uz, r2, L);
+                    cntB += ball_tcount<false>(pmB, W.qs + 64, ux, uy, uz, r2, L);
+                } else {
+                    cntA += ball_tcount<M>(pmA, W.qs, ux, uy, uz, r2, L);
+                    cntB += ball_tcount<M>(pmB, W.qs + 64, ux, uy, uz, r2, L);
+                }
+                if constexpr (STATS) {
+                    bst[3] += np;
+                    bst[1] += np * cn;
+                }
+                NBKD_BPH(3);
+            } else {
+                // many partial queries: each lane loops over the staged points
+                // for its two queries
+#pragma unroll 1
+                for (uint32_t u = 0; u < cn; ++u) {
+                    const float4 a = W.p4[u];
+                    cntA += (partA && point_d2_fast<M>(ax, ay, az, a.x, a.y, a.z, L) <= thrA) ? 1u : 0u;
+                    cntB += (partB && point_d2_fast<M>(bx_, by, bz, a.x, a.y, a.z, L) <= thrB) ? 1u : 0u;
+                }
+                if constexpr (STATS) {
+                    ++bst[7];
+                    bst[1] += np * cn;
+                }
+                NBKD_BPH(4);
+            }
+        }
+    }
+#undef NBKD_BPH
+}
+
+template <bool PER, bool STATS>
+__global__ void __launch_bounds__(TB, STATS ? 4 : 8) // (the instrumented instance would spill)
+ball_count2_kernel(DevTree t, const uint32_t *__restrict__ linfo, const float *__restrict__ q,
+                   const uint32_t *__restrict__ order, uint32_t m, float r2, PadLeaves pad,
+                   uint32_t *__restrict__ out_count, uint32_t tnum, bool plain_ok,
+                   unsigned long long *__restrict__ stats) {
+    __shared__ BallLds2 Wl[WPB];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    BallLds2 &W = Wl[wave];
+    const uint32_t ga = (xcd_block(blockIdx.x, gridDim.x) * WPB + wave) * 128u + lane;
+    const uint32_t gb = ga + 64u;
+    const bool va = ga < m, vb = gb < m;
+    uint32_t oa = va ? order[ga] : 0u, ob = vb ? order[gb] : 0u;
+    const float ax = va ? q[3 * (size_t)oa] : 0.0f, ay = va ? q[3 * (size_t)oa + 1] : 0.0f,
+                az = va ? q[3 * (size_t)oa + 2] : 0.0f;
+    const float bx_ = vb ? q[3 * (size_t)ob] : 0.0f, by = vb ? q[3 * (size_t)ob + 1] : 0.0f,
+                bz = vb ? q[3 * (size_t)ob + 2] : 0.0f;
+    const float L = t.box;
+    const bool ina = !PER || (ax >= 0.0f && ax <= L && ay >= 0.0f && ay <= L && az >= 0.0f && az <= L);
+    const bool inb = !PER || (bx_ >= 0.0f && bx_ <= L && by >= 0.0f && by <= L && bz >= 0.0f && bz <= L);
+    const bool acta = va && ina, actb = vb && inb;
+    const float thrA = acta ? r2 : -INFINITY, thrB = actb ? r2 : -INFINITY;
+    W.qs[lane] = make_float4(ax, ay, az, 0.0f);
+    W.qs[64 + lane] = make_float4(bx_, by, bz, 0.0f);
+    bool plain = false;
+    if constexpr (PER) {
+        const float r1 = sqrtf(fmaxf(r2, 0.0f)) * 1.01f + L * 1e-6f;
+        const bool wa = !acta || (r1 <= 0.25f * L && ax >= r1 && L - ax >= r1 && ay >= r1 &&
+                                  L - ay >= r1 && az >= r1 && L - az >= r1);
+        const bool wb = !actb || (r1 <= 0.25f * L && bx_ >= r1 && L - bx_ >= r1 && by >= r1 &&
+                                  L - by >= r1 && bz >= r1 && L - bz >= r1);
+        plain = plain_ok && __all(wa && wb);
+    }
+    uint32_t cntA = 0, cntB = 0;
+    uint32_t bst[BALL_NST] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    if (plain)
+        ball_walk2<PER, false, STATS>(t, linfo, r2, pad, tnum, plain_ok, W, lane, ax, ay, az, bx_,
+                                      by, bz, thrA, thrB, cntA, cntB, bst);
+    else
+        ball_walk2<PER, PER, STATS>(t, linfo, r2, pad, tnum, plain_ok, W, lane, ax, ay, az, bx_,
+                                    by, bz, thrA, thrB, cntA, cntB, bst);
+    // the ids again (not kept live through the walk: registers)
+    oa = acta ? order[ga] : 0u;
+    ob = actb ? order[gb] : 0u;
+    if (acta) out_count[oa] = cntA;
+    if (actb) out_count[ob] = cntB;
+    if constexpr (STATS) {
+        constexpr int slot[BALL_NST] = {0, 1, 2, 3, 4, 6, 7, 8, 10, 11, 12, 13, 14};
+        if (lane == 0) {
+#pragma unroll
+            for (int i = 0; i < BALL_NST; ++i)
+                atomicAdd(&stats[slot[i]], (unsigned long long)bst[i]);
+            atomicAdd(&stats[5], 1ull);
+        }
+    }
+}
+
 // Periodic queries outside [0, L]^3 (unvalidated input, as in the reference's
 // kNN): no box bound is valid for the reference's per-axis metric there, so
 // every point is tested.  Grid: x = point tiles, y = listed query.  Counts
@@ -502,6 +812,7 @@ void launch_ball_packet(const Tree &t, const float *q, const uint32_t *order, ui
     ball_packet_kernel<PER, FILL, STATS><<<blocks, TB, 0, s>>>(                                \
         view(t), t.leafinfo, q, order, m, r2, pad, out_count, row_offsets, out_idx, tnum,      \
         plain_ok, stats)
+#if NBKD_BALL_64
     if (t.periodic) {
         if (out_idx) NBKD_BALL(true, true, false);
         else if (stats) NBKD_BALL(true, false, true);
@@ -511,6 +822,22 @@ void launch_ball_packet(const Tree &t, const float *q, const uint32_t *order, ui
         else if (stats) NBKD_BALL(false, false, true);
         else NBKD_BALL(false, false, false);
     }
+#else
+    // count: 128-query packets (ball_count2_kernel); CSR fill: 64-query packets
+    const unsigned blocks2 = (unsigned)((m + 128 * WPB - 1) / (128 * WPB));
+#define NBKD_BALL2(PER, STATS)                                                                     \
+    ball_count2_kernel<PER, STATS><<<blocks2, TB, 0, s>>>(view(t), t.leafinfo, q, order, m, r2,   \
+                                                          pad, out_count, tnum, plain_ok, stats)
+    if (out_idx) {
+        if (t.periodic) NBKD_BALL(true, true, false);
+        else NBKD_BALL(false, true, false);
+    } else if (t.periodic) {
+        if (stats) NBKD_BALL2(true, true); else NBKD_BALL2(true, false);
+    } else {
+        if (stats) NBKD_BALL2(false, true); else NBKD_BALL2(false, false);
+    }
+#undef NBKD_BALL2
+#endif
 #undef NBKD_BALL
 }
 
