@@ -625,19 +625,20 @@ __device__ __forceinline__ void ball_walk2(const DevTree &t, const uint32_t *__r
                 }
                 NBKD_BPH(3);
             } else {
-                // many partial queries: each lane loops over the staged points,
-                // once per query set that has partial queries
-                auto lane_loop = [&](bool part, float x, float y, float z, float thr) {
-                    uint32_t c = 0;
+                // many partial queries: each lane loops over the staged points
+                // for its two queries (one LDS read per point for both; one
+                // loop per set read every point twice and, latency-bound, ran
+                // the count 78.4 -> 88.2 ms per 1e8, profiles/r05f_ball_ab.txt)
+#if NBKD_BALL_LL_UNROLL2
+#pragma unroll 2
+#else
 #pragma unroll 1
-                    for (uint32_t u = 0; u < cn; ++u) {
-                        const float4 a = W.p4[u];
-                        c += (part && point_d2_fast<M>(x, y, z, a.x, a.y, a.z, L) <= thr) ? 1u : 0u;
-                    }
-                    return c;
-                };
-                if (pmA) cntA += lane_loop(partA, ax, ay, az, thrA);
-                if (pmB) cntB += lane_loop(partB, bx_, by, bz, thrB);
+#endif
+                for (uint32_t u = 0; u < cn; ++u) {
+                    const float4 a = W.p4[u];
+                    cntA += (partA && point_d2_fast<M>(ax, ay, az, a.x, a.y, a.z, L) <= thrA) ? 1u : 0u;
+                    cntB += (partB && point_d2_fast<M>(bx_, by, bz, a.x, a.y, a.z, L) <= thrB) ? 1u : 0u;
+                }
                 if constexpr (STATS) {
                     ++bst[7];
                     bst[1] += np * cn;
