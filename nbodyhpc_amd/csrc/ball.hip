@@ -3,12 +3,15 @@
 // query, d2 in the reference's f32 point metric (kdtree.hpp:20-121, the a10
 // formula: ((dx^2 + dy^2) + dz^2), periodic per-axis minimum image).
 //
-// Same packet walk as knn_collect_kernel with a fixed bound r2: one wave64 =
-// 64 kd-ordered queries walking the tree together, near child first by
-// majority vote; at a leaf the lanes whose ball reaches the leaf's tight box
-// take part.  A lane whose ball CONTAINS the tight box (an upper bound of the
+// The kNN collect kernel's packet walk with a fixed bound r2: one wave64
+// walks the tree for a packet of kd-ordered queries, near child first by
+// majority vote; at a leaf the queries whose ball reaches the leaf's tight box
+// take part.  A query whose ball CONTAINS the tight box (an upper bound of the
 // f32 d2 over the box <= r2) counts the leaf's points without evaluating them;
-// the others evaluate the points staged in LDS.
+// the others evaluate the points staged in LDS.  The count
+// (ball_count2_kernel) runs packets of 128 queries, two per lane, the partial
+// ones mostly by transposed steps (lanes = points, one step = one query); the
+// CSR fill (ball_fill_kernel) packets of 64, one query per lane.
 //
 // Tried and dropped: the kNN collect's 8-point groups here (whole groups
 // counted, partial (lane, group) pairs compacted 8 lanes per pair): the same
@@ -37,22 +40,11 @@ struct PadLeaves {
 
 struct alignas(16) BallLds {
     float4 p4[CHUNK]; // the staged points: x, y, z, original id bits (Tree::p4)
-    float4 qs[64]; // the wave's query coordinates, for the transposed count
-#if NBKD_BALL_V4
-    float qsx[64], qsy[64], qsz[64]; // the same, one array per axis (two queries a step)
-#endif
 };
 
 // upper bound of the f32 d2 of point_d2_fast over every point of the box: per
 // axis |fl(x - q)| is monotone in x, so it is at most the larger end value; the
 // periodic minimum image only lowers it
-// lane j of v = c (c, j wave-uniform): one v_writelane_b32 (lane select in
-// M0: one SGPR source per VALU instruction); the s_nop covers the M0 write
-__device__ __forceinline__ void lane_write(uint32_t &v, uint32_t c, int j) {
-    asm volatile("s_mov_b32 m0, %2\n\ts_nop 1\n\tv_writelane_b32 %0, %1, m0"
-                 : "+v"(v) : "s"(c), "s"(j) : "m0");
-}
-
 template <bool PER>
 __device__ __forceinline__ float box_ub2(float qx, float qy, float qz, const float b[6]) {
     const float ux = fmaxf(fabsf(b[0] - qx), fabsf(b[1] - qx));
@@ -61,30 +53,18 @@ __device__ __forceinline__ float box_ub2(float qx, float qy, float qz, const flo
     return (ux * ux + uy * uy) + uz * uz;
 }
 
-
-// occupancy per variant ([periodic][fill]).  With the node-id stack the
-// periodic count fits 8 waves per SIMD without spills (62 VGPRs); the
-// non-periodic count still spills 44 B per lane.  Round 3 before the node-id
-// stack: the periodic count spilled 20 B per lane at 8 waves (4.7 GB written
-// per 1e8 count, r03f), and 7 waves without spills ran 128.5 ms against 124.3
-// (r03g): spills that stay in L2 cost less than the lost occupancy
-constexpr int BALL_OCC[2][2] = {{8, 8}, {8, 8}};
-
-// the packet's walk and leaf scans (M: the metric's formulas, plain for a
-// packet whose balls all clear the box faces, ball_packet_kernel)
-// STATS (count mode, the instrumented instance): bst = node visits, points
-// evaluated, leaves needed, transposed steps, points staged, full (lane, leaf)
-// pairs, partial (lane, leaf) pairs, per-lane-loop chunks, then the s_memtime
-// phase clocks walk / leaf test / staging wait / transposed steps / per-lane loop
-constexpr int BALL_NST = 13;
-template <bool PER, bool M, bool FILL, bool STATS>
-__device__ __forceinline__ void ball_walk(const DevTree &t, const uint32_t *__restrict__ linfo,
-                                          float r2, const PadLeaves &pad,
-                                          uint32_t *__restrict__ out_idx, uint32_t tnum,
-                                          bool plain_ok, BallLds &W, const int lane,
-                                          const float qx, const float qy, const float qz,
-                                          const float thr, const uint64_t wpos, uint32_t &cnt,
-                                          uint32_t (&bst)[BALL_NST]) {
+// The CSR fill (nbkd_query_ball_csr's second pass): 64-query packets, the
+// packet walk, and at each leaf the lanes whose ball contains the tight box
+// write all its ids, the partial ones loop over the staged points.  (Until
+// round 5 this kernel counted too, with the transposed steps that
+// ball_count2_kernel below now runs over 128-query packets.)  M: the metric's
+// formulas, plain for a packet whose balls all clear the box faces.
+template <bool PER, bool M>
+__device__ __forceinline__ void ball_fill_walk(const DevTree &t, const uint32_t *__restrict__ linfo,
+                                               const PadLeaves &pad, uint32_t *__restrict__ out_idx,
+                                               BallLds &W, const int lane, const float qx,
+                                               const float qy, const float qz, const float thr,
+                                               const uint64_t wpos) {
     const float L = t.box;
     uint32_t sk_node = 0;
     int sp = 0;
@@ -102,32 +82,18 @@ __device__ __forceinline__ void ball_walk(const DevTree &t, const uint32_t *__re
     uint64_t wm = __ballot((tm[0] + tm[1]) + tm[2] <= thr);
     bool have = wm != 0;
     nbkd_node nd = cnodes[0]; // record of `node` while `have`
-    // the shared packet walk (packet.hpp: per-axis steps, node-id stack);
-    // NBKD_GWALK counts node visits in st[0]
+    // the shared packet walk (packet.hpp: per-axis steps, node-id stack)
+    constexpr bool STATS = false;
     const float kth = thr;
-    uint32_t (&st)[BALL_NST] = bst;
-    uint64_t tclk = STATS ? clock64() : 0;
-#define NBKD_BPH(I)                                                                                \
-    do {                                                                                           \
-        if constexpr (STATS) {                                                                     \
-            const uint64_t t_ = clock64();                                                         \
-            bst[8 + (I)] += (uint32_t)(t_ - tclk);                                                 \
-            tclk = t_;                                                                             \
-        }                                                                                          \
-    } while (0)
-
+    uint32_t st[1] = {0};
+    (void)st;
+    uint32_t cnt = 0;
     for (;;) {
         bool found;
         uint32_t lpos = 0, lend = 0;
         NBKD_GWALK(found, lpos, lend);
-        NBKD_BPH(0);
         if (!found) break;
-
-        // leaf: its tight box first (leafinfo words lo.xyz, hi.xyz: one
-        // s_load_dwordx8 through the scalar cache, straight into SGPRs), then
-        // the chunks.  Round 4 loaded it per lane (lanes < 6, a vector load
-        // and six v_readlane): the leaf test was 23 % of the kernel's wave
-        // clocks at 1e8, r = 0.01 (profiles/r05c_probes.txt, stats pass)
+        // the leaf's tight box (leafinfo lo.xyz, hi.xyz): one s_load_dwordx8
         const NodeBox lb_ = ((cbox_ptr)linfo)[node];
         const float tb[6] = {lb_.b[0], lb_.b[3], lb_.b[1], lb_.b[4], lb_.b[2], lb_.b[5]};
         const bool need = box_lb2<M>(qx, qy, qz, tb, L) <= thr;
@@ -138,204 +104,38 @@ __device__ __forceinline__ void ball_walk(const DevTree &t, const uint32_t *__re
         for (int j = 0; j < NBKD_PAD_LEAVES; ++j) padded |= pad.id[j] == node;
         const bool full = need && !padded && box_ub2<PER>(qx, qy, qz, tb) <= thr;
         const bool part = need && !full;
-        if constexpr (STATS) {
-            ++bst[2];
-            bst[5] += (uint32_t)__popcll(__ballot(full));
-            bst[6] += (uint32_t)__popcll(__ballot(part));
-        }
-        NBKD_BPH(1);
-        if constexpr (!FILL) {
-            if (full) cnt += lend - lpos;
-            if (!__any(part)) continue;
-        }
         for (uint32_t c0 = lpos; c0 < lend; c0 += CHUNK) {
             const uint32_t cn = min((uint32_t)CHUNK, lend - c0);
             wave_sync();
             glds_f4(t.p4 + c0, W.p4, lane, cn);
             wait_vm0();
             wave_sync();
-            if constexpr (STATS) bst[4] += cn;
-            NBKD_BPH(2);
-            if constexpr (FILL) {
-                if (full) {
+            if (full) {
 #pragma unroll 1
-                    for (uint32_t u = 0; u < cn; ++u)
-                        out_idx[wpos + cnt + u] = __float_as_uint(W.p4[u].w);
-                    cnt += cn;
-                }
+                for (uint32_t u = 0; u < cn; ++u)
+                    out_idx[wpos + cnt + u] = __float_as_uint(W.p4[u].w);
+                cnt += cn;
             }
-            // count mode, few partial lanes: transpose the loop.  Lanes hold
-            // the staged points, each step tests them against one partial
-            // query (coordinates broadcast from LDS), and the ballot's
-            // popcount is that query's hit count.  One step is ~14 VALU per
-            // query against ~16 per point for the whole wave below, so it
-            // pays while #partial <= tnum/8 x #points.
-            bool trans = false;
-            if constexpr (!FILL) {
-                const uint64_t pm = __ballot(part);
-                trans = (uint32_t)__popcll(pm) * 8u <= cn * tnum;
-                if (trans) {
-                    const bool pv = (uint32_t)lane < cn;
-                    const float4 pl = W.p4[lane];
-                    const float px = pl.x, py = pl.y, pz = pl.z;
-                    uint64_t rem = pm;
-                    // the staged lanes as a mask (AND-ed with each step's
-                    // ballot), and each step's count written into lane j of
-                    // tc by one v_writelane; added to cnt once per chunk
-                    const uint64_t pvm = __ballot(pv);
-                    uint32_t tc = 0;
-                    // periodic leaves no partial query wraps around: the plain d2
-                    // has the same bits (wrap_free), 8 VALU instead of 14 a step
-                    if (!M || (plain_ok && __all(!part || wrap_free(qx, qy, qz, tb, L)))) {
-                        // two queries a step: two independent chains in flight
-                        // (one a step: 91.87 -> 89.41 ms per 1e8 count at r = 0.01,
-                        // same count SHA, profiles/r05d_ab.txt)
-#if NBKD_BALL_V4
-                        // lanes past the chunk hold FLT_MAX (d2 = inf): no mask AND;
-                        // the pair's coordinates per axis as float2, so each axis
-                        // term is one packed op for both queries
-                        typedef float f2 __attribute__((ext_vector_type(2)));
-                        const float ux = pv ? px : FLT_MAX, uy = pv ? py : FLT_MAX,
-                                    uz = pv ? pz : FLT_MAX;
-                        const f2 px2 = {ux, ux}, py2 = {uy, uy}, pz2 = {uz, uz};
-                        while (rem) {
-                            const int j = __builtin_ctzll(rem);
-                            rem &= ~(1ull << j);
-                            asm volatile("s_mov_b32 m0, %0" : : "s"(j) : "m0");
-                            if (rem) {
-                                const int j2 = __builtin_ctzll(rem);
-                                rem &= ~(1ull << j2);
-                                const f2 qx2 = {W.qsx[j], W.qsx[j2]}, qy2 = {W.qsy[j], W.qsy[j2]},
-                                         qz2 = {W.qsz[j], W.qsz[j2]};
-                                const f2 dx = px2 - qx2, dy = py2 - qy2, dz = pz2 - qz2;
-                                const f2 d = (dx * dx + dy * dy) + dz * dz;
-                                const uint32_t c = (uint32_t)__popcll(__ballot(d.x <= r2));
-                                const uint32_t c2 = (uint32_t)__popcll(__ballot(d.y <= r2));
-                                asm volatile("v_writelane_b32 %0, %1, m0\n\ts_mov_b32 m0, %2\n\ts_nop 1\n\t"
-                                             "v_writelane_b32 %0, %3, m0"
-                                             : "+v"(tc) : "s"(c), "s"(j2), "s"(c2) : "m0");
-                            } else {
-                                const float d = point_d2_fast<false>(W.qsx[j], W.qsy[j], W.qsz[j],
-                                                                     ux, uy, uz, L);
-                                const uint32_t c = (uint32_t)__popcll(__ballot(d <= r2));
-                                asm volatile("v_writelane_b32 %0, %1, m0" : "+v"(tc) : "s"(c));
-                            }
-                        }
-#elif NBKD_BALL_V2
-                        // lanes past the chunk hold FLT_MAX (d2 = inf): no mask AND
-                        const float ux = pv ? px : FLT_MAX, uy = pv ? py : FLT_MAX,
-                                    uz = pv ? pz : FLT_MAX;
-                        while (rem) {
-                            const int j = __builtin_ctzll(rem);
-                            rem &= ~(1ull << j);
-#if NBKD_BALL_M0EARLY
-                            asm volatile("s_mov_b32 m0, %0" : : "s"(j) : "m0");
-#endif
-                            const float4 sq = W.qs[j]; // LDS broadcast
-                            if (rem) {
-                                const int j2 = __builtin_ctzll(rem);
-                                rem &= ~(1ull << j2);
-                                const float4 sq2 = W.qs[j2];
-                                const float d = point_d2_fast<false>(sq.x, sq.y, sq.z, ux, uy, uz, L);
-                                const float d2 = point_d2_fast<false>(sq2.x, sq2.y, sq2.z, ux, uy, uz, L);
-                                const uint32_t c = (uint32_t)__popcll(__ballot(d <= r2));
-                                const uint32_t c2 = (uint32_t)__popcll(__ballot(d2 <= r2));
-#if NBKD_BALL_M0EARLY
-                                asm volatile("v_writelane_b32 %0, %1, m0\n\ts_mov_b32 m0, %2\n\ts_nop 1\n\t"
-                                             "v_writelane_b32 %0, %3, m0"
-                                             : "+v"(tc) : "s"(c), "s"(j2), "s"(c2) : "m0");
-#else
-                                lane_write(tc, c, j);
-                                lane_write(tc, c2, j2);
-#endif
-                            } else {
-                                const float d = point_d2_fast<false>(sq.x, sq.y, sq.z, ux, uy, uz, L);
-                                const uint32_t c = (uint32_t)__popcll(__ballot(d <= r2));
-#if NBKD_BALL_M0EARLY
-                                asm volatile("v_writelane_b32 %0, %1, m0" : "+v"(tc) : "s"(c));
-#else
-                                lane_write(tc, c, j);
-#endif
-                            }
-                        }
-#else
-                        while (rem) {
-                            const int j = __builtin_ctzll(rem);
-                            rem &= rem - 1;
-                            const float4 sq = W.qs[j]; // LDS broadcast
-                            if (rem) {
-                                const int j2 = __builtin_ctzll(rem);
-                                rem &= rem - 1;
-                                const float4 sq2 = W.qs[j2];
-                                const float d = point_d2_fast<false>(sq.x, sq.y, sq.z, px, py, pz, L);
-                                const float d2 = point_d2_fast<false>(sq2.x, sq2.y, sq2.z, px, py, pz, L);
-                                const uint32_t c = (uint32_t)__popcll(__ballot(d <= r2) & pvm);
-                                const uint32_t c2 = (uint32_t)__popcll(__ballot(d2 <= r2) & pvm);
-                                lane_write(tc, c, j);
-                                lane_write(tc, c2, j2);
-                            } else {
-                                const float d = point_d2_fast<false>(sq.x, sq.y, sq.z, px, py, pz, L);
-                                const uint32_t c = (uint32_t)__popcll(__ballot(d <= r2) & pvm);
-                                lane_write(tc, c, j);
-                            }
-                        }
-#endif
-                    } else {
-                        while (rem) {
-                            const int j = __builtin_ctzll(rem);
-                            rem &= rem - 1;
-                            const float4 sq = W.qs[j]; // LDS broadcast
-                            const float d = point_d2_fast<M>(sq.x, sq.y, sq.z, px, py, pz, L);
-                            const uint32_t c = (uint32_t)__popcll(__ballot(d <= r2) & pvm);
-                            lane_write(tc, c, j);
-                        }
-                    }
-                    cnt += tc;
-                    if constexpr (STATS) {
-                        const uint32_t nst = (uint32_t)__popcll(pm);
-                        bst[3] += nst;
-                        bst[1] += nst * cn;
-                    }
-                    NBKD_BPH(3);
-                    // (round 4: before, each step added its count with
-                    // cnt += lane == j ? c : 0 and ballotted pv && d <= r2: 5 more
-                    // VALU a step; 100.9 -> 98.3 ms at 1e8, r = 0.01, same counts,
-                    // profiles/r04ac_ab_ball_writelane.txt)
-                }
-            }
-            if (part && !trans) {
-                // each lane loops over the staged points (one 16-B LDS read each)
+            if (part) {
 #pragma unroll 2
                 for (uint32_t u = 0; u < cn; ++u) {
                     const float4 a = W.p4[u];
                     if (point_d2_fast<M>(qx, qy, qz, a.x, a.y, a.z, L) <= thr) {
-                        if constexpr (FILL) out_idx[wpos + cnt] = __float_as_uint(a.w);
+                        out_idx[wpos + cnt] = __float_as_uint(a.w);
                         ++cnt;
                     }
                 }
             }
-            if constexpr (STATS) {
-                if (__any(part && !trans)) {
-                    ++bst[7];
-                    bst[1] += (uint32_t)__popcll(__ballot(part)) * cn;
-                }
-            }
-            NBKD_BPH(4);
         }
     }
-#undef NBKD_BPH
 }
 
-template <bool PER, bool FILL, bool STATS>
-__global__ void __launch_bounds__(TB, BALL_OCC[PER][FILL])
-ball_packet_kernel(DevTree t, const uint32_t *__restrict__ linfo, const float *__restrict__ q,
-                   const uint32_t *__restrict__ order, uint32_t m, float r2, PadLeaves pad,
-                   uint32_t *__restrict__ out_count, const uint64_t *__restrict__ row_offsets,
-                   uint32_t *__restrict__ out_idx, uint32_t tnum, bool plain_ok,
-                   unsigned long long *__restrict__ stats) {
+template <bool PER>
+__global__ void __launch_bounds__(TB, 8)
+ball_fill_kernel(DevTree t, const uint32_t *__restrict__ linfo, const float *__restrict__ q,
+                 const uint32_t *__restrict__ order, uint32_t m, float r2, PadLeaves pad,
+                 const uint64_t *__restrict__ row_offsets, uint32_t *__restrict__ out_idx) {
     __shared__ BallLds Wl[WPB];
-    // (threadIdx.x >> 6 as is: the wave-uniform wave_id() made this kernel slower,
-    // 100.6 -> 104.7 ms at 1e8, profiles/r04v_ab_uniform_wave.txt)
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     BallLds &W = Wl[wave];
     const uint32_t gq = (xcd_block(blockIdx.x, gridDim.x) * WPB + wave) * 64u + lane;
@@ -349,47 +149,30 @@ ball_packet_kernel(DevTree t, const uint32_t *__restrict__ linfo, const float *_
         !PER || (qx >= 0.0f && qx <= L && qy >= 0.0f && qy <= L && qz >= 0.0f && qz <= L);
     const bool active = valid && inside;
     const float thr = active ? r2 : -INFINITY;
-    const uint64_t wpos = (FILL && active) ? row_offsets[qo] : 0;
-    uint32_t cnt = 0;
-    if constexpr (!FILL) W.qs[lane] = make_float4(qx, qy, qz, 0.0f);
-#if NBKD_BALL_V4
-    if constexpr (!FILL) {
-        W.qsx[lane] = qx;
-        W.qsy[lane] = qy;
-        W.qsz[lane] = qz;
-    }
-#endif
-
+    const uint64_t wpos = active ? row_offsets[qo] : 0;
     // every active lane's ball clears the box faces by a margin r' > r: the
     // plain formulas then give the periodic ones' bits for every point within
     // r and fail the test for every point beyond (knn_collect.hip
-    // collect_packet), so the packet walks and counts with them
+    // collect_packet), so the packet walks and tests with them
     bool plain = false;
     if constexpr (PER) {
         const float r1 = sqrtf(fmaxf(r2, 0.0f)) * 1.01f + L * 1e-6f;
         const bool wf = !active || (r1 <= 0.25f * L && qx >= r1 && L - qx >= r1 && qy >= r1 &&
                                     L - qy >= r1 && qz >= r1 && L - qz >= r1);
-        plain = plain_ok && __all(wf);
+        plain = __all(wf);
     }
-    uint32_t bst[BALL_NST] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     if (plain)
-        ball_walk<PER, false, FILL, STATS>(t, linfo, r2, pad, out_idx, tnum, plain_ok, W, lane, qx,
-                                           qy, qz, thr, wpos, cnt, bst);
+        ball_fill_walk<PER, false>(t, linfo, pad, out_idx, W, lane, qx, qy, qz, thr, wpos);
     else
-        ball_walk<PER, PER, FILL, STATS>(t, linfo, r2, pad, out_idx, tnum, plain_ok, W, lane, qx,
-                                         qy, qz, thr, wpos, cnt, bst);
-    if (active && out_count) out_count[qo] = cnt;
-    if constexpr (STATS) {
-        // the nbkd_stats_read_all slots of a radius count (capi.BALL_STATS_NAMES)
-        constexpr int slot[BALL_NST] = {0, 1, 2, 3, 4, 6, 7, 8, 10, 11, 12, 13, 14};
-        if (lane == 0) {
-#pragma unroll
-            for (int i = 0; i < BALL_NST; ++i)
-                atomicAdd(&stats[slot[i]], (unsigned long long)bst[i]);
-            atomicAdd(&stats[5], 1ull);
-        }
-    }
+        ball_fill_walk<PER, PER>(t, linfo, pad, out_idx, W, lane, qx, qy, qz, thr, wpos);
 }
+
+// STATS (ball_count2_kernel's instrumented instance): bst = node visits,
+// points evaluated, leaves needed, transposed steps, points staged, full
+// (query, leaf) pairs, partial (query, leaf) pairs, per-lane-loop chunks,
+// then the s_memtime phase clocks walk / leaf test / staging wait /
+// transposed steps / per-lane loop
+constexpr int BALL_NST = 13;
 
 // ------------------------------------------------------ 128-query packets (count)
 // Two queries per lane: A = sorted position 128 p + lane, B = A + 64.  One walk
@@ -628,12 +411,9 @@ __device__ __forceinline__ void ball_walk2(const DevTree &t, const uint32_t *__r
                 // many partial queries: each lane loops over the staged points
                 // for its two queries (one LDS read per point for both; one
                 // loop per set read every point twice and, latency-bound, ran
-                // the count 78.4 -> 88.2 ms per 1e8, profiles/r05f_ball_ab.txt)
-#if NBKD_BALL_LL_UNROLL2
-#pragma unroll 2
-#else
+                // the count 78.4 -> 88.2 ms per 1e8, profiles/r05f_ball_ab.txt;
+                // unrolled by 2 it spilled 16 B and ran 77.2 -> 78.0 ms, r05g)
 #pragma unroll 1
-#endif
                 for (uint32_t u = 0; u < cn; ++u) {
                     const float4 a = W.p4[u];
                     cntA += (partA && point_d2_fast<M>(ax, ay, az, a.x, a.y, a.z, L) <= thrA) ? 1u : 0u;
@@ -800,11 +580,12 @@ void launch_ball_outside(const Tree &t, const float *q, const uint32_t *list, ui
 void launch_ball_packet(const Tree &t, const float *q, const uint32_t *order, uint32_t m, float r2,
                         uint32_t *out_count, const uint64_t *row_offsets, uint32_t *out_idx,
                         unsigned long long *stats, hipStream_t s) {
-    const unsigned blocks = (unsigned)((m + TB - 1) / TB);
-    // transposed count threshold (x/8 partial lanes per staged point); 0 = off
+    // transposed-count threshold: a chunk runs the transposed steps while
+    // #partial queries x 8 <= #points x tnum (128-query packets: 12 measured
+    // best of 8, 12, 16, 24, 32, profiles/r05g_ball_ab.txt); 0 = never
     static const uint32_t tnum = [] {
         const char *e = knob("NBKD_BALL_T");
-        return e ? (uint32_t)atoi(e) : 8u;
+        return e ? (uint32_t)atoi(e) : 12u;
     }();
     // NBKD_BALL_PLAIN=0 (experiments build): the periodic d2 at every leaf (A/B)
     static const bool plain_ok = [] {
@@ -814,37 +595,27 @@ void launch_ball_packet(const Tree &t, const float *q, const uint32_t *order, ui
     PadLeaves pad;
     for (int j = 0; j < NBKD_PAD_LEAVES; ++j)
         pad.id[j] = t.npad_leaves <= NBKD_PAD_LEAVES ? t.pad_leaves[j] : 0xFFFFFFFFu;
-#define NBKD_BALL(PER, FILL, STATS)                                                            \
-    ball_packet_kernel<PER, FILL, STATS><<<blocks, TB, 0, s>>>(                                \
-        view(t), t.leafinfo, q, order, m, r2, pad, out_count, row_offsets, out_idx, tnum,      \
-        plain_ok, stats)
-#if NBKD_BALL_64
-    if (t.periodic) {
-        if (out_idx) NBKD_BALL(true, true, false);
-        else if (stats) NBKD_BALL(true, false, true);
-        else NBKD_BALL(true, false, false);
-    } else {
-        if (out_idx) NBKD_BALL(false, true, false);
-        else if (stats) NBKD_BALL(false, false, true);
-        else NBKD_BALL(false, false, false);
+    if (out_idx) { // CSR fill: 64-query packets
+        const unsigned blocks = (unsigned)((m + TB - 1) / TB);
+        if (t.periodic)
+            ball_fill_kernel<true><<<blocks, TB, 0, s>>>(view(t), t.leafinfo, q, order, m, r2, pad,
+                                                         row_offsets, out_idx);
+        else
+            ball_fill_kernel<false><<<blocks, TB, 0, s>>>(view(t), t.leafinfo, q, order, m, r2,
+                                                          pad, row_offsets, out_idx);
+        return;
     }
-#else
-    // count: 128-query packets (ball_count2_kernel); CSR fill: 64-query packets
+    // count: 128-query packets
     const unsigned blocks2 = (unsigned)((m + 128 * WPB - 1) / (128 * WPB));
 #define NBKD_BALL2(PER, STATS)                                                                     \
     ball_count2_kernel<PER, STATS><<<blocks2, TB, 0, s>>>(view(t), t.leafinfo, q, order, m, r2,   \
                                                           pad, out_count, tnum, plain_ok, stats)
-    if (out_idx) {
-        if (t.periodic) NBKD_BALL(true, true, false);
-        else NBKD_BALL(false, true, false);
-    } else if (t.periodic) {
+    if (t.periodic) {
         if (stats) NBKD_BALL2(true, true); else NBKD_BALL2(true, false);
     } else {
         if (stats) NBKD_BALL2(false, true); else NBKD_BALL2(false, false);
     }
 #undef NBKD_BALL2
-#endif
-#undef NBKD_BALL
 }
 
 } // namespace nbkd

@@ -18,6 +18,8 @@
 #   ab        scripts/gpu_ab.sh with LIBS / BALL_LIBS / ARGS / ROUNDS
 #   final     smoke() + the default bench line
 #   probe     each command of PROBE ("cmd1; cmd2; ..."), 600 s each, into probe.log
+#   summarize summarize_prof.py / summarize_step.py on the box (profiles/<tag>_*,
+#             copied to $O/profiles), so a later bench / suite step matches them
 # Afterwards, in the build container:
 #   python scripts/summarize_prof.py gpurun_out/$TAG $TAG     (trace, pmc)
 #   python scripts/summarize_step.py gpurun_out/$TAG $TAG     (step)
@@ -95,6 +97,14 @@ step_pmc() {
 }
 step_step() {
   steps4 step --n 1e8 --k 32
+}
+# summarise trace / pmc / step on the box too (so a later bench step of this
+# call finds this build's profiles); the summaries are copied back under $O
+step_summarize() {
+  say summarize
+  python3 scripts/summarize_prof.py $O $TAG > $O/summarize.log 2>&1 && \
+  { [ ! -d $O/step ] || python3 scripts/summarize_step.py $O/step $TAG >> $O/summarize.log 2>&1; } && \
+  mkdir -p $O/profiles && cp profiles/${TAG}_* $O/profiles/
 }
 step_slab() {
   local s w sc n

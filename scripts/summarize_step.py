@@ -41,6 +41,8 @@ def main():
     tot_f = sum(v["fetch_bytes"] for v in kern.values())
     tot_w = sum(v["write_bytes"] for v in kern.values())
     shaf = os.path.join(src, "lib.sha256")
+    if not os.path.exists(shaf):  # gpu_run.sh keeps it one level up (<tag>/step/)
+        shaf = os.path.join(os.path.dirname(os.path.normpath(src)), "lib.sha256")
     out = {
         "lib_sha256": open(shaf).read().split()[0] if os.path.exists(shaf) else None,
         "workload": "nbkd_query_knn of every particle, 1e8 uniform periodic, k = 32, leafsize 64",
