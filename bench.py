@@ -499,7 +499,7 @@ def suite(args, capi, hip, tree, dev_pts, n, k, L, stream, od, oi):
         traffic, tsrc = pmc_traffic(n, k, n, kind="ball")
         out["radius_count"]["roofline"] = roofline_entry(
             traffic, tsrc, kern_ms / steps, ach,
-            kernel="ball_packet_kernel<periodic, count> (nbodyhpc_amd/csrc/ball.hip)",
+            kernel="ball_count2_kernel<periodic> (nbodyhpc_amd/csrc/ball.hip)",
             bytes_per_query=br, queries_per_launch=n)
     log(f"suite: radius count {n / sec:.3e} q/s, mean {c.mean():.1f} (expect {expect:.1f})")
     # C3: CSR batch (host in / host out: PCIe-inclusive)

@@ -1,4 +1,4 @@
-"""The C3 radius count alone (for rocprofv3 PMC passes of ball_packet_kernel):
+"""The C3 radius count alone (for rocprofv3 PMC passes of ball_count2_kernel):
 1e8 uniform periodic points (the bench's), leafsize 64, r = 0.01 L, every
 particle counted, `--steps` timed passes after one untimed."""
 import argparse

@@ -87,13 +87,13 @@ step_trace() {
 step_pmc() {
   pmc fetch FETCH_SIZE "knn_collect|knn_select" $B \
     && pmc write WRITE_SIZE "knn_collect|knn_select" $B \
-    && pmc ball_fetch FETCH_SIZE ball_packet $BR \
-    && pmc ball_write WRITE_SIZE ball_packet $BR \
+    && pmc ball_fetch FETCH_SIZE ball_count2 $BR \
+    && pmc ball_write WRITE_SIZE ball_count2 $BR \
     && pmc pmc_sq1 "$SQ1" "knn_collect|knn_select" $B \
     && pmc pmc_sq2 "$SQ2" "knn_collect|knn_select" $B \
     && pmc pmc_tcc "$TCC" "knn_collect|knn_select" $B \
-    && pmc ball_sq1 "$SQ1" ball_packet $BR \
-    && pmc ball_sq2 "$SQ2" ball_packet $BR
+    && pmc ball_sq1 "$SQ1" ball_count2 $BR \
+    && pmc ball_sq2 "$SQ2" ball_count2 $BR
 }
 step_step() {
   steps4 step --n 1e8 --k 32

@@ -100,7 +100,7 @@ def main():
         with open(trace) as f:
             for row in csv.DictReader(f):
                 name = row["Kernel_Name"]
-                if not any(r in name for r in (regex, "knn_select", "ball_packet")):
+                if not any(r in name for r in (regex, "knn_select", "ball_count2")):
                     continue
                 key = (name[:120], int(row["Grid_Size_X"]))
                 ms = (int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) * 1e-6
@@ -156,15 +156,15 @@ def main():
     bf = find(os.path.join(src, "ball_fetch"), "*counter_collection.csv")
     bw = find(os.path.join(src, "ball_write"), "*counter_collection.csv")
     if bf and bw:
-        fv = per_dispatch(bf, "ball_packet")
-        wv = per_dispatch(bw, "ball_packet")
+        fv = per_dispatch(bf, "ball_count2")
+        wv = per_dispatch(bw, "ball_count2")
         f_kib, w_kib = sum(fv) / len(fv), sum(wv) / len(wv)
         shaf = os.path.join(src, "lib.sha256")
         out = {
             "lib_sha256": open(shaf).read().split()[0] if os.path.exists(shaf) else None,
-            "kernel": "ball_packet_kernel<periodic, count> (nbodyhpc_amd/csrc/ball.hip)",
+            "kernel": "ball_count2_kernel<periodic> (nbodyhpc_amd/csrc/ball.hip)",
             "command": "rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE --kernel-include-regex "
-                       "ball_packet -- python3 scripts/ball_run.py",
+                       "ball_count2 -- python3 scripts/ball_run.py",
             "n_particles": 100_000_000, "r": 0.01, "queries_per_launch": 100_000_000,
             "dispatches": [len(fv), len(wv)],
             "FETCH_SIZE_KiB_per_launch": f_kib, "WRITE_SIZE_KiB_per_launch": w_kib,
