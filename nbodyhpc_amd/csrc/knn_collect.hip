@@ -478,7 +478,11 @@ __device__ __forceinline__ void issue_block(const uint4 *b4, uint4 *lds4, int la
 #pragma unroll
     for (int i = 0; i < 8; ++i)
         if (m & (1u << i))
+#if NBKD_SEL_NT
+            __builtin_amdgcn_global_load_lds((gas_ptr)(src + 64 * i), (las_ptr)(lds4 + 64 * i), 16, 0, 2);
+#else
             __builtin_amdgcn_global_load_lds((gas_ptr)(src + 64 * i), (las_ptr)(lds4 + 64 * i), 16, 0, 0);
+#endif
 }
 
 // One lane per query: the k smallest of its candidate column, sorted, as rows.

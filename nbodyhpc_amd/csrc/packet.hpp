@@ -69,7 +69,11 @@ __device__ __forceinline__ void store_rows(const uint32_t *stage, const uint32_t
             uint32_t v = stage[j * 64 + (row ^ j)];
             if (qr != 0xFFFFFFFFu) {
                 if (remap && v != 0xFFFFFFFFu) v = remap[v];
+#if NBKD_SEL_NT
+                __builtin_nontemporal_store(v, &dst[(size_t)qr * k + c0 + j]);
+#else
                 dst[(size_t)qr * k + c0 + j] = v;
+#endif
             }
         }
         return;
