@@ -285,6 +285,10 @@ struct QSpan {
     uint32_t base;         // this pass's first entry of the device-counted list
     uint32_t total;        // queries of the call (density test)
     int mode;              // 0: always; 1: only dense; 2: only sparse
+    // a device-counted pass that is usually empty (round 1's later batches):
+    // its select runs on a capped grid that strides over the wave-blocks
+    // (cheap when empty) instead of one wave per 64 queries of the cap
+    bool capped = false;
 };
 __host__ __device__ inline QSpan static_span(uint32_t m) { return QSpan{m, nullptr, 0u, 0u, 0}; }
 __device__ __forceinline__ uint32_t span_m(const QSpan &s) {

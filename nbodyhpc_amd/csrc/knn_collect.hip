@@ -478,11 +478,8 @@ __device__ __forceinline__ void issue_block(const uint4 *b4, uint4 *lds4, int la
 #pragma unroll
     for (int i = 0; i < 8; ++i)
         if (m & (1u << i))
-#if NBKD_SEL_NT
+            // non-temporal (aux 2 = nt): each column line is read once
             __builtin_amdgcn_global_load_lds((gas_ptr)(src + 64 * i), (las_ptr)(lds4 + 64 * i), 16, 0, 2);
-#else
-            __builtin_amdgcn_global_load_lds((gas_ptr)(src + 64 * i), (las_ptr)(lds4 + 64 * i), 16, 0, 0);
-#endif
 }
 
 // One lane per query: the k smallest of its candidate column, sorted, as rows.
@@ -1052,11 +1049,15 @@ void launch_select(const Tree &t, const float *q, const uint32_t *order, QSpan s
                    float *od, uint32_t *oi, uint32_t *fail_list, uint32_t *fail_count,
                    uint32_t *fail_bits, uint32_t pos_base, float *tg_fix, float mu, bool sq,
                    hipStream_t s) {
-    // a device-counted pass: at most resident_blocks() blocks striding over
-    // its wave-blocks (LOOP); a static one: one wave per 64 queries
+    // a capped pass (round 1's later batches, usually empty): at most
+    // resident_blocks() blocks striding over its wave-blocks (LOOP); any other
+    // pass one wave per 64 queries of its count or cap, at 4 waves per SIMD
+    // (the LOOP instance runs at 2: the dense log-normal retry's select took
+    // 8.7 -> 10.4 ms per 1e8 with every round-1 batch capped, r05i suite)
+    const bool loop = span.count && span.capped;
     const unsigned blocks =
-        span.count ? (unsigned)std::min<uint64_t>((span.m + TB - 1) / TB, resident_blocks())
-                   : (span.m + TB - 1) / TB;
+        loop ? (unsigned)std::min<uint64_t>((span.m + TB - 1) / TB, resident_blocks())
+             : (span.m + TB - 1) / TB;
     static const uint64_t all_rows = [] { // NBKD_SELECT_ROWMASK=0: read whole blocks
         const char *e = knob("NBKD_SELECT_ROWMASK");
         return (e && atoi(e) == 0) ? ~0ull : 0ull;
@@ -1066,7 +1067,7 @@ void launch_select(const Tree &t, const float *q, const uint32_t *order, QSpan s
                                                             cand, capg, ccount, od, oi, fail_list, \
                                                             fail_count, pos_base, all_rows,        \
                                                             tg_fix, mu, sq, fail_bits)
-    if (span.count) {
+    if (loop) {
         if (t.periodic) {
             if (qpp == 64) NBKD_SELECT(true, true, true); else NBKD_SELECT(true, false, true);
         } else {
