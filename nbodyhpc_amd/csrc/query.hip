@@ -105,14 +105,14 @@ __global__ void __launch_bounds__(TB)
 leaf_key3_kernel(const float4 *__restrict__ hb, int o, uint32_t n8, uint32_t leaf,
                  const float *__restrict__ q, uint32_t m, uint32_t *__restrict__ keys,
                  uint32_t *__restrict__ vals, float *__restrict__ tg, float mu_c, uint32_t anchor,
-                 float3 box_lo, float3 box_hi, int rule, float ratio) {
+                 float3 box_lo, float3 box_hi) {
     for (uint32_t i = blockIdx.x * TB + threadIdx.x; i < m; i += gridDim.x * TB) {
         const float p[3] = {q[3 * (size_t)i], q[3 * (size_t)i + 1], q[3 * (size_t)i + 2]};
         uint32_t left = 0, count = n8;
         int dim = 0;
         float lo[3] = {box_lo.x, box_lo.y, box_lo.z}, hi[3] = {box_hi.x, box_hi.y, box_hi.z};
-        float r2 = FLT_MAX, r2p = FLT_MAX;
-        bool have_r2 = tg == nullptr, have_r2p = tg == nullptr || rule == 0;
+        float r2 = FLT_MAX;
+        bool have_r2 = tg == nullptr;
         // line b of block level j (level start `base`, `nb` lines); first level l0
         uint32_t b = 0, base = 0, nb = 1;
         int l0 = o;
@@ -124,10 +124,6 @@ leaf_key3_kernel(const float4 *__restrict__ hb, int o, uint32_t n8, uint32_t lea
             for (int l = 0; l < 4; ++l) {
                 if (l < l0) continue;
                 if (count <= leaf) break;
-                if (!have_r2p && count <= 2 * anchor) {
-                    r2p = guess_r2(count, lo, hi, mu_c);
-                    have_r2p = true;
-                }
                 if (!have_r2 && count <= anchor) {
                     r2 = guess_r2(count, lo, hi, mu_c);
                     have_r2 = true;
@@ -166,13 +162,6 @@ leaf_key3_kernel(const float4 *__restrict__ hb, int o, uint32_t n8, uint32_t lea
             l0 = 0;
         }
         if (!have_r2) r2 = guess_r2(count, lo, hi, mu_c);
-        // experiments (NBKD_SEED_RULE): the parent subtree's density against
-        // the anchor's, at density gradients (cluster edges)
-        if (rule != 0 && r2p < FLT_MAX && r2 < FLT_MAX) {
-            if (rule == 1) r2 = fmaxf(r2, r2p);
-            else if (rule == 2 && r2p > ratio * r2) r2 = r2p;
-            else if (rule == 3 && r2p > r2) r2 = sqrtf(r2 * r2p);
-        }
         keys[i] = left >> 3;
         vals[i] = i;
         if (tg) tg[i] = r2;
@@ -826,15 +815,6 @@ struct SeedParams {
     float mu_c;
     uint32_t anchor;
 };
-int seed_rule() {
-    const char *e = knob("NBKD_SEED_RULE");
-    return e ? atoi(e) : 0;
-}
-float seed_ratio() {
-    const char *e = knob("NBKD_SEED_RATIO");
-    return e ? (float)atof(e) : 1.5f;
-}
-
 SeedParams seed_params(const Tree &t, int k) {
     // a = 3.5: at 1e8 uniform 1.400e9 q/s (20.5 k retries) vs 1.376e9 at a = 4
     // (4.9 k), 1.393e9 at 3, 1.372e9 at 2.5, 1.361e9 at 5; log-normal 82.3 ms
@@ -875,8 +855,7 @@ nbkd_status sort_queries(const Tree &t, Workspace &ws, const float *dq, uint32_t
             leaf_key3_kernel<<<blocks, TB, 0, s>>>((const float4 *)t.hsplit, hblk_offset(t.depth),
                                                    (uint32_t)t.n8, (uint32_t)t.leaf, dq, m,
                                                    keys, order, tg, sp ? sp->mu_c : 0.0f,
-                                                   sp ? sp->anchor : 0u, lo, hi, seed_rule(),
-                                                   seed_ratio());
+                                                   sp ? sp->anchor : 0u, lo, hi);
         } else if (t.shape_len <= SHAPE_MAX) {
             const unsigned blocks = (unsigned)std::min<uint64_t>((m + TB - 1) / TB, 8192);
             // periodic: the box; otherwise the real points' bounding box (the
