@@ -158,6 +158,12 @@ void nbkd_free(nbkd_tree *tree);
  *                      about 1 GiB of queries plus results per batch).
  *   "host_threads"     threads copying between the caller's host arrays and
  *                      pinned staging (default 0 = the usable cores, <= 16).
+ *   "self_order"       1 (default): a kNN / k-th query whose queries are the
+ *                      first m rows of the device array the tree was built from
+ *                      (same pointer, NBKD_INPUT_DEVICE) runs in tree order
+ *                      instead of bucketing and sorting the queries; 0: always
+ *                      bucket and sort.  Results never depend on it (the order
+ *                      and the seeds only steer the work).
  * NEW (no reference counterpart: kdtree/src/cpp/pybind.cpp:196-216 has no knobs). */
 nbkd_status nbkd_set_tuning(const char *name, double value);
 nbkd_status nbkd_get_tuning(const char *name, double *value);

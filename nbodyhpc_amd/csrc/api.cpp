@@ -53,6 +53,9 @@ void free_tree(Tree &t) {
     tree_free(t.y);
     tree_free(t.z);
     tree_free(t.idx);
+    tree_free(t.sidx);
+    t.sidx = nullptr;
+    t.src = nullptr;
     tree_free(t.p4);
     t.p4 = nullptr;
     tree_free(t.nodes);
@@ -221,9 +224,9 @@ void tree_free(void *p) {
 
 namespace {
 // nbkd_set_tuning knobs (process-wide); defaults are the measured optima
-std::atomic<double> g_tune[TUNE_N] = {{3.5}, {0.0}, {0.0}, {0.0}};
+std::atomic<double> g_tune[TUNE_N] = {{3.5}, {0.0}, {0.0}, {0.0}, {1.0}};
 const char *const g_tune_names[TUNE_N] = {"knn_seed_margin", "candidate_bytes", "host_batch",
-                                          "host_threads"};
+                                          "host_threads", "self_order"};
 thread_local nbkd_interrupt_fn t_intr = nullptr;
 thread_local void *t_intr_user = nullptr;
 } // namespace
@@ -479,6 +482,7 @@ nbkd_status nbkd_build(const float *xyz, uint64_t n, int32_t leaf_size, int32_t 
         delete h;
         return st;
     }
+    if (flags & NBKD_INPUT_DEVICE) h->t.src = xyz;
     *out = h;
     return NBKD_OK;
     NBKD_GUARD_END

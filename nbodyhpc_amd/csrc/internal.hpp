@@ -22,7 +22,7 @@ namespace nbkd {
 enum WsSlot {
     WS_Q = 0, WS_KEYS, WS_KEYS2, WS_ORDER, WS_TMP, WS_HIST, WS_SUMS, WS_OUTD, WS_OUTI,
     WS_COUNT, WS_OFF, WS_IDX, WS_STATS, WS_LIST, WS_LT, WS_TG, WS_CAND, WS_CCOUNT,
-    WS_LIST2, WS_RSORT, WS_KTHD, WS_KTHI, WS_KB,
+    WS_LIST2, WS_RSORT, WS_KTHD, WS_KTHI, WS_KB, WS_ANCH,
     // host-buffer pipeline (query.hip host_pipeline): two slots of queries and
     // of up to two result arrays
     WS_HQ0, WS_HQ1, WS_HO00, WS_HO01, WS_HO10, WS_HO11, WS_NSLOTS
@@ -140,6 +140,12 @@ struct Tree {
     // only and reads a popped node's box here
     float *nbox = nullptr;
     float bbox_lo[3] = {0.0f, 0.0f, 0.0f}, bbox_hi[3] = {0.0f, 0.0f, 0.0f}; // of the real points
+    // self queries (query.hip self_order): the device array the tree was built
+    // from (nullptr for a host input), and the build's permutation (tree
+    // position -> input row) once nbkd_set_ids has replaced idx's ids;
+    // nullptr: idx is that permutation
+    const float *src = nullptr;
+    uint32_t *sidx = nullptr;
     // leaves holding padding points (FLT_MAX, n <= position id < n8): node ids
     int npad_leaves = 0;
     uint32_t pad_leaves[NBKD_PAD_LEAVES] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu,
@@ -193,7 +199,14 @@ inline const char *knob(const char *env) { return getenv(env); }
 #else
 inline const char *knob(const char *) { return nullptr; }
 #endif
-enum TuneId { TUNE_KNN_SEED = 0, TUNE_CAND_BYTES, TUNE_HOST_BATCH, TUNE_HOST_THREADS, TUNE_N };
+enum TuneId {
+    TUNE_KNN_SEED = 0,
+    TUNE_CAND_BYTES,
+    TUNE_HOST_BATCH,
+    TUNE_HOST_THREADS,
+    TUNE_SELF_ORDER,
+    TUNE_N
+};
 // host memcpy split over the library's copy threads (api.cpp): the host-buffer
 // pipeline's pinned staging <-> the caller's arrays; small copies stay on the
 // calling thread
@@ -289,6 +302,9 @@ struct QSpan {
     // its select runs on a capped grid that strides over the wave-blocks
     // (cheap when empty) instead of one wave per 64 queries of the cap
     bool capped = false;
+    // tg is indexed by the position in this pass's order (self queries: the
+    // seed per tree position), not by query id
+    bool tg_pos = false;
 };
 __host__ __device__ inline QSpan static_span(uint32_t m) { return QSpan{m, nullptr, 0u, 0u, 0}; }
 __device__ __forceinline__ uint32_t span_m(const QSpan &s) {

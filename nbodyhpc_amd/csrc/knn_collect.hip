@@ -348,7 +348,7 @@ template <bool PER, bool STATS, bool AHEAD>
 __device__ __forceinline__ void collect_packet(
     const DevTree &t, const float *__restrict__ ginfo, const uint32_t *__restrict__ linfo,
     const float *__restrict__ hinfo, const float *__restrict__ q, const uint32_t *__restrict__ order,
-    uint32_t m, int kq, const float *__restrict__ tg, float seed_mul, uint32_t qpp,
+    uint32_t m, int kq, const float *__restrict__ tg, bool tg_pos, float seed_mul, uint32_t qpp,
     uint2 *__restrict__ cand, uint32_t capg, uint32_t *__restrict__ ccount,
     unsigned long long *__restrict__ stats, float *__restrict__ kbound, CollectLdsG &W, int lane,
     uint32_t pk) {
@@ -358,7 +358,7 @@ __device__ __forceinline__ void collect_packet(
     const float qx = valid ? q[3 * (size_t)qo] : 0.0f;
     const float qy = valid ? q[3 * (size_t)qo + 1] : 0.0f;
     const float qz = valid ? q[3 * (size_t)qo + 2] : 0.0f;
-    const float seed = valid ? fminf(tg[qo] * seed_mul, FLT_MAX) : -INFINITY;
+    const float seed = valid ? fminf(tg[tg_pos ? gq : qo] * seed_mul, FLT_MAX) : -INFINITY;
     const bool fin = seed < FLT_MAX && seed >= 1e-30f;
     const float s_over_nb = fin ? seed * (1.0f / NB) : (seed > 0.0f ? INFINITY : 0.0f);
     const float nb_over_s = fin ? (float)NB / seed * 1.00000095367431640625f : 0.0f;
@@ -437,14 +437,16 @@ knn_collect_grp_kernel(DevTree t, const float *__restrict__ ginfo,
     if constexpr (LOOP) {
         for (uint32_t pk = bid * WPB + wave; pk < npk; pk += gridDim.x * WPB) {
             wave_sync(); // the previous packet's LDS reads are done
-            collect_packet<PER, STATS, AHEAD>(t, ginfo, linfo, hinfo, q, order, m, kq, tg, seed_mul, qpp,
-                                       cand, capg, ccount, stats, kbound, W, lane, pk);
+            collect_packet<PER, STATS, AHEAD>(t, ginfo, linfo, hinfo, q, order, m, kq, tg, span.tg_pos,
+                                              seed_mul, qpp, cand, capg, ccount, stats, kbound,
+                                              W, lane, pk);
         }
     } else {
         const uint32_t pk = bid * WPB + wave;
         if (pk < npk)
-            collect_packet<PER, STATS, AHEAD>(t, ginfo, linfo, hinfo, q, order, m, kq, tg, seed_mul, qpp,
-                                       cand, capg, ccount, stats, kbound, W, lane, pk);
+            collect_packet<PER, STATS, AHEAD>(t, ginfo, linfo, hinfo, q, order, m, kq, tg, span.tg_pos,
+                                              seed_mul, qpp, cand, capg, ccount, stats, kbound,
+                                              W, lane, pk);
     }
 }
 
@@ -495,8 +497,8 @@ select_block(const DevTree &t, const float *__restrict__ q, const uint32_t *__re
              const uint32_t *__restrict__ ccount, float *__restrict__ out_d,
              uint32_t *__restrict__ out_i, uint32_t *__restrict__ fail_list,
              uint32_t *__restrict__ fail_count, uint32_t pos_base, uint64_t all_rows,
-             float *__restrict__ tg_fix, float mu, bool sq, uint32_t *__restrict__ fail_bits,
-             uint32_t *stage, uint32_t *rowq, const int lane) {
+             float *__restrict__ tg_fix, bool tg_pos, float mu, bool sq,
+             uint32_t *__restrict__ fail_bits, uint32_t *stage, uint32_t *rowq, const int lane) {
     constexpr int NS = 16;                  // candidates merged per pass
     constexpr int CC = KC < 32 ? KC : 32;   // top-k registers staged per output pass
     // lane = one query gq; its candidates: packet gq / qpp, row gq % qpp
@@ -522,7 +524,8 @@ select_block(const DevTree &t, const float *__restrict__ q, const uint32_t *__re
                 fv = fminf(8.0f, fmaxf(2.0f, 1.5f * mu / fmaxf((float)n, 0.5f)));
             else
                 fv = fminf(1.0f, 4.0f * (float)capg / (float)n);
-            tg_fix[qo] = fminf(tg_fix[qo] * cbrtf(fv * fv), FLT_MAX);
+            const uint32_t ti = tg_pos ? gq : qo;
+            tg_fix[ti] = fminf(tg_fix[ti] * cbrtf(fv * fv), FLT_MAX);
         }
     }
     const uint32_t nn = ok ? n : 0u;
@@ -647,15 +650,15 @@ knn_select_kernel(DevTree t, const float *__restrict__ q, const uint32_t *__rest
         for (uint32_t wb = blockIdx.x * WPB + wave; wb * 64u < m; wb += gridDim.x * WPB) {
             wave_sync(); // the previous wave-block's LDS reads are done
             select_block<KC, PER, WHOLE>(t, q, order, m, wb, k, cand, capg, ccount, out_d, out_i,
-                                         fail_list, fail_count, pos_base, all_rows, tg_fix, mu,
-                                         sq, fail_bits, stage, rowq, lane);
+                                         fail_list, fail_count, pos_base, all_rows, tg_fix,
+                                         span.tg_pos, mu, sq, fail_bits, stage, rowq, lane);
         }
     } else {
         const uint32_t wb = blockIdx.x * WPB + wave;
         if (wb * 64u >= m) return;
         select_block<KC, PER, WHOLE>(t, q, order, m, wb, k, cand, capg, ccount, out_d, out_i,
-                                     fail_list, fail_count, pos_base, all_rows, tg_fix, mu, sq,
-                                     fail_bits, stage, rowq, lane);
+                                     fail_list, fail_count, pos_base, all_rows, tg_fix,
+                                     span.tg_pos, mu, sq, fail_bits, stage, rowq, lane);
     }
 }
 
@@ -828,7 +831,8 @@ knn_select_wave_kernel(DevTree t, const float *__restrict__ q, const uint32_t *_
                         fv = fminf(8.0f, fmaxf(2.0f, 1.5f * mu / fmaxf((float)n, 0.5f)));
                     else
                         fv = fminf(1.0f, 4.0f * (float)capg / (float)n);
-                    tg_fix[qo] = fminf(tg_fix[qo] * cbrtf(fv * fv), FLT_MAX);
+                    const uint32_t ti = span.tg_pos ? gq : qo;
+                    tg_fix[ti] = fminf(tg_fix[ti] * cbrtf(fv * fv), FLT_MAX);
                 }
             }
             continue;

@@ -168,6 +168,106 @@ leaf_key3_kernel(const float4 *__restrict__ hb, int o, uint32_t n8, uint32_t lea
     }
 }
 
+// Self queries (self_order below): the seed of the point at tree position p
+// comes from its anchor, the first subtree of <= anchor points that holds
+// position p -- the subtree leaf_key3_kernel's descent by the point's
+// coordinates reaches (a point tied with a split value may sit on the split's
+// other side; its seed is then only a different guess).  An anchor holds >= 64
+// points (its parent held more than anchor >= 128, and a split's smaller
+// child gets floor(count / 16) * 8), so the 64 positions of chunk c
+// (64c .. 64c + 63) meet at most two anchors: the one holding 64c and the one
+// holding 64(c + 1).  anchor_chunk_kernel finds, per chunk, the anchor holding
+// its first position -- its first position and seed -- and self_seed_kernel
+// gives position p the seed of chunk p / 64's anchor, or of the next chunk's
+// if p lies at or past that anchor's start.
+//
+// The descent turns by the counts alone (right iff p >= left + m), so it
+// loads nothing on the way: it records where in the blocked heap (internal.hpp
+// hblk_*) the last split bounding each axis from below and from above sits,
+// and the six split values load together at the end.
+struct SeedPath {
+    uint32_t left, count, b, base, nb, lp;
+    int l, dim;
+    // heap index + 1 of the last split bounding axis d from below / above
+    // (0: none, the box face); named, not an indexed private array
+    uint32_t lo0, lo1, lo2, hi0, hi1, hi2;
+};
+
+__device__ __forceinline__ void seed_turn(SeedPath &w, bool right, int o) {
+    const uint32_t mm = (w.count / 2) / 8 * 8;
+    const uint32_t at = 16u * w.b + (1u << w.l) + w.lp; // heap index + 1
+    if (right) {
+        w.lo0 = w.dim == 0 ? at : w.lo0;
+        w.lo1 = w.dim == 1 ? at : w.lo1;
+        w.lo2 = w.dim == 2 ? at : w.lo2;
+        w.left += mm;
+        w.count -= mm;
+    } else {
+        w.hi0 = w.dim == 0 ? at : w.hi0;
+        w.hi1 = w.dim == 1 ? at : w.hi1;
+        w.hi2 = w.dim == 2 ? at : w.hi2;
+        w.count = mm;
+    }
+    w.lp = 2 * w.lp + (right ? 1u : 0u);
+    w.dim = w.dim == 2 ? 0 : w.dim + 1;
+    if (++w.l == 4) { // next line: child lp of this one
+        const uint32_t nbase = w.base + w.nb;
+        w.b = nbase + (w.b - w.base) * 16u + w.lp;
+        w.nb = w.base == 0 ? (16u >> o) : w.nb * 16u;
+        w.base = nbase;
+        w.l = 0;
+        w.lp = 0;
+    }
+}
+
+// anch[c] = (first position, seed bits) of the anchor holding position 64c
+__global__ void __launch_bounds__(TB)
+anchor_chunk_kernel(const float *__restrict__ hf, int o, uint32_t n8, uint32_t stop,
+                    uint32_t nchunks, uint2 *__restrict__ anch, float mu_c, float3 box_lo,
+                    float3 box_hi) {
+    const uint32_t c = blockIdx.x * TB + threadIdx.x;
+    if (c >= nchunks) return;
+    const uint32_t p = c * 64u;
+    SeedPath w{0u, n8, 0u, 0u, 1u, 0u, o, 0, 0u, 0u, 0u, 0u, 0u, 0u};
+    while (w.count > stop) seed_turn(w, p >= w.left + (w.count / 2) / 8 * 8, o);
+    const float lo[3] = {w.lo0 ? hf[w.lo0 - 1] : box_lo.x, w.lo1 ? hf[w.lo1 - 1] : box_lo.y,
+                         w.lo2 ? hf[w.lo2 - 1] : box_lo.z};
+    const float hi[3] = {w.hi0 ? hf[w.hi0 - 1] : box_hi.x, w.hi1 ? hf[w.hi1 - 1] : box_hi.y,
+                         w.hi2 ? hf[w.hi2 - 1] : box_hi.z};
+    anch[c] = make_uint2(w.left, __float_as_uint(guess_r2(w.count, lo, hi, mu_c)));
+}
+
+// tgp[i] = the seed of position pos[i] (pos nullptr: i); with pos, also
+// order[i] = perm[pos[i]]; tgp nullptr: the order alone
+__global__ void __launch_bounds__(TB)
+self_seed_kernel(const uint2 *__restrict__ anch, uint32_t nchunks,
+                 const uint32_t *__restrict__ pos, const uint32_t *__restrict__ perm, uint32_t m,
+                 uint32_t *__restrict__ order, float *__restrict__ tgp) {
+    for (uint32_t i = blockIdx.x * TB + threadIdx.x; i < m; i += gridDim.x * TB) {
+        const uint32_t p = pos ? pos[i] : i;
+        if (pos) order[i] = perm[p];
+        if (!tgp) continue;
+        const uint32_t c = p >> 6;
+        const uint2 a = anch[c];
+        const uint2 b = c + 1 < nchunks ? anch[c + 1] : a;
+        tgp[i] = __uint_as_float(p >= b.x ? b.y : a.y);
+    }
+}
+
+// bits[p / 32] bit p % 32 = perm[p] < m: the tree positions of the first m
+// input rows (self queries over a prefix of the build input, e.g. a slab's
+// owned particles ahead of its halo)
+__global__ void __launch_bounds__(TB)
+self_bits_kernel(const uint32_t *__restrict__ perm, uint64_t n8, uint32_t m,
+                 uint32_t *__restrict__ bits) {
+    const uint64_t p = (uint64_t)blockIdx.x * TB + threadIdx.x;
+    const bool in = p < n8 && perm[p] < m;
+    const uint64_t bal = __ballot(in);
+    const int lane = threadIdx.x & 63;
+    const uint64_t w = p / 32;
+    if ((lane & 31) == 0 && p < n8) bits[w] = (uint32_t)(lane ? bal >> 32 : bal);
+}
+
 __global__ void __launch_bounds__(TB)
 leaf_key2_kernel(const float *__restrict__ splits, const uint32_t *__restrict__ shape_c,
                  const uint32_t *__restrict__ shape_n, int shape_len, uint32_t n8, uint32_t leaf,
@@ -746,10 +846,14 @@ bits_popc_kernel(const uint32_t *__restrict__ bits, uint64_t nwords, uint32_t *_
     if (w < nwords) pc[w] = (uint32_t)__popc(bits[w]);
 }
 
+// out = ord[j] for every set bit j in order (ord == nullptr: j itself); with
+// tgp, also tgi[ord[j]] = tgp[j] (self queries: a failure's seed, kept per
+// position in the first pass, by query id for the retry rounds)
 __global__ void __launch_bounds__(TB)
 bits_emit_kernel(const uint32_t *__restrict__ bits, const uint32_t *__restrict__ pc_excl,
                  uint64_t nwords, const uint32_t *__restrict__ ord, uint32_t *__restrict__ out,
-                 uint32_t *__restrict__ count) {
+                 uint32_t *__restrict__ count, const float *__restrict__ tgp,
+                 float *__restrict__ tgi) {
     const uint64_t w = (uint64_t)blockIdx.x * TB + threadIdx.x;
     if (w >= nwords) return;
     uint32_t b = bits[w], o = pc_excl[w];
@@ -757,7 +861,10 @@ bits_emit_kernel(const uint32_t *__restrict__ bits, const uint32_t *__restrict__
     while (b) {
         const uint32_t j = (uint32_t)__builtin_ctz(b);
         b &= b - 1u;
-        out[o++] = ord[w * 32 + j];
+        const uint32_t pj = (uint32_t)(w * 32 + j);
+        const uint32_t id = ord ? ord[pj] : pj;
+        out[o++] = id;
+        if (tgp) tgi[id] = tgp[pj];
     }
 }
 
@@ -773,25 +880,19 @@ spill_kernel(const uint32_t *__restrict__ from, const uint32_t *__restrict__ fro
 }
 
 nbkd_status compact_failures(Workspace &ws, const uint32_t *bits, uint32_t mm, const uint32_t *ord,
-                             uint32_t *out, uint32_t *count, hipStream_t s) {
+                             uint32_t *out, uint32_t *count, hipStream_t s,
+                             const float *tgp = nullptr, float *tgi = nullptr,
+                             int pc_slot = WS_KEYS2) {
     const uint64_t nwords = ((uint64_t)mm + 31) / 32;
-    uint32_t *pc = (uint32_t *)ws.get(WS_KEYS2, nwords * 4u + 16u, s);
+    uint32_t *pc = (uint32_t *)ws.get(pc_slot, nwords * 4u + 16u, s);
     if (!pc) return NBKD_ENOMEM;
     const unsigned blocks = (unsigned)((nwords + TB - 1) / TB);
     bits_popc_kernel<<<blocks, TB, 0, s>>>(bits, nwords, pc);
     nbkd_status rc = device_excl_scan(ws, pc, nwords, s);
     if (rc) return rc;
-    bits_emit_kernel<<<blocks, TB, 0, s>>>(bits, pc, nwords, ord, out, count);
+    bits_emit_kernel<<<blocks, TB, 0, s>>>(bits, pc, nwords, ord, out, count, tgp, tgi);
     NBKD_HIP(hipGetLastError());
     return NBKD_OK;
-}
-
-// out[i] = ord[pos[i]]: sorted positions back to query ids// out[i] = ord[pos[i]]: sorted positions back to query ids
-__global__ void __launch_bounds__(TB)
-gather_kernel(const uint32_t *__restrict__ pos, uint32_t n, const uint32_t *__restrict__ ord,
-              uint32_t *__restrict__ out) {
-    const uint32_t i = blockIdx.x * TB + threadIdx.x;
-    if (i < n) out[i] = ord[pos[i]];
 }
 
 int key_bits(const Tree &t) {
@@ -877,6 +978,69 @@ nbkd_status sort_queries(const Tree &t, Workspace &ws, const float *dq, uint32_t
     return radix_sort(ws, keys, order, keys2, tmp, m, key_bits(t), s, &order);
 }
 
+// Self queries: the call's queries are the first m rows of the device array
+// the tree was built from (the same pointer), as in the kNN of every particle
+// that the bench and the density estimates run.  Tree order is then kd order
+// already: the queries need neither the bucketing descent nor the sort, and
+// each seed comes from the query's tree position (self_seed_kernel), indexed
+// by its position in the order (QSpan::tg_pos).  Nothing checks that the
+// array still holds the points the tree was built from, and nothing needs to:
+// the order and the seeds only steer the work (a seed too small or too large
+// is a seed failure and re-walked), every distance is computed from the
+// queries as given.  nbkd_set_tuning("self_order", 0) turns it off.
+bool self_query(const Tree &t, const float *q, uint64_t m, uint32_t flags) {
+    return (flags & NBKD_INPUT_DEVICE) && q != nullptr && q == t.src && m > 0 && m <= t.n &&
+           t.n8 < (1ull << 32) && t.hsplit != nullptr && tuning(TUNE_SELF_ORDER) != 0.0;
+}
+
+// tgp / sp nullptr: the order alone (radius queries)
+nbkd_status self_order(const Tree &t, Workspace &ws, uint32_t m, uint32_t *&order, hipStream_t s,
+                       float *tgp = nullptr, const SeedParams *sp = nullptr) {
+    TimedScope ts("self_order", s);
+    const uint32_t *perm = t.sidx ? t.sidx : t.idx;
+    // the padding rows (FLT_MAX) sort after every real point on every axis,
+    // so they hold the positions n..n8-1 unless a real coordinate is FLT_MAX
+    const bool pads_last = t.n8 == t.n || t.periodic ||
+                           (t.bbox_hi[0] < FLT_MAX && t.bbox_hi[1] < FLT_MAX && t.bbox_hi[2] < FLT_MAX);
+    const uint32_t *pos = nullptr;
+    if (m == t.n && pads_last) {
+        order = const_cast<uint32_t *>(perm); // read only
+    } else {
+        // the tree positions of input rows 0..m-1, in tree order
+        const uint64_t nwords = (t.n8 + 31) / 32;
+        uint32_t *bits = (uint32_t *)ws.get(WS_KEYS2, nwords * 4u + 64u, s);
+        uint32_t *plist = (uint32_t *)ws.get(WS_TMP, (size_t)m * 4 + 16, s);
+        order = (uint32_t *)ws.get(WS_ORDER, (size_t)m * 4, s);
+        if (!bits || !plist || !order) return NBKD_ENOMEM;
+        self_bits_kernel<<<(unsigned)((t.n8 + TB - 1) / TB), TB, 0, s>>>(perm, t.n8, m, bits);
+        NBKD_HIP(hipGetLastError());
+        const nbkd_status rc = compact_failures(ws, bits, (uint32_t)t.n8, nullptr, plist, plist + m,
+                                                s, nullptr, nullptr, WS_RSORT);
+        if (rc) return rc;
+        pos = plist;
+    }
+    if (!pos && !tgp) return NBKD_OK;
+    const uint32_t nchunks = (uint32_t)((t.n8 + 63) / 64);
+    uint2 *anch = nullptr;
+    if (tgp) {
+        anch = (uint2 *)ws.get(WS_ANCH, (size_t)nchunks * 8, s);
+        if (!anch) return NBKD_ENOMEM;
+        const float3 lo = t.periodic ? make_float3(0.0f, 0.0f, 0.0f)
+                                     : make_float3(t.bbox_lo[0], t.bbox_lo[1], t.bbox_lo[2]);
+        const float3 hi = t.periodic ? make_float3(t.box, t.box, t.box)
+                                     : make_float3(t.bbox_hi[0], t.bbox_hi[1], t.bbox_hi[2]);
+        // an anchor below 64 points would break the two-anchors-per-chunk rule
+        const uint32_t stop = std::max<uint32_t>({sp->anchor, (uint32_t)t.leaf, 128u});
+        anchor_chunk_kernel<<<(nchunks + TB - 1) / TB, TB, 0, s>>>(
+            t.hsplit, hblk_offset(t.depth), (uint32_t)t.n8, stop, nchunks, anch, sp->mu_c, lo, hi);
+        NBKD_HIP(hipGetLastError());
+    }
+    const unsigned blocks = (unsigned)std::min<uint64_t>(((uint64_t)m + TB - 1) / TB, 65536);
+    self_seed_kernel<<<blocks, TB, 0, s>>>(anch, nchunks, pos, perm, m, order, tgp);
+    NBKD_HIP(hipGetLastError());
+    return NBKD_OK;
+}
+
 nbkd_status stage_queries(Workspace &ws, const float *q, uint64_t m, uint32_t flags,
                           const float *&dq, hipStream_t s) {
     if (flags & NBKD_INPUT_DEVICE) {
@@ -955,7 +1119,16 @@ nbkd_status knn_locked(const Tree &t, Workspace &ws, const float *q, uint64_t m,
         if (!tg) return NBKD_ENOMEM;
     }
     uint32_t *ord = nullptr;
-    rc = sort_queries(t, ws, dq, mm, ord, s, tg, &sp);
+    // self queries: tree order, seeds per position (tgp) for the first pass
+    const bool self = packet && tg && self_query(t, q, m, flags);
+    float *tgp = nullptr;
+    if (self) {
+        tgp = (float *)ws.get(WS_KEYS, (size_t)mm * 4, s);
+        if (!tgp) return NBKD_ENOMEM;
+        rc = self_order(t, ws, mm, ord, s, tgp, &sp);
+    } else {
+        rc = sort_queries(t, ws, dq, mm, ord, s, tg, &sp);
+    }
     if (rc) return rc;
     float *dd = out_d;
     uint32_t *di = out_i;
@@ -1073,15 +1246,19 @@ nbkd_status knn_locked(const Tree &t, Workspace &ws, const float *q, uint64_t m,
                 TimedScope ts("knn", s);
                 for (uint64_t b0 = 0; b0 < mm; b0 += batch) {
                     const uint32_t nb = (uint32_t)std::min<uint64_t>(batch, mm - b0);
-                    rc = launch_knn_collect(t, dq, ord + b0, static_span(nb), k, tg, 1.0f, 64u, cand,
-                                            capg, ccount, dd, di, nullptr, nullptr, bits,
+                    QSpan sp1 = static_span(nb);
+                    sp1.tg_pos = self; // seeds (and the first pass's rewritten ones) per position
+                    rc = launch_knn_collect(t, dq, ord + b0, sp1, k, self ? tgp + b0 : tg, 1.0f, 64u,
+                                            cand, capg, ccount, dd, di, nullptr, nullptr, bits,
                                             (uint32_t)b0, false, adaptive, sq, kb, stats, s);
                     if (rc) return rc;
                 }
             }
             {
                 TimedScope ts2("knn_retry_order", s);
-                rc = compact_failures(ws, bits, mm, ord, rq, rq_count, s);
+                // self queries: the failures' seeds move to tg by query id
+                rc = compact_failures(ws, bits, mm, ord, rq, rq_count, s, self ? tgp : nullptr,
+                                      self ? tg : nullptr);
                 if (rc) return rc;
             }
             if (stats) NBKD_HIP(hipMemcpyAsync(stats + 9, rq_count, 4, hipMemcpyDeviceToDevice, s));
@@ -1407,7 +1584,8 @@ static nbkd_status ball_common(const Tree &t, Workspace &ws, const float *q, uin
     nbkd_status rc = stage_queries(ws, q, m, flags, dq, s);
     if (rc) return rc;
     uint32_t *ord = nullptr;
-    rc = sort_queries(t, ws, dq, mm, ord, s);
+    rc = self_query(t, q, m, flags) ? self_order(t, ws, mm, ord, s)
+                                    : sort_queries(t, ws, dq, mm, ord, s);
     if (rc) return rc;
     const float r2 = r * r;
     // periodic queries outside [0, L]^3: listed, every point tested for them.

@@ -289,6 +289,11 @@ nbkd_status nbkd_set_ids(nbkd_tree *tree, const uint32_t *ids, uint32_t flags, v
         NBKD_HIP(hipStreamSynchronize(s));
         dids = tmp.as<uint32_t>();
     }
+    // the self-query order (query.hip self_order) keeps the build's permutation
+    if (!t.sidx) {
+        NBKD_HIP(tree_malloc((void **)&t.sidx, t.n8 * 4));
+        NBKD_HIP(hipMemcpyAsync(t.sidx, t.idx, t.n8 * 4, hipMemcpyDeviceToDevice, s));
+    }
     const unsigned blocks = (unsigned)((t.n8 + 255) / 256);
     remap_ids_kernel<<<blocks, 256, 0, s>>>(t.idx, t.p4, t.n8, t.n, dids);
     NBKD_HIP(hipGetLastError());

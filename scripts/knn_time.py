@@ -21,7 +21,7 @@ import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from nbodyhpc_amd import capi, hip, synth  # noqa: E402
 
-PHASES = ("leaf_key", "sort", "knn_collect", "knn_select", "knn_retry", "knn_retry_order",
+PHASES = ("self_order", "leaf_key", "sort", "knn_collect", "knn_select", "knn_retry", "knn_retry_order",
           "knn_fallback", "knn", "ball_count")
 
 
@@ -70,11 +70,16 @@ def main():
     ap.add_argument("--slab-rank", type=int, default=0)
     ap.add_argument("--scaling", choices=("strong", "weak"), default="strong")
     ap.add_argument("--seed", type=int, default=20261015)
+    ap.add_argument("--tune", action="append", default=[], metavar="NAME=VALUE",
+                    help="nbkd_set_tuning before the runs (e.g. self_order=0)")
     ap.add_argument("--stats", action="store_true",
                     help="one more (untimed) pass with the work counters and phase clocks on")
     a = ap.parse_args()
     hip.preload()
     hip.set_device(0)
+    for kv in a.tune:
+        name, val = kv.split("=")
+        capi.set_tuning(name, float(val))
     n, k = int(a.n), a.k
     ids = None
     if a.slab_world > 1:
@@ -132,7 +137,8 @@ def main():
                       "slab_rank": a.slab_rank, "scaling": a.scaling, "n_arg": int(a.n),
                       "seed": a.seed, "k": k, "leaf": a.leaf, "lognormal": a.lognormal,
                       "kth": a.kth, "ball": a.ball, "wall_ms": round(wall, 3), "qps": n / wall * 1e3,
-                      "phases_ms": ph, "sha": h.hexdigest()[:16], "stats": st}), flush=True)
+                      "phases_ms": ph, "sha": h.hexdigest()[:16], "tune": a.tune, "stats": st}),
+          flush=True)
 
 
 if __name__ == "__main__":
