@@ -406,7 +406,7 @@ def suite(args, capi, hip, tree, dev_pts, n, k, L, stream, od, oi):
         sec = timed(lambda: t128.query_device(dev_pts.ptr, n, k, od.ptr, oi.ptr, stream.handle),
                     steps, hip)
         br = {nm: capi.timing_read(nm)[0] / steps for nm in
-              ("leaf_key", "sort", "knn_collect", "knn_select", "knn_retry")}
+              ("self_order", "leaf_key", "sort", "knn_collect", "knn_select", "knn_retry")}
         capi.timing_enable(False)
         out["knn_leafsize128"] = {"queries_per_s": n / sec, "ms": sec * 1e3, "k": k,
                                   "queries": n, "breakdown_ms": br}
@@ -427,7 +427,8 @@ def suite(args, capi, hip, tree, dev_pts, n, k, L, stream, od, oi):
     sec = timed(lambda: tree.query_device(dev_pts.ptr, n, k2, od2.ptr, oi2.ptr, stream.handle),
                 steps, hip)
     br = {nm: capi.timing_read(nm)[0] / steps for nm in
-          ("leaf_key", "sort", "knn_collect", "knn_select", "knn_retry", "knn_fallback")}
+          ("self_order", "leaf_key", "sort", "knn_collect", "knn_select", "knn_retry",
+           "knn_fallback")}
     capi.timing_enable(False)
     out["knn_k100"] = {"queries_per_s": n / sec, "ms": sec * 1e3, "k": k2, "queries": n,
                        "breakdown_ms": br}
@@ -534,7 +535,7 @@ def suite(args, capi, hip, tree, dev_pts, n, k, L, stream, od, oi):
     capi.timing_enable(True)
     sec = timed(lambda: lt.query_device(dl.ptr, n, k, od.ptr, oi.ptr, stream.handle), steps, hip)
     br = {nm: capi.timing_read(nm)[0] / steps for nm in
-          ("leaf_key", "sort", "knn_collect", "knn_select", "knn_retry_order",
+          ("self_order", "leaf_key", "sort", "knn_collect", "knn_select", "knn_retry_order",
            "knn_retry", "knn_fallback")}
     capi.timing_enable(False)
     capi.stats_enable(True)
@@ -1022,6 +1023,7 @@ def main():
     knn_ms, knn_launches = capi.timing_read("knn")
     sort_ms, _ = capi.timing_read("sort")
     key_ms, _ = capi.timing_read("leaf_key")
+    self_ms, _ = capi.timing_read("self_order")
     oob_ms, _ = capi.timing_read("knn_outside_box")
     fb_ms, _ = capi.timing_read("knn_fallback")
     rt_ms, _ = capi.timing_read("knn_retry")
@@ -1163,8 +1165,8 @@ def main():
             step_achieved=step_ach,
             step_frac=None if step_ach is None else step_ach / peak),
         "breakdown_ms_per_step": {
-            "leaf_key": key_ms / args.steps, "sort": sort_ms / args.steps,
-            "knn": knn_ms / args.steps, "knn_collect": col_ms / args.steps,
+            "self_order": self_ms / args.steps, "leaf_key": key_ms / args.steps,
+            "sort": sort_ms / args.steps, "knn": knn_ms / args.steps, "knn_collect": col_ms / args.steps,
             "knn_select": sel_ms / args.steps, "outside_box_check": oob_ms / args.steps,
             "retry": (rt_ms + rto_ms) / args.steps, "fallback": fb_ms / args.steps,
         },

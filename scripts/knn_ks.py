@@ -12,7 +12,7 @@ import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from nbodyhpc_amd import capi, hip, synth  # noqa: E402
 
-PARTS = ("leaf_key", "sort", "knn_collect", "knn_select", "knn_retry", "knn_fallback",
+PARTS = ("self_order", "leaf_key", "sort", "knn_collect", "knn_select", "knn_retry", "knn_fallback",
          "knn_exact")
 
 
