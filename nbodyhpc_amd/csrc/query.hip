@@ -221,6 +221,9 @@ __device__ __forceinline__ void seed_turn(SeedPath &w, bool right, int o) {
 }
 
 // anch[c] = (first position, seed bits) of the anchor holding position 64c
+// (tried and dropped: the anchor's tight span from its 8-point group boxes
+// where the cell reaches through empty space -- the same seed failures on
+// slab trees and log-normal data, +0.13 ms per 1e8; profiles/r05s_ab.txt)
 __global__ void __launch_bounds__(TB)
 anchor_chunk_kernel(const float *__restrict__ hf, int o, uint32_t n8, uint32_t stop,
                     uint32_t nchunks, uint2 *__restrict__ anch, float mu_c, float3 box_lo,
@@ -868,6 +871,19 @@ bits_emit_kernel(const uint32_t *__restrict__ bits, const uint32_t *__restrict__
     }
 }
 
+// the set bits' indices in order, one thread per bit (consecutive threads
+// write consecutive entries): a dense bitmap, as the self order's
+// prefix selection (most bits set), where bits_emit_kernel's per-word loop
+// would write 32 scattered runs per wave
+__global__ void __launch_bounds__(TB)
+bits_emit_dense_kernel(const uint32_t *__restrict__ bits, const uint32_t *__restrict__ pc_excl,
+                       uint64_t nbits, uint32_t *__restrict__ out) {
+    const uint64_t j = (uint64_t)blockIdx.x * TB + threadIdx.x;
+    if (j >= nbits) return;
+    const uint32_t w = bits[j >> 5], b = (uint32_t)j & 31u;
+    if ((w >> b) & 1u) out[pc_excl[j >> 5] + (uint32_t)__popc(w & ((1u << b) - 1u))] = (uint32_t)j;
+}
+
 // the entries of a device-counted list past what the rounds handled: appended
 // to the next list (order irrelevant there: one query per wave, or the exact
 // kernel)
@@ -881,10 +897,9 @@ spill_kernel(const uint32_t *__restrict__ from, const uint32_t *__restrict__ fro
 
 nbkd_status compact_failures(Workspace &ws, const uint32_t *bits, uint32_t mm, const uint32_t *ord,
                              uint32_t *out, uint32_t *count, hipStream_t s,
-                             const float *tgp = nullptr, float *tgi = nullptr,
-                             int pc_slot = WS_KEYS2) {
+                             const float *tgp = nullptr, float *tgi = nullptr) {
     const uint64_t nwords = ((uint64_t)mm + 31) / 32;
-    uint32_t *pc = (uint32_t *)ws.get(pc_slot, nwords * 4u + 16u, s);
+    uint32_t *pc = (uint32_t *)ws.get(WS_KEYS2, nwords * 4u + 16u, s);
     if (!pc) return NBKD_ENOMEM;
     const unsigned blocks = (unsigned)((nwords + TB - 1) / TB);
     bits_popc_kernel<<<blocks, TB, 0, s>>>(bits, nwords, pc);
@@ -1012,11 +1027,15 @@ nbkd_status self_order(const Tree &t, Workspace &ws, uint32_t m, uint32_t *&orde
         uint32_t *plist = (uint32_t *)ws.get(WS_TMP, (size_t)m * 4 + 16, s);
         order = (uint32_t *)ws.get(WS_ORDER, (size_t)m * 4, s);
         if (!bits || !plist || !order) return NBKD_ENOMEM;
-        self_bits_kernel<<<(unsigned)((t.n8 + TB - 1) / TB), TB, 0, s>>>(perm, t.n8, m, bits);
-        NBKD_HIP(hipGetLastError());
-        const nbkd_status rc = compact_failures(ws, bits, (uint32_t)t.n8, nullptr, plist, plist + m,
-                                                s, nullptr, nullptr, WS_RSORT);
+        uint32_t *pc = (uint32_t *)ws.get(WS_RSORT, nwords * 4u + 16u, s);
+        if (!pc) return NBKD_ENOMEM;
+        const unsigned pblocks = (unsigned)((t.n8 + TB - 1) / TB);
+        self_bits_kernel<<<pblocks, TB, 0, s>>>(perm, t.n8, m, bits);
+        bits_popc_kernel<<<(unsigned)((nwords + TB - 1) / TB), TB, 0, s>>>(bits, nwords, pc);
+        const nbkd_status rc = device_excl_scan(ws, pc, nwords, s);
         if (rc) return rc;
+        bits_emit_dense_kernel<<<pblocks, TB, 0, s>>>(bits, pc, t.n8, plist);
+        NBKD_HIP(hipGetLastError());
         pos = plist;
     }
     if (!pos && !tgp) return NBKD_OK;
