@@ -597,8 +597,10 @@ def run_c5(args, rank, world, local_rank, dist, same_dev, barrier, allmax, allsu
         f"generated in {gen_s:.1f} s")
 
     def build_tree():
+        # slab trees split by their points' extent (nbkd_build_ext)
         t = capi.Tree(n=n_local, dev_ptr=dev_pts.ptr, leafsize=args.leafsize, boxsize=L,
-                      device=local_rank, stream=stream.handle)
+                      device=local_rank, stream=stream.handle,
+                      extent=None if ds is None else ds.extent())
         if ds is not None:
             t.set_ids(dev_ptr=ds.ids.ptr, stream=stream.handle)
         return t
@@ -912,8 +914,10 @@ def main():
         f"{time.perf_counter() - t_gen:.1f} s")
 
     def build_tree():
+        # slab trees split by their points' extent (nbkd_build_ext)
         t = capi.Tree(n=n_local, dev_ptr=dev_pts.ptr, leafsize=args.leafsize, boxsize=L,
-                      device=local_rank, stream=stream.handle)
+                      device=local_rank, stream=stream.handle,
+                      extent=None if ds is None else ds.extent())
         if ds is not None:
             t.set_ids(dev_ptr=ds.ids.ptr, stream=stream.handle)
         return t

@@ -38,6 +38,8 @@ _u32 = ctypes.c_uint32
 _PROTOS = {
     "nbkd_build": (_i32, [_c_p, _u64, _i32, _i32, ctypes.c_float, _i32, _u32, _c_p,
                           ctypes.POINTER(_c_p)]),
+    "nbkd_build_ext": (_i32, [_c_p, _u64, _i32, _i32, ctypes.c_float, _c_p, _i32, _u32, _c_p,
+                              ctypes.POINTER(_c_p)]),
     "nbkd_query_knn": (_i32, [_c_p, _c_p, _u64, _i32, _c_p, _c_p, _u32, _c_p]),
     "nbkd_query_kth": (_i32, [_c_p, _c_p, _u64, _i32, _c_p, _u32, _c_p]),
     "nbkd_query_ball_count": (_i32, [_c_p, _c_p, _u64, ctypes.c_float, _c_p, _u32, _c_p]),
@@ -126,7 +128,7 @@ class Tree:
     device pointers (int) with `device_ptrs=True`."""
 
     def __init__(self, points=None, leafsize=128, boxsize=None, device=-1, *, n=None,
-                 dev_ptr=None, stream=None):
+                 dev_ptr=None, stream=None, extent=None):
         L = lib()
         h = _c_p()
         flags = 0
@@ -139,9 +141,13 @@ class Tree:
             ptr, count = pts.ctypes.data, pts.shape[0]
             self._keep = pts
         periodic = boxsize is not None
-        st = L.nbkd_build(ptr, count, int(leafsize), 1 if periodic else 0,
-                          float(boxsize) if periodic else 0.0, int(device), flags, stream,
-                          ctypes.byref(h))
+        # extent (ex, ey, ez): nbkd_build_ext, split axes by the points' extent
+        # (slab trees); None: the reference's depth % 3
+        ext = None if extent is None else (ctypes.c_float * 3)(*[float(e) for e in extent])
+        ext = None if ext is None else ctypes.cast(ext, ctypes.c_void_p)
+        st = L.nbkd_build_ext(ptr, count, int(leafsize), 1 if periodic else 0,
+                              float(boxsize) if periodic else 0.0, ext, int(device), flags,
+                              stream, ctypes.byref(h))
         _check(st)
         self.h = h
         self._keep = None

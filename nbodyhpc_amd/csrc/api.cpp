@@ -46,6 +46,23 @@ struct DeviceGuard {
     }
 };
 
+} // namespace
+
+uint64_t axes_for_extent(const float e[3]) {
+    double x[3] = {e[0], e[1], e[2]};
+    uint64_t a = 0;
+    for (int d = 0; d < 32; ++d) {
+        int k = 0;
+        if (x[1] > x[k]) k = 1;
+        if (x[2] > x[k]) k = 2;
+        a |= (uint64_t)k << (2 * d);
+        x[k] *= 0.5;
+    }
+    return a;
+}
+
+namespace {
+
 void free_tree(Tree &t) {
     // no kernel of this tree may still run when its blocks are reused
     if (t.x || t.nodes) (void)hipDeviceSynchronize();
@@ -446,10 +463,23 @@ nbkd_status nbkd_device_count(int32_t *count) {
 nbkd_status nbkd_build(const float *xyz, uint64_t n, int32_t leaf_size, int32_t periodic,
                        float box_size, int32_t device, uint32_t flags, void *stream,
                        nbkd_tree **out) {
+    return nbkd_build_ext(xyz, n, leaf_size, periodic, box_size, nullptr, device, flags, stream,
+                          out);
+}
+
+nbkd_status nbkd_build_ext(const float *xyz, uint64_t n, int32_t leaf_size, int32_t periodic,
+                           float box_size, const float *extent, int32_t device, uint32_t flags,
+                           void *stream, nbkd_tree **out) {
     NBKD_GUARD_BEGIN
     g_err.clear();
     if (!out || (n > 0 && !xyz)) {
         set_error("nbkd_build: NULL argument");
+        return NBKD_EINVAL;
+    }
+    if (extent && !(extent[0] > 0.0f && extent[1] > 0.0f && extent[2] > 0.0f &&
+                    std::isfinite(extent[0]) && std::isfinite(extent[1]) &&
+                    std::isfinite(extent[2]))) {
+        set_error("nbkd_build_ext: extents must be positive and finite");
         return NBKD_EINVAL;
     }
     *out = nullptr;
@@ -474,6 +504,7 @@ nbkd_status nbkd_build(const float *xyz, uint64_t n, int32_t leaf_size, int32_t 
     h->t.device = dev;
     h->t.periodic = periodic ? 1 : 0;
     h->t.box = periodic ? box_size : 0.0f;
+    h->t.axes = extent ? axes_for_extent(extent) : AXES_REF;
     nbkd_status st = build_tree(h->t, xyz, n, leaf_size, (flags & NBKD_INPUT_DEVICE) != 0,
                                 (hipStream_t)stream);
     if (st != NBKD_OK) {

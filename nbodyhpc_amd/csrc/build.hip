@@ -5,6 +5,8 @@
 //   * leaf iff count <= max(leaf_size, 16)                       (:485, :495)
 //   * m = (count / 2) / 8 * 8; split = m-th order statistic of the
 //     segment's coordinate on axis depth % 3                      (:502-510)
+//     (Tree::axes; a tree built with nbkd_build_ext splits the axis of
+//     largest remaining extent instead: slab trees, not the reference's)
 //   * preorder ids, left child = id + 1, right = id + 1 + |left subtree|
 // The tree SHAPE is a pure function of (n8, leaf); only the split VALUES and
 // the point permutation depend on the data.  The shape (ids, segment ranges)
@@ -49,10 +51,10 @@ struct SelState {
     uint32_t prefix, rank, below, eq;
 };
 struct SSeg {
-    uint32_t node, left, count, flags; // flags: dim (bits 0-1), source buffer (bit 2)
+    uint32_t node, left, count, depth; // source buffer: B at odd depths
 };
 struct SubSeg {
-    uint32_t node, off, count, dim;
+    uint32_t node, off, count, depth; // split axis axis_at(axes, depth)
 };
 
 struct Soa {
@@ -425,10 +427,12 @@ struct SmallLds {
 template <int TS>
 __device__ void team_level(SmallLds &L, const SSeg &sg, uint32_t leaf, Soa out,
                            nbkd_node *__restrict__ nodes, const uint32_t *__restrict__ tab_c,
-                           const uint32_t *__restrict__ tab_n, int tab_len, int cur, int lc) {
+                           const uint32_t *__restrict__ tab_n, int tab_len, int cur, int lc,
+                           uint64_t axes) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint32_t s = (uint32_t)wave / TS, wt = (uint32_t)wave % TS;
     const SubSeg ss = L.list[lc][s];
+    const uint32_t sdim = (uint32_t)axis_at(axes, (int)ss.depth);
     const bool work = ss.count > leaf;
     const uint32_t tl = wt * 64 + lane; // thread within the team
     if (!work) {
@@ -442,7 +446,7 @@ __device__ void team_level(SmallLds &L, const SSeg &sg, uint32_t leaf, Soa out,
             out.i[g] = L.i[cur][ss.off + e];
         }
     }
-    const float *kx = ss.dim == 0 ? L.x[cur] : (ss.dim == 1 ? L.y[cur] : L.z[cur]);
+    const float *kx = sdim == 0 ? L.x[cur] : (sdim == 1 ? L.y[cur] : L.z[cur]);
     const uint32_t m = (ss.count / 2) / 8 * 8;
     uint32_t rank = m, prefix = 0, below = 0, eqc = 0;
     uint32_t *h = L.hist[s * TS];
@@ -566,7 +570,7 @@ __device__ void team_level(SmallLds &L, const SSeg &sg, uint32_t leaf, Soa out,
                 py = L.y[cur][ss.off + e];
                 pz = L.z[cur][ss.off + e];
                 pi = L.i[cur][ss.off + e];
-                const uint32_t k = fkey(pick(ss.dim, px, py, pz));
+                const uint32_t k = fkey(pick(sdim, px, py, pz));
                 c = k < piv ? 0u : (k == piv ? 1u : 2u);
             }
             const uint64_t b0 = __ballot(c == 0), b1 = __ballot(c == 1), b2 = __ballot(c == 2);
@@ -591,11 +595,10 @@ __device__ void team_level(SmallLds &L, const SSeg &sg, uint32_t leaf, Soa out,
         }
         if (tl == 0) {
             const uint32_t rid = ss.node + 1 + subtree_nodes(m, leaf, tab_c, tab_n, tab_len);
-            nodes[ss.node] = nbkd_node{(int32_t)ss.dim, fkey_inv(piv), ss.node + 1, rid};
+            nodes[ss.node] = nbkd_node{(int32_t)sdim, fkey_inv(piv), ss.node + 1, rid};
             const uint32_t slot = atomicAdd(&L.nlist[lc ^ 1], 2u);
-            const uint32_t nd = (ss.dim + 1) % 3;
-            L.list[lc ^ 1][slot] = SubSeg{ss.node + 1, ss.off, m, nd};
-            L.list[lc ^ 1][slot + 1] = SubSeg{rid, ss.off + m, ss.count - m, nd};
+            L.list[lc ^ 1][slot] = SubSeg{ss.node + 1, ss.off, m, ss.depth + 1};
+            L.list[lc ^ 1][slot + 1] = SubSeg{rid, ss.off + m, ss.count - m, ss.depth + 1};
         }
     }
 }
@@ -603,12 +606,12 @@ __device__ void team_level(SmallLds &L, const SSeg &sg, uint32_t leaf, Soa out,
 __global__ void __launch_bounds__(TB)
 small_kernel(const SSeg *__restrict__ list, uint32_t leaf, Soa bufA, Soa bufB,
              nbkd_node *__restrict__ nodes, const uint32_t *__restrict__ tab_c,
-             const uint32_t *__restrict__ tab_n, int tab_len, int team) {
+             const uint32_t *__restrict__ tab_n, int tab_len, int team, uint64_t axes) {
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
     SmallLds &L = *reinterpret_cast<SmallLds *>(smem_raw);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const SSeg sg = list[blockIdx.x];
-    const Soa src = (sg.flags & 4u) ? bufB : bufA;
+    const Soa src = (sg.depth & 1u) ? bufB : bufA;
     const Soa out = bufA;
 
     if (sg.count > SMALL) { // a leaf larger than SMALL (leaf_size > SMALL): move it to A
@@ -629,7 +632,7 @@ small_kernel(const SSeg *__restrict__ list, uint32_t leaf, Soa bufA, Soa bufB,
         L.i[0][e] = src.i[sg.left + e];
     }
     if (threadIdx.x == 0) {
-        L.list[0][0] = SubSeg{sg.node, 0u, sg.count, sg.flags & 3u};
+        L.list[0][0] = SubSeg{sg.node, 0u, sg.count, sg.depth};
         L.nlist[0] = 1;
         L.nlist[1] = 0;
     }
@@ -639,12 +642,13 @@ small_kernel(const SSeg *__restrict__ list, uint32_t leaf, Soa bufA, Soa bufB,
         const uint32_t nsub = L.nlist[lc];
         if (nsub <= 2 && team) {
             if (nsub == 1)
-                team_level<4>(L, sg, leaf, out, nodes, tab_c, tab_n, tab_len, cur, lc);
+                team_level<4>(L, sg, leaf, out, nodes, tab_c, tab_n, tab_len, cur, lc, axes);
             else
-                team_level<2>(L, sg, leaf, out, nodes, tab_c, tab_n, tab_len, cur, lc);
+                team_level<2>(L, sg, leaf, out, nodes, tab_c, tab_n, tab_len, cur, lc, axes);
         } else
         for (uint32_t s = wave; s < nsub; s += TB / 64) {
             const SubSeg ss = L.list[lc][s];
+            const uint32_t sdim = (uint32_t)axis_at(axes, (int)ss.depth);
             if (ss.count <= leaf) {
                 if (lane == 0)
                     nodes[ss.node] =
@@ -658,7 +662,7 @@ small_kernel(const SSeg *__restrict__ list, uint32_t leaf, Soa bufA, Soa bufB,
                 }
                 continue;
             }
-            const float *kx = ss.dim == 0 ? L.x[cur] : (ss.dim == 1 ? L.y[cur] : L.z[cur]);
+            const float *kx = sdim == 0 ? L.x[cur] : (sdim == 1 ? L.y[cur] : L.z[cur]);
             const uint32_t m = (ss.count / 2) / 8 * 8;
             // wave radix select of rank m, 4 x 8-bit digits
             uint32_t rank = m, prefix = 0, below = 0, eqc = 0;
@@ -754,7 +758,7 @@ small_kernel(const SSeg *__restrict__ list, uint32_t leaf, Soa bufA, Soa bufB,
                     py = L.y[cur][ss.off + e];
                     pz = L.z[cur][ss.off + e];
                     pi = L.i[cur][ss.off + e];
-                    uint32_t k = fkey(pick(ss.dim, px, py, pz));
+                    uint32_t k = fkey(pick(sdim, px, py, pz));
                     c = k < piv ? 0u : (k == piv ? 1u : 2u);
                 }
                 uint64_t b0 = __ballot(c == 0), b1 = __ballot(c == 1), b2 = __ballot(c == 2);
@@ -779,11 +783,10 @@ small_kernel(const SSeg *__restrict__ list, uint32_t leaf, Soa bufA, Soa bufB,
             }
             const uint32_t rid = ss.node + 1 + subtree_nodes(m, leaf, tab_c, tab_n, tab_len);
             if (lane == 0) {
-                nodes[ss.node] = nbkd_node{(int32_t)ss.dim, fkey_inv(piv), ss.node + 1, rid};
+                nodes[ss.node] = nbkd_node{(int32_t)sdim, fkey_inv(piv), ss.node + 1, rid};
                 uint32_t slot = atomicAdd(&L.nlist[lc ^ 1], 2u);
-                uint32_t nd = (ss.dim + 1) % 3;
-                L.list[lc ^ 1][slot] = SubSeg{ss.node + 1, ss.off, m, nd};
-                L.list[lc ^ 1][slot + 1] = SubSeg{rid, ss.off + m, ss.count - m, nd};
+                L.list[lc ^ 1][slot] = SubSeg{ss.node + 1, ss.off, m, ss.depth + 1};
+                L.list[lc ^ 1][slot + 1] = SubSeg{rid, ss.off + m, ss.count - m, ss.depth + 1};
             }
         }
         __syncthreads();
@@ -1220,9 +1223,8 @@ struct Skeleton {
         return d;
     }
     void rec(uint32_t node, uint32_t left, uint32_t count, int depth) {
-        const uint32_t dim = depth % 3;
         if (count <= SMALL || count <= leaf) {
-            small.push_back(SSeg{node, left, count, dim | ((uint32_t)(depth & 1) << 2)});
+            small.push_back(SSeg{node, left, count, (uint32_t)depth});
             return;
         }
         uint32_t m = (count / 2) / 8 * 8;
@@ -1485,7 +1487,7 @@ nbkd_status build_tree(Tree &t, const float *xyz, uint64_t n, int32_t leaf_size,
         for (size_t d = 0; d < info.size(); ++d) {
             const LevelInfo &li = info[d];
             if (li.nseg == 0) continue;
-            const int dim = (int)(d % 3);
+            const int dim = axis_at(t.axes, (int)d);
             const Soa src = (d & 1) ? B : A;
             const Soa dst = (d & 1) ? A : B;
             const float *key = dim == 0 ? src.x : (dim == 1 ? src.y : src.z);
@@ -1526,7 +1528,7 @@ nbkd_status build_tree(Tree &t, const float *xyz, uint64_t n, int32_t leaf_size,
                                          (int)sizeof(SmallLds)));
             small_kernel<<<(unsigned)small.size(), TB, sizeof(SmallLds), s>>>(
                 d_small, leaf, A, B, t.nodes, d_tabc,
-                d_tabn, (int)tab_c.size(), small_team);
+                d_tabn, (int)tab_c.size(), small_team, t.axes);
             NBKD_HIP(hipGetLastError());
         }
     }

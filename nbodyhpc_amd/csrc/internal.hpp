@@ -98,6 +98,22 @@ constexpr int NBKD_GBLOCK = 128; // points ordered together into groups (<= 64 l
 // Device-resident tree.  Points are SoA in tree order (the reference layout,
 // kdtree/src/cpp/include/kdtree/position_array.hpp:166-271): x, y, z, original
 // index; leaves are contiguous ranges.  Nodes are the reference's 16-B records.
+// Split axis per depth, 2 bits each for depths 0..31 (deeper: depth % 3).
+// The reference splits on depth % 3 (kdtree_impl.hpp:98-146); a tree built
+// with nbkd_build_ext follows its points' extent instead (axes_for_extent).
+constexpr uint64_t axes_ref() {
+    uint64_t a = 0;
+    for (int d = 0; d < 32; ++d) a |= (uint64_t)(d % 3) << (2 * d);
+    return a;
+}
+constexpr uint64_t AXES_REF = axes_ref();
+__host__ __device__ inline int axis_at(uint64_t axes, int depth) {
+    return depth < 32 ? (int)((axes >> (2 * depth)) & 3u) : depth % 3;
+}
+// each depth splits the axis with the largest remaining extent (halved per
+// split; ties to the lower axis): e = (1, 1, 1) gives depth % 3
+uint64_t axes_for_extent(const float e[3]);
+
 struct Tree {
     int device = 0;
     uint64_t n = 0;  // caller's point count
@@ -107,6 +123,7 @@ struct Tree {
     float box = 0.0f;
     int leaf = 16; // effective leaf size max(leaf_size, 16)
     int depth = 0; // max node depth (root = 0)
+    uint64_t axes = AXES_REF; // split axis per depth (axis_at)
     float *x = nullptr, *y = nullptr, *z = nullptr;
     uint32_t *idx = nullptr;
     // the same points packed (x, y, z, idx bits) per tree position: the packet

@@ -105,11 +105,11 @@ __global__ void __launch_bounds__(TB)
 leaf_key3_kernel(const float4 *__restrict__ hb, int o, uint32_t n8, uint32_t leaf,
                  const float *__restrict__ q, uint32_t m, uint32_t *__restrict__ keys,
                  uint32_t *__restrict__ vals, float *__restrict__ tg, float mu_c, uint32_t anchor,
-                 float3 box_lo, float3 box_hi) {
+                 float3 box_lo, float3 box_hi, uint64_t axes) {
     for (uint32_t i = blockIdx.x * TB + threadIdx.x; i < m; i += gridDim.x * TB) {
         const float p[3] = {q[3 * (size_t)i], q[3 * (size_t)i + 1], q[3 * (size_t)i + 2]};
         uint32_t left = 0, count = n8;
-        int dim = 0;
+        int depth = 0;
         float lo[3] = {box_lo.x, box_lo.y, box_lo.z}, hi[3] = {box_hi.x, box_hi.y, box_hi.z};
         float r2 = FLT_MAX;
         bool have_r2 = tg == nullptr;
@@ -141,6 +141,7 @@ leaf_key3_kernel(const float4 *__restrict__ hb, int o, uint32_t n8, uint32_t lea
                                   : ((pos & 2) ? ((pos & 1) ? a2.z : a2.y)
                                                : ((pos & 1) ? a2.x : a1.w));
                 const uint32_t mm = (count / 2) / 8 * 8;
+                const int dim = axis_at(axes, depth++);
                 const bool right = p[dim] > s; // near child, kdtree_impl.hpp:239
                 if (right) {
                     lo[dim] = s;
@@ -151,7 +152,6 @@ leaf_key3_kernel(const float4 *__restrict__ hb, int o, uint32_t n8, uint32_t lea
                     count = mm;
                 }
                 pos = 2 * pos + (right ? 1u : 0u);
-                dim = dim == 2 ? 0 : dim + 1;
             }
             if (count <= leaf) break;
             // pos = child index 0..15 of the next line
@@ -187,29 +187,29 @@ leaf_key3_kernel(const float4 *__restrict__ hb, int o, uint32_t n8, uint32_t lea
 // and the six split values load together at the end.
 struct SeedPath {
     uint32_t left, count, b, base, nb, lp;
-    int l, dim;
+    int l, depth;
     // heap index + 1 of the last split bounding axis d from below / above
     // (0: none, the box face); named, not an indexed private array
     uint32_t lo0, lo1, lo2, hi0, hi1, hi2;
 };
 
-__device__ __forceinline__ void seed_turn(SeedPath &w, bool right, int o) {
+__device__ __forceinline__ void seed_turn(SeedPath &w, bool right, int o, uint64_t axes) {
     const uint32_t mm = (w.count / 2) / 8 * 8;
     const uint32_t at = 16u * w.b + (1u << w.l) + w.lp; // heap index + 1
+    const int dim = axis_at(axes, w.depth++);
     if (right) {
-        w.lo0 = w.dim == 0 ? at : w.lo0;
-        w.lo1 = w.dim == 1 ? at : w.lo1;
-        w.lo2 = w.dim == 2 ? at : w.lo2;
+        w.lo0 = dim == 0 ? at : w.lo0;
+        w.lo1 = dim == 1 ? at : w.lo1;
+        w.lo2 = dim == 2 ? at : w.lo2;
         w.left += mm;
         w.count -= mm;
     } else {
-        w.hi0 = w.dim == 0 ? at : w.hi0;
-        w.hi1 = w.dim == 1 ? at : w.hi1;
-        w.hi2 = w.dim == 2 ? at : w.hi2;
+        w.hi0 = dim == 0 ? at : w.hi0;
+        w.hi1 = dim == 1 ? at : w.hi1;
+        w.hi2 = dim == 2 ? at : w.hi2;
         w.count = mm;
     }
     w.lp = 2 * w.lp + (right ? 1u : 0u);
-    w.dim = w.dim == 2 ? 0 : w.dim + 1;
     if (++w.l == 4) { // next line: child lp of this one
         const uint32_t nbase = w.base + w.nb;
         w.b = nbase + (w.b - w.base) * 16u + w.lp;
@@ -227,12 +227,12 @@ __device__ __forceinline__ void seed_turn(SeedPath &w, bool right, int o) {
 __global__ void __launch_bounds__(TB)
 anchor_chunk_kernel(const float *__restrict__ hf, int o, uint32_t n8, uint32_t stop,
                     uint32_t nchunks, uint2 *__restrict__ anch, float mu_c, float3 box_lo,
-                    float3 box_hi) {
+                    float3 box_hi, uint64_t axes) {
     const uint32_t c = blockIdx.x * TB + threadIdx.x;
     if (c >= nchunks) return;
     const uint32_t p = c * 64u;
     SeedPath w{0u, n8, 0u, 0u, 1u, 0u, o, 0, 0u, 0u, 0u, 0u, 0u, 0u};
-    while (w.count > stop) seed_turn(w, p >= w.left + (w.count / 2) / 8 * 8, o);
+    while (w.count > stop) seed_turn(w, p >= w.left + (w.count / 2) / 8 * 8, o, axes);
     const float lo[3] = {w.lo0 ? hf[w.lo0 - 1] : box_lo.x, w.lo1 ? hf[w.lo1 - 1] : box_lo.y,
                          w.lo2 ? hf[w.lo2 - 1] : box_lo.z};
     const float hi[3] = {w.hi0 ? hf[w.hi0 - 1] : box_hi.x, w.hi1 ? hf[w.hi1 - 1] : box_hi.y,
@@ -276,7 +276,7 @@ leaf_key2_kernel(const float *__restrict__ splits, const uint32_t *__restrict__ 
                  const uint32_t *__restrict__ shape_n, int shape_len, uint32_t n8, uint32_t leaf,
                  const float *__restrict__ q, uint32_t m, uint32_t *__restrict__ keys,
                  uint32_t *__restrict__ vals, float *__restrict__ tg, float mu_c, uint32_t anchor,
-                 float3 box_lo, float3 box_hi) {
+                 float3 box_lo, float3 box_hi, uint64_t axes) {
     __shared__ uint32_t sc[SHAPE_MAX], sn[SHAPE_MAX];
     for (int i = threadIdx.x; i < shape_len; i += TB) {
         sc[i] = shape_c[i];
@@ -286,7 +286,7 @@ leaf_key2_kernel(const float *__restrict__ splits, const uint32_t *__restrict__ 
     for (uint32_t i = blockIdx.x * TB + threadIdx.x; i < m; i += gridDim.x * TB) {
         const float p[3] = {q[3 * (size_t)i], q[3 * (size_t)i + 1], q[3 * (size_t)i + 2]};
         uint32_t node = 0, left = 0, count = n8;
-        int dim = 0;
+        int depth = 0;
         float lo[3] = {box_lo.x, box_lo.y, box_lo.z}, hi[3] = {box_hi.x, box_hi.y, box_hi.z};
         float r2 = FLT_MAX;
         bool have_r2 = tg == nullptr;
@@ -297,6 +297,7 @@ leaf_key2_kernel(const float *__restrict__ splits, const uint32_t *__restrict__ 
             }
             const uint32_t mm = (count / 2) / 8 * 8;
             const float s = splits[node];
+            const int dim = axis_at(axes, depth++);
             if (p[dim] > s) { // near child, kdtree_impl.hpp:239
                 lo[dim] = s;
                 uint32_t sub = 1;
@@ -319,7 +320,6 @@ leaf_key2_kernel(const float *__restrict__ splits, const uint32_t *__restrict__ 
                 node += 1;
                 count = mm;
             }
-            dim = dim == 2 ? 0 : dim + 1;
         }
         if (!have_r2) r2 = guess_r2(count, lo, hi, mu_c);
         keys[i] = left >> 3;
@@ -952,6 +952,17 @@ SeedParams seed_params(const Tree &t, int k) {
     return p;
 }
 
+// The box the seeds' density estimates cut with the splits: the real points'
+// bounding box, periodic trees too (the density estimate only; the traversal
+// starts from the box or unbounded).  A slab tree's points fill a strip of
+// the periodic box; cells at the strip's faces reaching through the empty
+// rest diluted their density, and their seeds overflowed the columns: with
+// the extent-scheduled slab axes (nbkd_build_ext), 558 k of 12.5 M queries
+// of an N = 8 slab were re-walked instead of 7 k (profiles/r05t_slab_ab.txt).
+// For a filled box it is the box up to its outermost points.
+float3 seed_lo(const Tree &t) { return make_float3(t.bbox_lo[0], t.bbox_lo[1], t.bbox_lo[2]); }
+float3 seed_hi(const Tree &t) { return make_float3(t.bbox_hi[0], t.bbox_hi[1], t.bbox_hi[2]); }
+
 nbkd_status sort_queries(const Tree &t, Workspace &ws, const float *dq, uint32_t m, uint32_t *&order,
                          hipStream_t s, float *tg = nullptr, const SeedParams *sp = nullptr) {
     order = (uint32_t *)ws.get(WS_ORDER, (size_t)m * 4, s);
@@ -964,25 +975,17 @@ nbkd_status sort_queries(const Tree &t, Workspace &ws, const float *dq, uint32_t
         static const bool no_heap = knob("NBKD_NO_HEAP_SPLITS") != nullptr; // A/B only
         if (t.hsplit && !no_heap) {
             const unsigned blocks = (unsigned)std::min<uint64_t>((m + TB - 1) / TB, 8192);
-            const float3 lo = t.periodic ? make_float3(0.0f, 0.0f, 0.0f)
-                                         : make_float3(t.bbox_lo[0], t.bbox_lo[1], t.bbox_lo[2]);
-            const float3 hi = t.periodic ? make_float3(t.box, t.box, t.box)
-                                         : make_float3(t.bbox_hi[0], t.bbox_hi[1], t.bbox_hi[2]);
+            const float3 lo = seed_lo(t), hi = seed_hi(t);
             leaf_key3_kernel<<<blocks, TB, 0, s>>>((const float4 *)t.hsplit, hblk_offset(t.depth),
                                                    (uint32_t)t.n8, (uint32_t)t.leaf, dq, m,
                                                    keys, order, tg, sp ? sp->mu_c : 0.0f,
-                                                   sp ? sp->anchor : 0u, lo, hi);
+                                                   sp ? sp->anchor : 0u, lo, hi, t.axes);
         } else if (t.shape_len <= SHAPE_MAX) {
             const unsigned blocks = (unsigned)std::min<uint64_t>((m + TB - 1) / TB, 8192);
-            // periodic: the box; otherwise the real points' bounding box (the
-            // density estimate only; the traversal itself starts unbounded)
-            const float3 lo = t.periodic ? make_float3(0.0f, 0.0f, 0.0f)
-                                         : make_float3(t.bbox_lo[0], t.bbox_lo[1], t.bbox_lo[2]);
-            const float3 hi = t.periodic ? make_float3(t.box, t.box, t.box)
-                                         : make_float3(t.bbox_hi[0], t.bbox_hi[1], t.bbox_hi[2]);
+            const float3 lo = seed_lo(t), hi = seed_hi(t);
             leaf_key2_kernel<<<blocks, TB, 0, s>>>(
                 t.splits, t.shape_c, t.shape_n, t.shape_len, (uint32_t)t.n8, (uint32_t)t.leaf, dq,
-                m, keys, order, tg, sp ? sp->mu_c : 0.0f, sp ? sp->anchor : 0u, lo, hi);
+                m, keys, order, tg, sp ? sp->mu_c : 0.0f, sp ? sp->anchor : 0u, lo, hi, t.axes);
         } else {
             if (tg) NBKD_HIP(hipMemsetD32Async((hipDeviceptr_t)tg, 0x7F7FFFFF, m, s)); // FLT_MAX: no seed
             leaf_key_kernel<<<(m + TB - 1) / TB, TB, 0, s>>>(view(t), dq, m, keys, order);
@@ -1044,14 +1047,12 @@ nbkd_status self_order(const Tree &t, Workspace &ws, uint32_t m, uint32_t *&orde
     if (tgp) {
         anch = (uint2 *)ws.get(WS_ANCH, (size_t)nchunks * 8, s);
         if (!anch) return NBKD_ENOMEM;
-        const float3 lo = t.periodic ? make_float3(0.0f, 0.0f, 0.0f)
-                                     : make_float3(t.bbox_lo[0], t.bbox_lo[1], t.bbox_lo[2]);
-        const float3 hi = t.periodic ? make_float3(t.box, t.box, t.box)
-                                     : make_float3(t.bbox_hi[0], t.bbox_hi[1], t.bbox_hi[2]);
+        const float3 lo = seed_lo(t), hi = seed_hi(t);
         // an anchor below 64 points would break the two-anchors-per-chunk rule
         const uint32_t stop = std::max<uint32_t>({sp->anchor, (uint32_t)t.leaf, 128u});
         anchor_chunk_kernel<<<(nchunks + TB - 1) / TB, TB, 0, s>>>(
-            t.hsplit, hblk_offset(t.depth), (uint32_t)t.n8, stop, nchunks, anch, sp->mu_c, lo, hi);
+            t.hsplit, hblk_offset(t.depth), (uint32_t)t.n8, stop, nchunks, anch, sp->mu_c, lo, hi,
+            t.axes);
         NBKD_HIP(hipGetLastError());
     }
     const unsigned blocks = (unsigned)std::min<uint64_t>(((uint64_t)m + TB - 1) / TB, 65536);

@@ -54,7 +54,8 @@ def slab_points(a, k):
     ids = np.concatenate([oi, fl[1], fr[1]]).astype(np.uint32)
     print(f"[knn_time] slab {r}/{W} {a.scaling}: {len(ox)} own + {len(fl[0])} + {len(fr[0])} "
           f"halo, h = {h:.4g}", file=sys.stderr, flush=True)
-    return xyz, ids, len(ox)
+    ext = (min(L, bounds[r + 1] - bounds[r] + 2.0 * h), L, L)  # DeviceSlab.extent
+    return xyz, ids, len(ox), ext
 
 
 def main():
@@ -69,6 +70,8 @@ def main():
     ap.add_argument("--slab-world", type=int, default=1)
     ap.add_argument("--slab-rank", type=int, default=0)
     ap.add_argument("--scaling", choices=("strong", "weak"), default="strong")
+    ap.add_argument("--no-extent", action="store_true",
+                    help="slab tree with the reference's depth %% 3 axes (A/B of nbkd_build_ext)")
     ap.add_argument("--seed", type=int, default=20261015)
     ap.add_argument("--tune", action="append", default=[], metavar="NAME=VALUE",
                     help="nbkd_set_tuning before the runs (e.g. self_order=0)")
@@ -82,8 +85,11 @@ def main():
         capi.set_tuning(name, float(val))
     n, k = int(a.n), a.k
     ids = None
+    ext = None
     if a.slab_world > 1:
-        pts, ids, n_own = slab_points(a, k)
+        pts, ids, n_own, ext = slab_points(a, k)
+        if a.no_extent:
+            ext = None
     else:
         pts = synth.lognormal(n) if a.lognormal else synth.uniform(n, a.seed)
         n_own = n
@@ -91,7 +97,8 @@ def main():
     d = hip.DeviceArray.from_numpy(pts)
     n_tree = pts.shape[0]
     del pts
-    t = capi.Tree(n=n_tree, dev_ptr=d.ptr, leafsize=a.leaf, boxsize=1.0, stream=s.handle)
+    t = capi.Tree(n=n_tree, dev_ptr=d.ptr, leafsize=a.leaf, boxsize=1.0, stream=s.handle,
+                  extent=ext)
     if ids is not None:
         di = hip.DeviceArray.from_numpy(ids)
         t.set_ids(dev_ptr=di.ptr, stream=s.handle)
@@ -137,7 +144,8 @@ def main():
                       "slab_rank": a.slab_rank, "scaling": a.scaling, "n_arg": int(a.n),
                       "seed": a.seed, "k": k, "leaf": a.leaf, "lognormal": a.lognormal,
                       "kth": a.kth, "ball": a.ball, "wall_ms": round(wall, 3), "qps": n / wall * 1e3,
-                      "phases_ms": ph, "sha": h.hexdigest()[:16], "tune": a.tune, "stats": st}),
+                      "phases_ms": ph, "sha": h.hexdigest()[:16], "tune": a.tune,
+                      "extent": ext, "stats": st}),
           flush=True)
 
 

@@ -456,3 +456,71 @@ def test_multi_hop_second_round_on_one_gpu(gpu, oracle, tmp_path, world, bounds)
         assert np.array_equal(x["rk"].view(np.uint32), gd[ids][:, -1].view(np.uint32))
         hops = max(hops, int(x["hops"]))
     assert hops >= 2
+
+
+def _axes_for_extent(e, depth):
+    """The greedy schedule of nbkd_build_ext (api.cpp axes_for_extent)."""
+    x, out = [float(v) for v in e], []
+    for _ in range(depth):
+        k = 0
+        if x[1] > x[k]:
+            k = 1
+        if x[2] > x[k]:
+            k = 2
+        out.append(k)
+        x[k] *= 0.5
+    return out
+
+
+def _node_depths(nodes):
+    depth = np.zeros(len(nodes), np.int64)
+    for i, nd in enumerate(nodes):  # preorder: children after their parent
+        if nd["dim"] >= 0:
+            depth[nd["left"]] = depth[nd["right"]] = depth[i] + 1
+    return depth
+
+
+@pytest.mark.parametrize("box", [None, 1.0])
+def test_extent_axes_slab_tree(gpu, oracle, box):
+    """nbkd_build_ext (slab trees): every internal node splits the axis the
+    extent schedule names for its depth, extent (1, 1, 1) reproduces
+    nbkd_build's node table bit for bit, and kNN rows and radius counts equal
+    those of the depth % 3 tree (and the oracle's) on a thin x-slab."""
+    from nbodyhpc_amd import hip
+    from tests.golden.inputs import uniform
+    from tests.parity import assert_knn_equal
+    rng = np.random.Generator(np.random.PCG64(95))
+    pts = uniform(120_000, 94)
+    pts[:, 0] = (0.30 + 0.15 * rng.random(len(pts))).astype(np.float32)
+    ext = (0.15, 1.0, 1.0)
+    t_ref = gpu.Tree(pts, leafsize=32, boxsize=box)
+    t_ext = gpu.Tree(pts, leafsize=32, boxsize=box, extent=ext)
+    t_cube = gpu.Tree(pts, leafsize=32, boxsize=box, extent=(1.0, 1.0, 1.0))
+    n_ref, n_ext, n_cube = t_ref.export()[0], t_ext.export()[0], t_cube.export()[0]
+    assert n_ref.tobytes() == n_cube.tobytes()
+    depth = _node_depths(n_ext)
+    sched = _axes_for_extent(ext, int(depth.max()) + 1)
+    internal = n_ext["dim"] >= 0
+    assert np.array_equal(n_ext["dim"][internal], np.array(sched)[depth[internal]])
+    assert (n_ext["dim"][internal][:1] == 1).all()  # y first: the slab is thin in x
+    leaves = ~internal
+    assert np.array_equal(np.sort(n_ext["right"][leaves] - n_ext["left"][leaves]),
+                          np.sort(n_ref["right"][~(n_ref["dim"] >= 0)]
+                                  - n_ref["left"][~(n_ref["dim"] >= 0)]))
+    k = 24
+    dp = hip.DeviceArray.from_numpy(pts)
+    t_dev = gpu.Tree(n=len(pts), dev_ptr=dp.ptr, leafsize=32, boxsize=box, extent=ext)
+    od = hip.DeviceArray((len(pts), k), np.float32)
+    oi = hip.DeviceArray((len(pts), k), np.uint32)
+    s = hip.Stream()
+    t_dev.query_device(dp.ptr, len(pts), k, od.ptr, oi.ptr, s.handle)  # self order
+    s.synchronize()
+    d0, i0 = t_ref.query(pts, k)
+    for d, i in ((od.numpy(), oi.numpy()), t_ext.query(pts, k)):
+        assert np.array_equal(d.view(np.uint32), d0.view(np.uint32))
+        assert_knn_equal(d, i, d0, i0, pts, pts, box)
+    q = uniform(20_000, 96)
+    d1, i1 = t_ext.query(q, k)
+    dr, ir = oracle.tree(pts, 32, box).query(q, k, workers=8)
+    assert_knn_equal(d1, i1, dr, ir, pts, q, box)
+    assert np.array_equal(t_ext.ball_count(pts, 0.01), t_ref.ball_count(pts, 0.01))
