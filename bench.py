@@ -949,8 +949,14 @@ def main():
     # N > 1: rows whose k-th neighbour lies past the halo are forwarded to the
     # neighbours and merged (second-round exchange) inside
     # every step, so every row of every step is exact; no rebuild, no widening
+    # the rows' k-th distances beside them (nbkd_set_kth_out): the forward test
+    # reads 4 B per own row instead of each row's last line
+    side = None if ds is None else hip.DeviceArray((own,), np.float32)
+    if side is not None:
+        tree.set_kth_out(side.ptr, own)
     rows_b = None if ds is None else [slab.DeviceRows(ds, tree, k, b[0].ptr, b[1].ptr,
-                                                      stream=stream.handle) for b in bufs]
+                                                      stream=stream.handle,
+                                                      side_ptr=side.ptr) for b in bufs]
     rows = None if rows_b is None else rows_b[0]
     cover = None if ds is None else slab.covered_range(ds.bounds, rank, ds.h)
     sr_acc = {"rows_forwarded": 0, "forwards": 0, "hops": 0, "calls": 0, "host_s": 0.0}

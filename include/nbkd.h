@@ -226,6 +226,15 @@ nbkd_status nbkd_stats_read_all(uint64_t *out, int32_t n);
  * queries then return these ids (e.g. global particle ids of a slab tree). */
 nbkd_status nbkd_set_ids(nbkd_tree *tree, const uint32_t *ids, uint32_t flags, void *stream);
 
+/* A device array of `capacity` floats beside the tree's kNN rows: each later
+ * nbkd_query_knn of the tree's own points (the first m <= capacity rows of
+ * the device array it was built from) with NBKD_OUTPUT_DEVICE also writes
+ * every row's last column (its k-th distance, as the row holds it) to
+ * kth[row].  A slab's exactness test then reads 4 B per row instead of a
+ * row's last line (nbkd_slab_forward_async with dist = kth, k = 1).  kth =
+ * NULL or capacity = 0 detaches it; other calls leave it untouched. */
+nbkd_status nbkd_set_kth_out(nbkd_tree *tree, float *kth, uint64_t capacity);
+
 /* Stable compaction of the points with lo <= x < hi into out_xyz / out_ids
  * (ids may be NULL: then the row number is stored).  *count receives the
  * number selected; with out_xyz or out_ids NULL only the count is computed. */

@@ -38,6 +38,7 @@ _u32 = ctypes.c_uint32
 _PROTOS = {
     "nbkd_build": (_i32, [_c_p, _u64, _i32, _i32, ctypes.c_float, _i32, _u32, _c_p,
                           ctypes.POINTER(_c_p)]),
+    "nbkd_set_kth_out": (_i32, [_c_p, _c_p, _u64]),
     "nbkd_build_ext": (_i32, [_c_p, _u64, _i32, _i32, ctypes.c_float, _c_p, _i32, _u32, _c_p,
                               ctypes.POINTER(_c_p)]),
     "nbkd_query_knn": (_i32, [_c_p, _c_p, _u64, _i32, _c_p, _c_p, _u32, _c_p]),
@@ -199,6 +200,11 @@ class Tree:
     def query_kth_device(self, q_ptr, m, k, d_ptr, stream=None, input_device=True):
         flags = NBKD_OUTPUT_DEVICE | (NBKD_INPUT_DEVICE if input_device else 0)
         _check(lib().nbkd_query_kth(self.h, q_ptr, int(m), int(k), d_ptr, flags, stream))
+
+    def set_kth_out(self, dev_ptr=None, capacity=0):
+        """nbkd_set_kth_out: self queries with device rows also write each row's
+        k-th distance to dev_ptr[row] (None detaches)."""
+        _check(lib().nbkd_set_kth_out(self.h, dev_ptr, int(capacity) if dev_ptr else 0))
 
     def set_ids(self, ids=None, *, dev_ptr=None, stream=None):
         """Map the tree's point ids through `ids` (host array or device pointer)."""

@@ -167,6 +167,10 @@ struct Tree {
     int npad_leaves = 0;
     uint32_t pad_leaves[NBKD_PAD_LEAVES] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu,
                                             0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+    // nbkd_set_kth_out: self queries with device outputs also write each
+    // row's last column to kth_side[row] (rows < kth_side_cap)
+    mutable float *kth_side = nullptr;
+    mutable uint64_t kth_side_cap = 0;
     mutable Workspace ws;
     // further workspaces for concurrent calls (created on demand, at most
     // NBKD_MAX_WS - 1), guarded by ws_mu
@@ -348,7 +352,8 @@ nbkd_status launch_knn_collect(const Tree &t, const float *q, const uint32_t *or
                                uint32_t capg, uint32_t *ccount, float *od, uint32_t *oi,
                                uint32_t *fail_list, uint32_t *fail_count, uint32_t *fail_bits,
                                uint32_t pos_base, bool retry, bool fix_seed, bool sq, float *kb,
-                               unsigned long long *stats, hipStream_t s);
+                               unsigned long long *stats, hipStream_t s,
+                               float *kth_side = nullptr);
 
 // the same pass as its two halves
 nbkd_status launch_collect_pass(const Tree &t, const float *q, const uint32_t *order, QSpan span,
@@ -360,7 +365,7 @@ nbkd_status launch_select_pass(const Tree &t, const float *q, const uint32_t *or
                                uint32_t capg, const uint32_t *ccount, float *od, uint32_t *oi,
                                uint32_t *fail_list, uint32_t *fail_count, uint32_t *fail_bits,
                                uint32_t pos_base, bool retry, bool fix_seed, bool sq, float *kb,
-                               hipStream_t s);
+                               hipStream_t s, float *kth_side = nullptr);
 
 // ball.hip: radius count (out_idx == nullptr) or CSR fill over m kd-ordered
 // queries (periodic queries outside [0, L]^3 are skipped: query.hip answers them)

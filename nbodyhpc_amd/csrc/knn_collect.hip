@@ -498,7 +498,8 @@ select_block(const DevTree &t, const float *__restrict__ q, const uint32_t *__re
              uint32_t *__restrict__ out_i, uint32_t *__restrict__ fail_list,
              uint32_t *__restrict__ fail_count, uint32_t pos_base, uint64_t all_rows,
              float *__restrict__ tg_fix, bool tg_pos, float mu, bool sq,
-             uint32_t *__restrict__ fail_bits, uint32_t *stage, uint32_t *rowq, const int lane) {
+             uint32_t *__restrict__ fail_bits, uint32_t *stage, uint32_t *rowq, const int lane,
+             float *__restrict__ kth_side) {
     constexpr int NS = 16;                  // candidates merged per pass
     constexpr int CC = KC < 32 ? KC : 32;   // top-k registers staged per output pass
     // lane = one query gq; its candidates: packet gq / qpp, row gq % qpp
@@ -604,6 +605,9 @@ select_block(const DevTree &t, const float *__restrict__ q, const uint32_t *__re
         if (valid) out_d[qo] = sq ? td[KC - 1] : sqrtf(td[KC - 1]);
         return;
     }
+    // the row's last column beside it (nbkd_set_kth_out); a failed row is
+    // written again by its re-walk
+    if (kth_side && ok) kth_side[qo] = sq ? td[KC - 1] : sqrtf(td[KC - 1]);
     rowq[lane] = valid ? qo : 0xFFFFFFFFu;
 #pragma unroll
     for (int j0 = 0; j0 < KC; j0 += CC) {
@@ -639,7 +643,8 @@ knn_select_kernel(DevTree t, const float *__restrict__ q, const uint32_t *__rest
                   const uint32_t *__restrict__ ccount, float *__restrict__ out_d,
                   uint32_t *__restrict__ out_i, uint32_t *__restrict__ fail_list,
                   uint32_t *__restrict__ fail_count, uint32_t pos_base, uint64_t all_rows,
-                  float *__restrict__ tg_fix, float mu, bool sq, uint32_t *__restrict__ fail_bits) {
+                  float *__restrict__ tg_fix, float mu, bool sq, uint32_t *__restrict__ fail_bits,
+                  float *__restrict__ kth_side) {
     constexpr int SW = select_stage_words<KC>();
     __shared__ uint32_t stage_all[WPB][SW];
     __shared__ uint32_t rowq_all[WPB][64];
@@ -651,14 +656,16 @@ knn_select_kernel(DevTree t, const float *__restrict__ q, const uint32_t *__rest
             wave_sync(); // the previous wave-block's LDS reads are done
             select_block<KC, PER, WHOLE>(t, q, order, m, wb, k, cand, capg, ccount, out_d, out_i,
                                          fail_list, fail_count, pos_base, all_rows, tg_fix,
-                                         span.tg_pos, mu, sq, fail_bits, stage, rowq, lane);
+                                         span.tg_pos, mu, sq, fail_bits, stage, rowq, lane,
+                                         kth_side);
         }
     } else {
         const uint32_t wb = blockIdx.x * WPB + wave;
         if (wb * 64u >= m) return;
         select_block<KC, PER, WHOLE>(t, q, order, m, wb, k, cand, capg, ccount, out_d, out_i,
                                      fail_list, fail_count, pos_base, all_rows, tg_fix,
-                                     span.tg_pos, mu, sq, fail_bits, stage, rowq, lane);
+                                     span.tg_pos, mu, sq, fail_bits, stage, rowq, lane,
+                                     kth_side);
     }
 }
 
@@ -1052,7 +1059,7 @@ void launch_select(const Tree &t, const float *q, const uint32_t *order, QSpan s
                    uint32_t qpp, const uint2 *cand, uint32_t capg, const uint32_t *ccount,
                    float *od, uint32_t *oi, uint32_t *fail_list, uint32_t *fail_count,
                    uint32_t *fail_bits, uint32_t pos_base, float *tg_fix, float mu, bool sq,
-                   hipStream_t s) {
+                   hipStream_t s, float *kth_side) {
     // a capped pass (round 1's later batches, usually empty): at most
     // resident_blocks() blocks striding over its wave-blocks (LOOP); any other
     // pass one wave per 64 queries of its count or cap, at 4 waves per SIMD
@@ -1070,7 +1077,7 @@ void launch_select(const Tree &t, const float *q, const uint32_t *order, QSpan s
     knn_select_kernel<KC, PER, WH, LP><<<blocks, TB, 0, s>>>(view(t), q, order, span, k, qpp,     \
                                                             cand, capg, ccount, od, oi, fail_list, \
                                                             fail_count, pos_base, all_rows,        \
-                                                            tg_fix, mu, sq, fail_bits)
+                                                            tg_fix, mu, sq, fail_bits, kth_side)
     if (loop) {
         if (t.periodic) {
             if (qpp == 64) NBKD_SELECT(true, true, true); else NBKD_SELECT(true, false, true);
@@ -1110,13 +1117,13 @@ nbkd_status launch_knn_collect(const Tree &t, const float *q, const uint32_t *or
                                uint32_t capg, uint32_t *ccount, float *od, uint32_t *oi,
                                uint32_t *fail_list, uint32_t *fail_count, uint32_t *fail_bits,
                                uint32_t pos_base, bool retry, bool fix_seed, bool sq, float *kb,
-                               unsigned long long *stats, hipStream_t s) {
+                               unsigned long long *stats, hipStream_t s, float *kth_side) {
     nbkd_status rc = launch_collect_pass(t, q, order, span, k, tg, seed_mul, qpp, cand, capg,
                                          ccount, retry, kb, stats, s);
     if (rc) return rc;
     return launch_select_pass(t, q, order, span, k, tg, qpp, cand, capg, ccount, od, oi,
                               fail_list, fail_count, fail_bits, pos_base, retry, fix_seed, sq, kb,
-                              s);
+                              s, kth_side);
 }
 
 nbkd_status launch_collect_pass(const Tree &t, const float *q, const uint32_t *order, QSpan span,
@@ -1141,7 +1148,7 @@ nbkd_status launch_select_pass(const Tree &t, const float *q, const uint32_t *or
                                uint32_t capg, const uint32_t *ccount, float *od, uint32_t *oi,
                                uint32_t *fail_list, uint32_t *fail_count, uint32_t *fail_bits,
                                uint32_t pos_base, bool retry, bool fix_seed, bool sq, float *kb,
-                               hipStream_t s) {
+                               hipStream_t s, float *kth_side) {
     if (span.m == 0) return NBKD_OK;
     float *kbound = k > 64 ? kb : nullptr;
     {
@@ -1151,13 +1158,13 @@ nbkd_status launch_select_pass(const Tree &t, const float *q, const uint32_t *or
         const float mu = (float)k + 4.0f * sqrtf((float)k) + 4.0f;
         if (k <= 16)
             launch_select<16>(t, q, order, span, k, qpp, cand, capg, ccount, od, oi, fail_list,
-                              fail_count, fail_bits, pos_base, tg_fix, mu, sq, s);
+                              fail_count, fail_bits, pos_base, tg_fix, mu, sq, s, kth_side);
         else if (k <= 32)
             launch_select<32>(t, q, order, span, k, qpp, cand, capg, ccount, od, oi, fail_list,
-                              fail_count, fail_bits, pos_base, tg_fix, mu, sq, s);
+                              fail_count, fail_bits, pos_base, tg_fix, mu, sq, s, kth_side);
         else if (k <= 64)
             launch_select<64>(t, q, order, span, k, qpp, cand, capg, ccount, od, oi, fail_list,
-                              fail_count, fail_bits, pos_base, tg_fix, mu, sq, s);
+                              fail_count, fail_bits, pos_base, tg_fix, mu, sq, s, kth_side);
         else if (k <= 128)
             launch_select_wave<2>(t, q, order, span, k, qpp, cand, capg, ccount, od, oi,
                                   fail_list, fail_count, fail_bits, pos_base, tg_fix, mu, sq, kbound, s);

@@ -884,6 +884,19 @@ bits_emit_dense_kernel(const uint32_t *__restrict__ bits, const uint32_t *__rest
     if ((w >> b) & 1u) out[pc_excl[j >> 5] + (uint32_t)__popc(w & ((1u << b) - 1u))] = (uint32_t)j;
 }
 
+// kth[id] = rows[id * k + k - 1] for the ids of a device-counted list (list
+// nullptr: every row below m): the rows no lane select wrote (the exact
+// kernel's, every row at k > 64) into the nbkd_set_kth_out array
+__global__ void __launch_bounds__(TB)
+kth_patch_kernel(const float *__restrict__ rows, int k, const uint32_t *__restrict__ list,
+                 const uint32_t *__restrict__ count, uint32_t m, float *__restrict__ kth) {
+    const uint32_t n = list ? min(*count, m) : m;
+    for (uint32_t i = blockIdx.x * TB + threadIdx.x; i < n; i += gridDim.x * TB) {
+        const uint32_t id = list ? list[i] : i;
+        kth[id] = rows[(size_t)id * k + k - 1];
+    }
+}
+
 // the entries of a device-counted list past what the rounds handled: appended
 // to the next list (order irrelevant there: one query per wave, or the exact
 // kernel)
@@ -1150,6 +1163,10 @@ nbkd_status knn_locked(const Tree &t, Workspace &ws, const float *q, uint64_t m,
         rc = sort_queries(t, ws, dq, mm, ord, s, tg, &sp);
     }
     if (rc) return rc;
+    // nbkd_set_kth_out: self queries with device rows also leave each row's
+    // last column in t.kth_side (the slab layer's exactness test reads it)
+    float *const ks = self && !kth_only && (flags & NBKD_OUTPUT_DEVICE) && t.kth_side &&
+                              m <= t.kth_side_cap ? t.kth_side : nullptr;
     float *dd = out_d;
     uint32_t *di = out_i;
     if (!(flags & NBKD_OUTPUT_DEVICE)) {
@@ -1270,7 +1287,7 @@ nbkd_status knn_locked(const Tree &t, Workspace &ws, const float *q, uint64_t m,
                     sp1.tg_pos = self; // seeds (and the first pass's rewritten ones) per position
                     rc = launch_knn_collect(t, dq, ord + b0, sp1, k, self ? tgp + b0 : tg, 1.0f, 64u,
                                             cand, capg, ccount, dd, di, nullptr, nullptr, bits,
-                                            (uint32_t)b0, false, adaptive, sq, kb, stats, s);
+                                            (uint32_t)b0, false, adaptive, sq, kb, stats, s, ks);
                     if (rc) return rc;
                 }
             }
@@ -1298,7 +1315,8 @@ nbkd_status knn_locked(const Tree &t, Workspace &ws, const float *q, uint64_t m,
                     rc = launch_knn_collect(t, dq, rq + bi * rb, sp, k, tg, adaptive ? 1.0f : 4.0f,
                                             mode == 1 ? 64u : 1u, cand, capr, ccount, dd, di,
                                             adaptive ? r2 : list, adaptive ? r2_count : count,
-                                            nullptr, 0xFFFFFFFFu, true, adaptive, sq, kb, nullptr, s);
+                                            nullptr, 0xFFFFFFFFu, true, adaptive, sq, kb, nullptr, s,
+                                            ks);
                     if (rc) return rc;
                 }
             }
@@ -1319,7 +1337,7 @@ nbkd_status knn_locked(const Tree &t, Workspace &ws, const float *q, uint64_t m,
                     const QSpan sp{(uint32_t)cap2, r2_count, (uint32_t)(bi * rb2), mm, 0};
                     rc = launch_knn_collect(t, dq, r2 + bi * rb2, sp, k, tg, 1.0f, 1u, cand, capr2,
                                             ccount, dd, di, list, count, nullptr, 0xFFFFFFFFu, true,
-                                            false, sq, kb, nullptr, s);
+                                            false, sq, kb, nullptr, s, ks);
                     if (rc) return rc;
                 }
                 TimedScope ts4("knn_retry", s);
@@ -1346,6 +1364,14 @@ nbkd_status knn_locked(const Tree &t, Workspace &ws, const float *q, uint64_t m,
                                                                     k, lt, dd, di, sq);
             NBKD_HIP(hipGetLastError());
             if (stats) NBKD_HIP(hipMemcpyAsync(stats + 8, count, 4, hipMemcpyDeviceToDevice, s));
+        }
+    }
+    if (ks) { // rows the lane selects did not write: the exact kernel's, or all at k > 64
+        const bool all = !packet || k > 64;
+        if (all || list) {
+            kth_patch_kernel<<<all ? std::max(1u, std::min(65536u, (mm + TB - 1) / TB)) : 64, TB, 0,
+                               s>>>(dd, k, all ? nullptr : list, all ? nullptr : count, mm, ks);
+            NBKD_HIP(hipGetLastError());
         }
     }
     if (stats) {

@@ -303,6 +303,21 @@ nbkd_status nbkd_set_ids(nbkd_tree *tree, const uint32_t *ids, uint32_t flags, v
     SLAB_CATCH
 }
 
+nbkd_status nbkd_set_kth_out(nbkd_tree *tree, float *kth, uint64_t capacity) {
+    SLAB_TRY
+    if (!tree) {
+        set_error("nbkd_set_kth_out: NULL tree");
+        return NBKD_EINVAL;
+    }
+    Tree &t = tree->t;
+    DevGuard g(t.device);
+    AllWs all(t, nullptr); // no query of this tree runs while the target changes
+    t.kth_side = capacity ? kth : nullptr;
+    t.kth_side_cap = kth ? capacity : 0;
+    return NBKD_OK;
+    SLAB_CATCH
+}
+
 nbkd_status nbkd_slab_select(const float *xyz, const uint32_t *ids, uint64_t n, float lo, float hi,
                              float *out_xyz, uint32_t *out_ids, uint64_t capacity,
                              uint64_t *count, int32_t device, void *stream) {

@@ -793,9 +793,14 @@ class DeviceRows:
     buffers, grouped send/recv) when the slab has a communicator, else over
     gloo; the neighbour's answer is its tree's NBKD_SQUARED kNN."""
 
-    def __init__(self, ds, tree, k, od_ptr=None, oi_ptr=None, kth_ptr=None, stream=None):
+    def __init__(self, ds, tree, k, od_ptr=None, oi_ptr=None, kth_ptr=None, stream=None,
+                 side_ptr=None):
         self.ds, self.tree, self.k = ds, tree, int(k)
         self.od_ptr, self.oi_ptr, self.kth_ptr = od_ptr, oi_ptr, kth_ptr
+        # side_ptr: the tree's nbkd_set_kth_out array, holding the last
+        # column of the rows the latest kNN wrote: start()'s forward test
+        # reads 4 B per row there instead of each row's last line
+        self.side_ptr = side_ptr
         self.stream = stream
         self._cap = 0
         self._list = self._sides = None
@@ -852,7 +857,12 @@ class DeviceRows:
             self._dcount = hip.DeviceArray((1,), np.uint64)
             self._hcount = hip.HostBuffer((1,), np.uint64)
             self._ev = hip.Event()
-        dptr, kk = (self.kth_ptr, 1) if self.kth_ptr is not None else (self.od_ptr, self.k)
+        if self.kth_ptr is not None:
+            dptr, kk = self.kth_ptr, 1
+        elif self.side_ptr is not None:
+            dptr, kk = self.side_ptr, 1
+        else:
+            dptr, kk = self.od_ptr, self.k
         capi.slab_forward_async(ds.xyz.ptr, dptr, ds.n_own, kk, cl, ch, self._dcount.ptr,
                                 self._list.ptr, self._sides.ptr, self._cap, device=ds.device,
                                 stream=self.stream)
@@ -869,6 +879,8 @@ class DeviceRows:
         from . import capi
 
         ds = self.ds
+        # the rows themselves here, not side_ptr: a later kNN may have
+        # rewritten that array by now (the bench queues its next step first)
         dptr, kk = (self.kth_ptr, 1) if self.kth_ptr is not None else (self.od_ptr, self.k)
         if self._pending == (float(np.float32(cl)), float(np.float32(ch))):
             self._pending = None

@@ -158,3 +158,34 @@ def test_host_queries_do_not_take_the_self_order(knobs):
     d, _ = t.query(pts, 8)
     assert gpu.timing_read("self_order")[1] == 0
     assert np.all(d[:, 0] == 0.0)
+
+
+@pytest.mark.parametrize("box,k,margin", [(1.0, 32, 3.5), (1.0, 32, 0.05), (None, 16, 0.05),
+                                          (1.0, 80, 3.5)])
+def test_kth_out_beside_the_rows(knobs, box, k, margin):
+    """nbkd_set_kth_out: a self query with device rows leaves each row's last
+    column in the attached array, bit for bit, whichever path wrote the row
+    (lane select, re-walk rounds at a tiny seed margin, the exact kernel, the
+    wave select at k > 64); other queries leave it untouched."""
+    from nbodyhpc_amd import hip
+    gpu = knobs
+    gpu.set_tuning("knn_seed_margin", margin)
+    pts = _lognormal(120_000, 77, box or 1.0)
+    dp = hip.DeviceArray.from_numpy(pts)
+    t = gpu.Tree(n=len(pts), dev_ptr=dp.ptr, leafsize=64, boxsize=box)
+    m = 100_001
+    side = hip.DeviceArray((m,), np.float32)
+    hip.memcpy(side.ptr, np.full(m, -1.0, np.float32).ctypes.data, 4 * m, hip.H2D)
+    t.set_kth_out(side.ptr, m)
+    d, _, took = _knn(gpu, t, dp, m, k, True)
+    assert took
+    assert np.array_equal(side.numpy().view(np.uint32), d[:, k - 1].view(np.uint32))
+    before = side.numpy().copy()
+    other = hip.DeviceArray.from_numpy(uniform(m, 78, L=box or 1.0))
+    _knn(gpu, t, other, m, k, True)  # not the build array: no self order, no side write
+    gpu.set_tuning("self_order", 0.0)
+    _knn(gpu, t, dp, m, k, False)  # the sorted path leaves it untouched too
+    assert np.array_equal(side.numpy().view(np.uint32), before.view(np.uint32))
+    t.set_kth_out(None)
+    _knn(gpu, t, dp, 50_000, k, True)
+    assert np.array_equal(side.numpy().view(np.uint32), before.view(np.uint32))
