@@ -144,3 +144,25 @@ def test_type_stub_names_the_reference_surface():
         init = [f for f in cls.body if isinstance(f, ast.FunctionDef) and f.name == "__init__"][0]
         assert [a.arg for a in init.args.args][:5] == ["self", "points", "leafsize", "max_threads",
                                                        "boxsize"]
+
+
+def test_build_ext_and_kth_out_arguments_rejected():
+    """nbkd_build_ext checks its extents and nbkd_set_kth_out its tree before
+    any device call; self_order is a 0 / 1 knob like the others."""
+    L = capi.lib()
+    h = ctypes.c_void_p()
+    pts = np.zeros((16, 3), np.float32)
+    for bad in ((0.0, 1.0, 1.0), (1.0, -1.0, 1.0), (1.0, 1.0, float("inf")),
+                (float("nan"), 1.0, 1.0)):
+        ext = (ctypes.c_float * 3)(*bad)
+        assert L.nbkd_build_ext(pts.ctypes.data, 16, 16, 0, 0.0, ctypes.cast(ext, ctypes.c_void_p),
+                                0, 0, None, ctypes.byref(h)) == capi.NBKD_EINVAL
+        assert "extents must be positive" in L.nbkd_last_error().decode()
+    assert L.nbkd_set_kth_out(None, None, 0) == capi.NBKD_EINVAL
+    old = capi.get_tuning("self_order")
+    assert old == 1.0
+    try:
+        capi.set_tuning("self_order", 0.0)
+        assert capi.get_tuning("self_order") == 0.0
+    finally:
+        capi.set_tuning("self_order", old)
