@@ -117,15 +117,22 @@ def _worker(rank, world, port, n_per, k, outdir, rccl=False, hscale=1.0, same_gp
         ds = slab.DeviceSlab(xyz, ids, rank, world, 1.0, dev, dist, comm=comm)
         h = slab.halo_width(n_per * world, k, 1.0) * hscale
         ds.exchange(h)
-        t = capi.Tree(n=ds.n_local, dev_ptr=ds.xyz.ptr, leafsize=32, boxsize=1.0, device=dev)
+        # as the bench builds a rank's tree: split axes by the slab's extent,
+        # the rows' k-th distances beside them for the forward test
+        t = capi.Tree(n=ds.n_local, dev_ptr=ds.xyz.ptr, leafsize=32, boxsize=1.0, device=dev,
+                      extent=ds.extent())
         t.set_ids(dev_ptr=ds.ids.ptr)
+        side = hip.DeviceArray((n_per,), np.float32)
+        t.set_kth_out(side.ptr, n_per)
         od = hip.DeviceArray((n_per, k), np.float32)
         oi = hip.DeviceArray((n_per, k), np.uint32)
         t.query_device(ds.xyz.ptr, n_per, k, od.ptr, oi.ptr)
         hip.synchronize()
         v = ds.violations(od.ptr, k)
-        # second-round exchange (device forward test, gather / scatter, RCCL or gloo)
-        rows = slab.DeviceRows(ds, t, k, od.ptr, oi.ptr)
+        # second-round exchange (device forward test on the side array, as the
+        # bench's pipelined step starts it; gather / scatter, RCCL or gloo)
+        rows = slab.DeviceRows(ds, t, k, od.ptr, oi.ptr, side_ptr=side.ptr)
+        rows.start(*slab.covered_range(ds.bounds, rank, ds.h))
         st = slab.second_round(rows, rank, world, ds.bounds, 1.0, ds.h, k, dist)
         hip.synchronize()
         # and the k-th-distance-only form of the same resolution
