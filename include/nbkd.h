@@ -162,7 +162,7 @@ void nbkd_free(nbkd_tree *tree);
 
 /* Process-wide tuning knobs (the library reads no environment variable):
  *   "knn_seed_margin"  a in the seed ball's expected count mu = k + a sqrt(k) + a
- *                      (default 3.5; > 0).  Results never depend on it: a query
+ *                      (default 3.0; > 0).  Results never depend on it: a query
  *                      whose seed ball holds fewer than k points is re-walked.
  *   "candidate_bytes"  HBM budget of one collect / select batch's candidate
  *                      columns (default 0 = min(96 GiB, free / 3)).

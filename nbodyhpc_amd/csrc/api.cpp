@@ -241,7 +241,7 @@ void tree_free(void *p) {
 
 namespace {
 // nbkd_set_tuning knobs (process-wide); defaults are the measured optima
-std::atomic<double> g_tune[TUNE_N] = {{3.5}, {0.0}, {0.0}, {0.0}, {1.0}};
+std::atomic<double> g_tune[TUNE_N] = {{3.0}, {0.0}, {0.0}, {0.0}, {1.0}};
 const char *const g_tune_names[TUNE_N] = {"knn_seed_margin", "candidate_bytes", "host_batch",
                                           "host_threads", "self_order"};
 thread_local nbkd_interrupt_fn t_intr = nullptr;

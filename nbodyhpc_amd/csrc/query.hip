@@ -64,8 +64,8 @@ constexpr int SHAPE_MAX = 256;
 
 // Guessed squared search radius of a query from the point density of the
 // subtree it falls in (count points in the box lo..hi): the radius of a sphere
-// expected to hold `mu_c` * 4/3*pi points, mu = k + 3.5 sqrt(k) + 3.5 (Poisson
-// tail ~2e-4 below k; seed_params).  Only a pruning seed: the kNN kernel starts with this
+// expected to hold `mu_c` * 4/3*pi points, mu = k + a sqrt(k) + a, a = 3 (Poisson
+// tail ~8e-4 below k at k = 32; seed_params).  Only a pruning seed: the kNN kernel starts with this
 // bound instead of +inf and sends every query that finds fewer than k points
 // inside it to the reference-exact kernel, so a bad guess costs time, never
 // correctness.
@@ -945,11 +945,16 @@ struct SeedParams {
     uint32_t anchor;
 };
 SeedParams seed_params(const Tree &t, int k) {
-    // a = 3.5: at 1e8 uniform 1.400e9 q/s (20.5 k retries) vs 1.376e9 at a = 4
-    // (4.9 k), 1.393e9 at 3, 1.372e9 at 2.5, 1.361e9 at 5; log-normal 82.3 ms
-    // at both 3.5 and 4 (r02bg, r02bi).  The column capacity keeps a = 4.
-    // nbkd_set_tuning("knn_seed_margin") (default 3.5); NBKD_KNN_SEED in an
-    // experiments build (0 there: no seed, the register top-k packet kernel)
+    // a = 3.0 (round 5, with the self order, profiles/r05ab_seed_margin_ab.txt,
+    // r05ac): 1e8 uniform 57.13 -> 56.92 ms (20.6 k -> 82 k re-walks, 49.9 ->
+    // 47.9 candidates per query), log-normal 69.23 -> 69.11; 2.5 and below are
+    // faster on uniform (56.46 at 2.25) but slower on log-normal (+0.43 ms at
+    // 2.5, +1.6 at 2.0).  Until round 4 a = 3.5: 1.400e9 q/s at 1e8 uniform
+    // (20.5 k retries) vs 1.376e9 at 4 (4.9 k), 1.393e9 at 3, 1.372e9 at 2.5,
+    // 1.361e9 at 5; log-normal 82.3 ms at both 3.5 and 4 (r02bg, r02bi).  The
+    // column capacity keeps a = 4.  nbkd_set_tuning("knn_seed_margin")
+    // (default 3.0); NBKD_KNN_SEED in an experiments build (0 there: no seed,
+    // the register top-k packet kernel)
     const char *e = knob("NBKD_KNN_SEED");
     const float a = e ? (float)atof(e) : (float)tuning(TUNE_KNN_SEED);
     SeedParams p;
