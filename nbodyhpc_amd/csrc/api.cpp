@@ -28,10 +28,38 @@ std::mutex g_tmu;
 bool g_timing = false;
 bool g_stats_on = false;
 struct TimedLaunch {
-    std::string name;
+    const char *name; // a string literal (TimedScope's)
     hipEvent_t a, b;
+    int dev;
 };
 std::vector<TimedLaunch> g_pending;
+// harvested events go back to a per-device pool: creating two events per
+// timed scope cost ~0.4 ms per step of an N = 8 slab (the re-walk rounds'
+// ~40 launches; profiles/r05ak_timing_overhead.txt)
+std::map<int, std::vector<hipEvent_t>> g_free_events;
+hipEvent_t take_event(int dev) {
+    {
+        std::lock_guard<std::mutex> lk(g_tmu);
+        auto &v = g_free_events[dev];
+        if (!v.empty()) {
+            hipEvent_t e = v.back();
+            v.pop_back();
+            return e;
+        }
+    }
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    return e;
+}
+// g_tmu held
+void give_events(const TimedLaunch &p) {
+    auto &v = g_free_events[p.dev];
+    v.push_back(p.a);
+    v.push_back(p.b);
+}
 std::map<std::string, std::pair<double, uint64_t>> g_acc;
 
 struct DeviceGuard {
@@ -406,25 +434,26 @@ void stats_add(const uint64_t *v) {
     for (int i = 0; i < NBKD_NSTATS; ++i) g_stats[i] += v[i];
 }
 
-TimedScope::TimedScope(const char *name, hipStream_t s) : name_(name), s_(s) {
-    if (!g_timing) return;
-    if (hipEventCreate(&a_) != hipSuccess) {
-        a_ = nullptr;
+TimedScope::TimedScope(const char *name, hipStream_t s, bool on) : name_(name), s_(s) {
+    if (!g_timing || !on) return;
+    if (hipGetDevice(&dev_) != hipSuccess) {
+        (void)hipGetLastError();
         return;
     }
-    (void)hipEventRecord(a_, s_);
+    a_ = take_event(dev_);
+    if (a_) (void)hipEventRecord(a_, s_);
 }
 
 TimedScope::~TimedScope() {
     if (!a_) return;
-    hipEvent_t b;
-    if (hipEventCreate(&b) != hipSuccess) {
-        (void)hipEventDestroy(a_);
+    hipEvent_t b = take_event(dev_);
+    std::lock_guard<std::mutex> lk(g_tmu);
+    if (!b) {
+        g_free_events[dev_].push_back(a_);
         return;
     }
     (void)hipEventRecord(b, s_);
-    std::lock_guard<std::mutex> lk(g_tmu);
-    g_pending.push_back(TimedLaunch{name_, a_, b});
+    g_pending.push_back(TimedLaunch{name_, a_, b, dev_});
 }
 
 } // namespace nbkd
@@ -719,8 +748,7 @@ nbkd_status nbkd_timing_reset(void) {
     std::lock_guard<std::mutex> lk(g_tmu);
     for (auto &p : g_pending) {
         (void)hipEventSynchronize(p.b);
-        (void)hipEventDestroy(p.a);
-        (void)hipEventDestroy(p.b);
+        give_events(p);
     }
     g_pending.clear();
     g_acc.clear();
@@ -737,8 +765,7 @@ nbkd_status nbkd_timing_read(const char *name, double *ms, uint64_t *launches) {
         auto &acc = g_acc[p.name];
         acc.first += t;
         acc.second += 1;
-        (void)hipEventDestroy(p.a);
-        (void)hipEventDestroy(p.b);
+        give_events(p);
     }
     g_pending.clear();
     auto it = g_acc.find(name);

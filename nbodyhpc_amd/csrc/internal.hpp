@@ -248,12 +248,15 @@ nbkd_status hip_fail(hipError_t e, const char *what);
     } while (0)
 
 // event timing (api.cpp)
+// HIP events around a phase on stream s when nbkd_timing_enable is on (and
+// `on`); name must be a string literal (kept until the events are read)
 struct TimedScope {
-    TimedScope(const char *name, hipStream_t s);
+    TimedScope(const char *name, hipStream_t s, bool on = true);
     ~TimedScope();
     const char *name_;
     hipStream_t s_;
     hipEvent_t a_ = nullptr;
+    int dev_ = 0;
 };
 bool timing_enabled();
 bool stats_enabled();

@@ -1012,7 +1012,8 @@ void launch_collect(const Tree &t, const float *q, const uint32_t *order, QSpan 
             const char *e = knob("NBKD_XCD_MAP");
             return !(e && atoi(e) == 0);
         }();
-        TimedScope ts(name, s);
+        // the re-walk rounds are timed as one phase by the caller (query.hip)
+        TimedScope ts(name, s, !retry);
 #define NBKD_GRP(STATS, LOOP, AHEAD, STP, XCD)                                                     \
     knn_collect_grp_kernel<PER, 8, STATS, LOOP, AHEAD><<<blocks, TB, 0, s>>>(                      \
         view(t), t.ginfo, t.leafinfo, t.hinfo, q, order, span, k, tg, seed_mul, qpp, cand, capg,   \
@@ -1152,7 +1153,7 @@ nbkd_status launch_select_pass(const Tree &t, const float *q, const uint32_t *or
     if (span.m == 0) return NBKD_OK;
     float *kbound = k > 64 ? kb : nullptr;
     {
-        TimedScope ts(retry ? "knn_retry" : "knn_select", s);
+        TimedScope ts("knn_select", s, !retry);
         // a retry round follows: failures rewrite their seed for it
         float *tg_fix = fix_seed ? const_cast<float *>(tg) : nullptr;
         const float mu = (float)k + 4.0f * sqrtf((float)k) + 4.0f;

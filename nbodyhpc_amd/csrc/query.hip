@@ -1314,6 +1314,9 @@ nbkd_status knn_locked(const Tree &t, Workspace &ws, const float *q, uint64_t m,
             constexpr uint64_t RB1_MAX = 10;
             const uint32_t nb1 =
                 (uint32_t)std::min<uint64_t>(RB1_MAX, std::max<uint64_t>(1, (mm64 + rb - 1) / rb));
+            // the re-walk rounds as one timed phase (one pair of events, not
+            // one per launch of their ~40 mostly empty launches)
+            TimedScope ts3("knn_retry", s);
             for (uint32_t bi = 0; bi < nb1; ++bi) {
                 for (int mode = 1; mode <= 2; ++mode) {
                     const QSpan sp{(uint32_t)cap1, rq_count, (uint32_t)(bi * rb), mm, mode, bi > 0};
@@ -1325,12 +1328,9 @@ nbkd_status knn_locked(const Tree &t, Workspace &ws, const float *q, uint64_t m,
                     if (rc) return rc;
                 }
             }
-            {
-                TimedScope ts3("knn_retry", s);
-                spill_kernel<<<64, TB, 0, s>>>(rq, rq_count, (uint32_t)std::min<uint64_t>(nb1 * rb, mm64),
-                                               adaptive ? r2 : list, adaptive ? r2_count : count);
-                NBKD_HIP(hipGetLastError());
-            }
+            spill_kernel<<<64, TB, 0, s>>>(rq, rq_count, (uint32_t)std::min<uint64_t>(nb1 * rb, mm64),
+                                           adaptive ? r2 : list, adaptive ? r2_count : count);
+            NBKD_HIP(hipGetLastError());
             if (adaptive) {
                 // round 2, one query per wave: the seed each failure rewrote
                 // (2x..8x volume when short, the same seed when the 8x column
@@ -1345,7 +1345,6 @@ nbkd_status knn_locked(const Tree &t, Workspace &ws, const float *q, uint64_t m,
                                             false, sq, kb, nullptr, s, ks);
                     if (rc) return rc;
                 }
-                TimedScope ts4("knn_retry", s);
                 spill_kernel<<<64, TB, 0, s>>>(r2, r2_count, (uint32_t)std::min<uint64_t>(nb2 * rb2, mm),
                                                list, count);
                 NBKD_HIP(hipGetLastError());

@@ -73,6 +73,8 @@ def main():
     ap.add_argument("--no-extent", action="store_true",
                     help="slab tree with the reference's depth %% 3 axes (A/B of nbkd_build_ext)")
     ap.add_argument("--seed", type=int, default=20261015)
+    ap.add_argument("--no-timing", action="store_true",
+                    help="time the steps with the library's phase timers off (no phases)")
     ap.add_argument("--tune", action="append", default=[], metavar="NAME=VALUE",
                     help="nbkd_set_tuning before the runs (e.g. self_order=0)")
     ap.add_argument("--stats", action="store_true",
@@ -117,7 +119,7 @@ def main():
         run = lambda: t.query_device(d.ptr, n, k, od.ptr, oi.ptr, s.handle)  # noqa: E731
     run()
     s.synchronize()
-    capi.timing_enable(True)
+    capi.timing_enable(not a.no_timing)
     capi.timing_reset()
     t0 = time.perf_counter()
     for _ in range(a.steps):
