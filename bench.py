@@ -231,6 +231,7 @@ def parse():
                    help="raw float32 (N, 3) particle file (reference main.cpp -f format) "
                         "instead of the synthetic set; N > 1 streams each rank's slab")
     p.add_argument("--launch-probe", action="store_true", help=argparse.SUPPRESS)
+    p.add_argument("--probe-rccl-fail", default="", help=argparse.SUPPRESS)
     p.add_argument("--input-format", choices=("raw", "gadget"), default="raw",
                    help="gadget: a Gadget-2 snapshot (format 1/2, multi-file; N > 1 streams each "
                         "rank's slab unless --redistribute); the box is its BoxSize")
@@ -347,6 +348,29 @@ def gloo_halo() -> bool:
     instead of RCCL, e.g. where RCCL cannot run; the timed step has no collective
     either way."""
     return os.environ.get("NBKD_HALO_TRANSPORT", "rccl").lower() == "gloo"
+
+
+def rank_report(dist, rank, world, local, same_dev):
+    """N > 1: what every rank saw, gathered over gloo so a
+    first multi-GPU run can be read from its line alone.  `local` holds this
+    rank's numbers (step / collect ms, transports); the RCCL failures come from
+    slab.RCCL_ERRORS.  Returns
+      rccl_error  every rank's fallback reasons ("rank r: what: message"), or None;
+      degraded    True when the ranks sit on distinct devices, gloo was not
+                  asked for (NBKD_HALO_TRANSPORT=gloo) and some rank's halo or second
+                  round did not run over RCCL;
+      per_rank    each key of `local` as a list over the ranks."""
+    from nbodyhpc_amd import slab
+    mine = dict(local, rccl_errors=list(slab.RCCL_ERRORS))
+    got = [None] * world
+    dist.all_gather_object(got, mine)
+    errs = [e for g in got for e in g["rccl_errors"]]
+    tr = [g.get(kk) for g in got for kk in ("halo_transport", "second_round_transport")]
+    tr = [t for t in tr if t not in (None, "none")]
+    degraded = (not same_dev) and (not gloo_halo()) and any(t != "rccl" for t in tr)
+    keys = [kk for kk in local]
+    return {"rccl_error": errs or None, "degraded": bool(degraded),
+            "per_rank": {kk: [g.get(kk) for g in got] for kk in keys}}
 
 
 def timed(fn, steps, hip):
@@ -678,6 +702,9 @@ def run_c5(args, rank, world, local_rank, dist, same_dev, barrier, allmax, allsu
     # collectives on every rank, before rank 0 alone writes the line
     sr_fwd = 0.0 if ds is None else allsum(float(sr_acc["rows_forwarded"])) / max(sr_acc["calls"], 1)
     sr_hops = 0 if ds is None else int(allmax(float(sr_acc["hops"])))
+    rep = None if ds is None else rank_report(dist, rank, world, {
+        "own_particles": own, "local_points": n_local,
+        "halo_transport": ds.transport, "second_round_transport": rows.transport}, same_dev)
     if rank != 0:
         return
     q_total = sums[0] * args.steps
@@ -717,7 +744,8 @@ def run_c5(args, rank, world, local_rank, dist, same_dev, barrier, allmax, allsu
             "kth_rows_past_halo": violations,
             "second_round": {"transport": rows.transport,
                              "rows_forwarded_per_pass": sr_fwd,
-                             "max_hops": sr_hops}},
+                             "max_hops": sr_hops},
+            **rep},
         "bounds": bounds,
         "build_ms": build_ms,
         "generate_s": gen_s,
@@ -781,15 +809,30 @@ def init_gloo(rank, world):
     return dist
 
 
-def launch_probe(rank, world, dist):
+def launch_probe(rank, world, dist, fail_rccl=()):
     """--launch-probe (tests): the ranks meet over gloo and rank 0 prints one
-    JSON line naming them; no GPU is touched."""
+    JSON line naming them; no GPU is touched.  --probe-rccl-fail R,..: those
+    ranks' RCCL probe fails (a forced failure: slab.init_comm with a probe
+    that raises), and the line carries the N > 1 report fields the bench line
+    would (rank_report: rccl_error, degraded, per-rank numbers)."""
     import torch
+    from nbodyhpc_amd import slab
     out = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
     dist.all_gather(out, torch.tensor([rank], dtype=torch.int64))
+
+    def probe():
+        if rank in fail_rccl:
+            raise RuntimeError("forced RCCL failure (launch probe)")
+
+    slab.init_comm(dist, rank, world, None, probe=probe)  # None: a probe starts no communicator
+    # every rank holds the same list: with a failure every rank stages over gloo
+    transport = "gloo-staged" if fail_rccl else "rccl"
+    rep = rank_report(dist, rank, world, {"step_ms": 1.0 + rank, "collect_ms": 0.5 + rank,
+                                          "halo_transport": transport,
+                                          "second_round_transport": transport}, False)
     if rank == 0:
         print(json.dumps({"n_gpus": world, "ranks": [int(x.item()) for x in out],
-                          "launch_probe": True}), flush=True)
+                          "launch_probe": True, "halo": rep}), flush=True)
 
 
 def main():
@@ -803,7 +846,8 @@ def main():
         log(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
     if args.launch_probe:
         dist = init_gloo(rank, world)
-        launch_probe(rank, world, dist)
+        fail = [int(x) for x in args.probe_rccl_fail.split(",") if x != ""]
+        launch_probe(rank, world, dist, fail)
         dist.destroy_process_group()
         return
     from nbodyhpc_amd import capi, hip
@@ -1075,7 +1119,8 @@ def main():
             tree.query_device(dev_pts.ptr, own, k, bufs[0][0].ptr, bufs[0][1].ptr, stream.handle)
         hip.synchronize()
         barrier()
-        knn_only = allmax(time.perf_counter() - t_k) / args.steps
+        knn_only_local = (time.perf_counter() - t_k) / args.steps
+        knn_only = allmax(knn_only_local * args.steps) / args.steps
         halo["second_round"] = {
             "transport": rows.transport,
             "rows_forwarded_per_step": allsum(float(sr_timed["rows_forwarded"])) / max(args.steps, 1),
@@ -1089,6 +1134,17 @@ def main():
             "knn_only_ms_per_step": knn_only * 1e3,
         }
         counts = allgather_int(own)
+        # every rank's own numbers beside the max-over-ranks step (VERDICT r05
+        # #6: set them against profiles/r05ao_slab_ranks.txt's per-rank steps)
+        halo.update(rank_report(dist, rank, world, {
+            "step_ms": elapsed / args.steps * 1e3,
+            "collect_ms_per_launch": col_ms / max(col_launches, 1),
+            "select_ms_per_step": sel_ms / args.steps,
+            "knn_only_ms_per_step": knn_only_local * 1e3,
+            "second_round_host_ms_per_step": sr_timed["host_s"] / args.steps * 1e3,
+            "own_particles": own, "local_points": n_local,
+            "halo_transport": ds.transport, "second_round_transport": rows.transport},
+            same_dev))
     else:
         counts = [own]
     total_q = own_total * args.steps
@@ -1111,6 +1167,8 @@ def main():
     # the whole step's HBM bytes (every kernel of the query), same build, one GPU
     step_traffic, step_source = pmc_step_traffic(own, k) if world == 1 else (None, None)
     step_sec = elapsed_max / args.steps
+    useful = float(own_total) * k * 8 + 16.0 * (own_total if world == 1 else allsum(float(n_local))) \
+        + 16.0 * (tree.size if world == 1 else allsum(float(tree.size)))
     step_ach = None if step_traffic is None else step_traffic / step_sec / 1e9
     peak = HBM_PEAK_GBS
     basis = None
@@ -1173,7 +1231,14 @@ def main():
             # PMC HBM bytes of one step / the step's wall time
             step_traffic=step_traffic, step_traffic_source=step_source,
             step_achieved=step_ach,
-            step_frac=None if step_ach is None else step_ach / peak),
+            step_frac=None if step_ach is None else step_ach / peak,
+            # the bytes a step cannot avoid: the k-column rows
+            # written (f32 + u32), the packed points read once (16 B) and the
+            # node table (16 B per node); the step's PMC traffic over this is
+            # the step's waste factor
+            useful_bytes=useful,
+            useful_frac_of_step_traffic=None if step_traffic is None else useful / step_traffic,
+            useful_achieved=useful / step_sec / 1e9),
         "breakdown_ms_per_step": {
             "self_order": self_ms / args.steps, "leaf_key": key_ms / args.steps,
             "sort": sort_ms / args.steps, "knn": knn_ms / args.steps, "knn_collect": col_ms / args.steps,

@@ -176,6 +176,12 @@ void nbkd_free(nbkd_tree *tree);
  *                      instead of bucketing and sorting the queries; 0: always
  *                      bucket and sort.  Results never depend on it (the order
  *                      and the seeds only steer the work).
+ *   "pinned_bytes"     process-wide cap on the host-buffer pipeline's pinned
+ *                      staging (default 0 = 8 GiB).  A call whose staging would
+ *                      pass it, or whose hipHostMalloc fails, streams between
+ *                      the caller's pageable arrays and the device instead
+ *                      (same results, lower rate).  Idle workspaces release
+ *                      their staging when a device allocation needs memory.
  * NEW (no reference counterpart: kdtree/src/cpp/pybind.cpp:196-216 has no knobs). */
 nbkd_status nbkd_set_tuning(const char *name, double value);
 nbkd_status nbkd_get_tuning(const char *name, double *value);

@@ -269,9 +269,9 @@ void tree_free(void *p) {
 
 namespace {
 // nbkd_set_tuning knobs (process-wide); defaults are the measured optima
-std::atomic<double> g_tune[TUNE_N] = {{3.0}, {0.0}, {0.0}, {0.0}, {1.0}};
+std::atomic<double> g_tune[TUNE_N] = {{3.0}, {0.0}, {0.0}, {0.0}, {1.0}, {0.0}};
 const char *const g_tune_names[TUNE_N] = {"knn_seed_margin", "candidate_bytes", "host_batch",
-                                          "host_threads", "self_order"};
+                                          "host_threads", "self_order", "pinned_bytes"};
 thread_local nbkd_interrupt_fn t_intr = nullptr;
 thread_local void *t_intr_user = nullptr;
 } // namespace
@@ -834,8 +834,25 @@ void Workspace::release() {
     }
     if (copy) (void)hipStreamDestroy(copy);
     copy = nullptr;
+    free_pinned();
+}
+
+// Pinned staging over every workspace of the process is capped (ADVICE r05:
+// several trees or workspaces could each keep ~2 GiB pinned): past the cap,
+// or when hipHostMalloc fails, host_pinned returns nullptr and the pipeline
+// streams through pageable memory instead (the runtime stages those copies).
+static std::atomic<uint64_t> g_pinned_bytes{0};
+static uint64_t pinned_cap() { // nbkd_set_tuning("pinned_bytes"), 0 = 8 GiB
+    const double v = tuning(TUNE_PINNED_BYTES);
+    return v > 0.0 ? (uint64_t)v : (8ull << 30);
+}
+
+void Workspace::free_pinned() {
     for (int b = 0; b < 2; ++b) {
-        if (hpin[b]) (void)hipHostFree(hpin[b]);
+        if (hpin[b]) {
+            (void)hipHostFree(hpin[b]);
+            g_pinned_bytes -= hpin_cap[b];
+        }
         hpin[b] = nullptr;
         hpin_cap[b] = 0;
     }
@@ -848,12 +865,18 @@ void *Workspace::host_pinned(int slot, size_t bytes) {
         // the slot's last DMA belongs to a finished call (every call drains
         // its copies before returning)
         (void)hipHostFree(hpin[slot]);
+        g_pinned_bytes -= hpin_cap[slot];
         hpin[slot] = nullptr;
         hpin_cap[slot] = 0;
     }
+    if (g_pinned_bytes.fetch_add(bytes) + bytes > pinned_cap()) {
+        g_pinned_bytes -= bytes;
+        return nullptr; // over the process cap: pageable streaming
+    }
     hipError_t e = hipHostMalloc(&hpin[slot], bytes, hipHostMallocDefault);
     if (e != hipSuccess) {
-        (void)hip_fail(e, "hipHostMalloc(pipeline staging)");
+        (void)hipGetLastError(); // not an error of the call: pageable streaming
+        g_pinned_bytes -= bytes;
         hpin[slot] = nullptr;
         return nullptr;
     }
@@ -887,6 +910,9 @@ void Workspace::trim() {
         p[i] = nullptr;
         cap[i] = 0;
     }
+    // an idle workspace's pinned staging goes back too (every call drains its
+    // copies before returning, so no DMA can still use it)
+    free_pinned();
     (void)hipGetLastError();
 }
 

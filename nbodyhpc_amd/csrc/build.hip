@@ -2,9 +2,9 @@
 //
 // Produces the reference's node table (KDTreeBuilder::build_node,
 // kdtree/src/cpp/include/kdtree/kdtree_impl.hpp:98-146) on the device:
-//   * leaf iff count <= max(leaf_size, 16)                       (:485, :495)
+//   * leaf iff count <= max(leaf_size, 16)     (kdtree_impl.hpp:101-104)
 //   * m = (count / 2) / 8 * 8; split = m-th order statistic of the
-//     segment's coordinate on axis depth % 3                      (:502-510)
+//     segment's coordinate on axis depth % 3    (kdtree_impl.hpp:107-116)
 //     (Tree::axes; a tree built with nbkd_build_ext splits the axis of
 //     largest remaining extent instead: slab trees, not the reference's)
 //   * preorder ids, left child = id + 1, right = id + 1 + |left subtree|

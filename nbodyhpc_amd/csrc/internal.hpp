@@ -48,7 +48,10 @@ struct Workspace {
     // kept across calls: pinning is paid once per workspace, not per call)
     void *hpin[2] = {};
     size_t hpin_cap[2] = {};
-    void *host_pinned(int slot, size_t bytes); // nullptr on failure (error recorded)
+    // nullptr when pinning fails or the process-wide cap (8 GiB) is reached:
+    // the pipeline then streams through pageable memory
+    void *host_pinned(int slot, size_t bytes);
+    void free_pinned();
     // returns nullptr on failure (hip error recorded via set_error)
     void *get(int slot, size_t bytes, hipStream_t s);
     void release();
@@ -226,6 +229,7 @@ enum TuneId {
     TUNE_HOST_BATCH,
     TUNE_HOST_THREADS,
     TUNE_SELF_ORDER,
+    TUNE_PINNED_BYTES,
     TUNE_N
 };
 // host memcpy split over the library's copy threads (api.cpp): the host-buffer

@@ -938,6 +938,11 @@ int key_bits(const Tree &t) {
 // the collect / select path serves k <= 1024 (knn_select_kernel for k <= 64,
 // knn_select_wave_kernel above); larger k replays the reference per lane
 constexpr int KNN_PACKET_KMAX = 1024;
+// internal flag (never a caller's): this knn_locked call is an nbkd_query_knn
+// whose CALLER asked for device rows, so it may write the nbkd_set_kth_out
+// array (host_pipeline adds NBKD_OUTPUT_DEVICE to its batch calls,
+// and kth_locked's k > 1024 rows go to scratch; neither may touch it)
+constexpr uint32_t KNN_SIDE_OK = 0x80000000u;
 
 struct SeedParams {
     bool on;
@@ -1168,9 +1173,16 @@ nbkd_status knn_locked(const Tree &t, Workspace &ws, const float *q, uint64_t m,
         rc = sort_queries(t, ws, dq, mm, ord, s, tg, &sp);
     }
     if (rc) return rc;
-    // nbkd_set_kth_out: self queries with device rows also leave each row's
-    // last column in t.kth_side (the slab layer's exactness test reads it)
-    float *const ks = self && !kth_only && (flags & NBKD_OUTPUT_DEVICE) && t.kth_side &&
+    // nbkd_set_kth_out: a query of the tree's own rows (the first m of the
+    // device array it was built from) with device rows also leaves each row's
+    // last column in t.kth_side (the slab layer's exactness test reads it).
+    // On every path: the self order or the sorted one
+    // (self_order = 0), the lane selects write it (select_block indexes it by
+    // query id), the exact kernel's rows and every row at k > 64 (including
+    // k > 1024, no packet path) are copied by kth_patch_kernel below
+    const bool own_rows = (flags & NBKD_INPUT_DEVICE) && q != nullptr && q == t.src && m > 0 &&
+                          m <= t.n;
+    float *const ks = own_rows && !kth_only && (flags & KNN_SIDE_OK) && t.kth_side &&
                               m <= t.kth_side_cap ? t.kth_side : nullptr;
     float *dd = out_d;
     uint32_t *di = out_i;
@@ -1456,6 +1468,7 @@ nbkd_status host_pipeline(Workspace &ws, const float *q, uint64_t m, uint32_t fl
     float *qslot[2] = {nullptr, nullptr};
     void *oslot[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
     char *hp[2] = {nullptr, nullptr};
+    bool pageable = false;
     // pinned slot layout: [queries hb x 12 B][output 0][output 1]
     size_t ooff[2] = {in_dev ? 0 : hb * 12, 0};
     if (nout > 1) ooff[1] = ooff[0] + (out_dev ? 0 : hb * obytes[0]);
@@ -1469,9 +1482,11 @@ nbkd_status host_pipeline(Workspace &ws, const float *q, uint64_t m, uint32_t fl
                 oslot[b][j] = ws.get(WS_HO00 + 2 * b + j, hb * obytes[j], s);
                 if (!oslot[b][j]) return NBKD_ENOMEM;
             }
-        if (per_q) {
+        if (per_q && !pageable) {
             hp[b] = (char *)ws.host_pinned(b, hb * per_q);
-            if (!hp[b]) return NBKD_ENOMEM;
+            // pinning failed or the process cap is reached:
+            // stream between the caller's pageable arrays and the device
+            if (!hp[b]) pageable = true;
         }
     }
     nbkd_status rc = NBKD_OK;
@@ -1502,10 +1517,11 @@ nbkd_status host_pipeline(Workspace &ws, const float *q, uint64_t m, uint32_t fl
             if (!in_dev) {
                 // pinned slot b's previous queries (batch i-2) have left for the device
                 if (in_rec[b]) NBKD_PIPE(hipEventSynchronize(ev_in[b]));
-                host_copy(hp[b], q + 3 * b0, nb * 12);
+                if (!pageable) host_copy(hp[b], q + 3 * b0, nb * 12);
                 // device slot b is free once batch i-2 finished reading it
                 if (comp_rec[b]) NBKD_PIPE(hipStreamWaitEvent(cp, ev_comp[b], 0));
-                NBKD_PIPE(hipMemcpyAsync(qslot[b], hp[b], nb * 12, hipMemcpyHostToDevice, cp));
+                NBKD_PIPE(hipMemcpyAsync(qslot[b], pageable ? (const void *)(q + 3 * b0) : hp[b],
+                                         nb * 12, hipMemcpyHostToDevice, cp));
                 NBKD_PIPE(hipEventRecord(ev_in[b], cp));
                 in_rec[b] = true;
                 NBKD_PIPE(hipStreamWaitEvent(s, ev_in[b], 0));
@@ -1523,8 +1539,9 @@ nbkd_status host_pipeline(Workspace &ws, const float *q, uint64_t m, uint32_t fl
             if (!out_dev) {
                 NBKD_PIPE(hipStreamWaitEvent(cp, ev_comp[b], 0));
                 for (int j = 0; j < nout; ++j)
-                    NBKD_PIPE(hipMemcpyAsync(hp[b] + ooff[j], oslot[b][j], nb * obytes[j],
-                                             hipMemcpyDeviceToHost, cp));
+                    NBKD_PIPE(hipMemcpyAsync(pageable ? (char *)outs[j] + b0 * obytes[j]
+                                                      : hp[b] + ooff[j],
+                                             oslot[b][j], nb * obytes[j], hipMemcpyDeviceToHost, cp));
                 NBKD_PIPE(hipEventRecord(ev_out[b], cp));
                 out_rec[b] = true;
             }
@@ -1535,8 +1552,9 @@ nbkd_status host_pipeline(Workspace &ws, const float *q, uint64_t m, uint32_t fl
             const int pb = (int)((i - 1) & 1) % nslots;
             const uint64_t p0 = (i - 1) * hb, pn = std::min<uint64_t>(hb, m - p0);
             NBKD_PIPE(hipEventSynchronize(ev_out[pb]));
-            for (int j = 0; j < nout; ++j)
-                host_copy((char *)outs[j] + p0 * obytes[j], hp[pb] + ooff[j], pn * obytes[j]);
+            if (!pageable)
+                for (int j = 0; j < nout; ++j)
+                    host_copy((char *)outs[j] + p0 * obytes[j], hp[pb] + ooff[j], pn * obytes[j]);
         }
     }
 #undef NBKD_PIPE
@@ -1573,7 +1591,9 @@ nbkd_status query_knn(const Tree &t, const float *q, uint64_t m, int k, float *o
     WsCall call(ws, s, std::adopt_lock);
     NBKD_HIP(call.err);
     const uint32_t dev_io = NBKD_INPUT_DEVICE | NBKD_OUTPUT_DEVICE;
-    if ((flags & dev_io) == dev_io) return knn_locked(t, ws, q, m, k, out_d, out_i, flags, s);
+    flags &= ~KNN_SIDE_OK;
+    if ((flags & dev_io) == dev_io)
+        return knn_locked(t, ws, q, m, k, out_d, out_i, flags | KNN_SIDE_OK, s);
     const size_t ob[2] = {(size_t)k * 4, (size_t)k * 4};
     void *const outs[2] = {out_d, out_i};
     return host_pipeline(ws, q, m, flags, 2, ob, outs, knn_scratch_per_query(t, k, false),

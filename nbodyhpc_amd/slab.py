@@ -329,6 +329,7 @@ def _redistribute_rccl(sx, si, rank, world, comm, soff, roff, n_own, device, dis
             hip.memcpy(dri.ptr + int(roff[rank]) * 4, dsi.ptr + int(soff[rank]) * 4, n_self * 4)
         err = _enqueue_agreed(dist, rank, "redistribution", lambda: comm.exchange(pairs))
         if err is not None:
+            note_rccl_error(rank, "redistribution failed, moved over gloo", err)
             # a failed group may still read or write these: never free them
             _ABANDONED.extend((dsx, dsi, drx, dri))
             dsx = dsi = drx = dri = None
@@ -420,7 +421,8 @@ class DeviceSlab:
                 # every rank failed: the gloo path below is exact too.  RCCL may
                 # have queued part of the group before failing, so the staged
                 # strips go to fresh buffers and the old ones are never freed.
-                self.log(f"rank {self.rank}: RCCL exchange failed ({err}); staging over gloo")
+                note_rccl_error(self.rank, "halo exchange failed, staged over gloo", err,
+                                self.log)
                 _ABANDONED.extend((xyz, ids) + tuple(b for v in sel.values() for b in v[1:]))
                 xyz = hip.DeviceArray((n_loc, 3), np.float32)
                 ids = hip.DeviceArray((n_loc,), np.uint32)
@@ -458,8 +460,23 @@ class DeviceSlab:
                                     self.h, device=self.device, stream=stream)
 
 
-def init_comm(dist, rank, world, device, log=None):
-    """RCCL communicator (unique id broadcast over gloo); None if it cannot start."""
+# This process's RCCL failures ("rank r: what: message"), in order: every path
+# that falls back to gloo (communicator start, halo exchange, second round,
+# redistribution) notes why here, so the bench line can carry the reason
+# (halo.rccl_error) instead of leaving it on stderr alone.
+RCCL_ERRORS = []
+
+
+def note_rccl_error(rank, what, err, log=None):
+    msg = f"rank {rank}: {what}: {err}"
+    RCCL_ERRORS.append(msg)
+    if log is not None:
+        log(msg)
+
+
+def init_comm(dist, rank, world, device, log=None, probe=None):
+    """RCCL communicator (unique id broadcast over gloo); None if it cannot
+    start.  `probe` (tests: a forced failure) replaces nbkd_comm_probe."""
     from . import capi
 
     log = log or (lambda *a: None)
@@ -472,12 +489,14 @@ def init_comm(dist, rank, world, device, log=None):
     # that cannot load it would leave the others waiting there for ever
     ok = torch.zeros(1, dtype=torch.int64)
     try:
-        capi.comm_probe()
+        (probe or capi.comm_probe)()
         ok[0] = 1
     except Exception as e:
-        log(f"rank {rank}: RCCL unavailable: {e}")
+        note_rccl_error(rank, "RCCL unavailable", e, log)
     dist.all_reduce(ok, op=dist.ReduceOp.MIN)
     if not int(ok[0]):
+        return None
+    if probe is not None:  # a probe run (tests): no communicator is started
         return None
     # only rank 0 creates the unique id (ncclGetUniqueId starts the bootstrap
     # root); its last byte says whether that worked
@@ -486,14 +505,14 @@ def init_comm(dist, rank, world, device, log=None):
         try:
             buf = torch.tensor(list(capi.comm_unique_id()) + [1], dtype=torch.uint8)
         except Exception as e:
-            log(f"rank 0: ncclGetUniqueId failed: {e}")
+            note_rccl_error(rank, "ncclGetUniqueId failed", e, log)
     dist.broadcast(buf, 0)
     if int(buf[-1]) != 1:
         return None
     try:
         c = capi.Comm(bytes(buf[:-1].numpy().tobytes()), rank, world, device)
     except Exception as e:
-        log(f"rank {rank}: ncclCommInitRank failed: {e}")
+        note_rccl_error(rank, "ncclCommInitRank failed", e, log)
         c = None
     flag = torch.tensor([1 if c is not None else 0], dtype=torch.int64)
     dist.all_reduce(flag, op=dist.ReduceOp.MIN)
@@ -949,6 +968,8 @@ class DeviceRows:
             # they leave the reuse cache and are never freed
             for key in ("xs_r", "xs_l", "xr_l", "xr_r"):
                 _ABANDONED.append(self._bufs.pop(key))
+            if self.transport != "gloo":  # once per rows object
+                note_rccl_error(self.ds.rank, "second-round exchange failed, moved over gloo", err)
             self.transport = "gloo"
             return _bytes_sendrecv(self.ds.dist, right, left, send_r, send_l, n_fl, n_fr,
                                    row_shape, dtype, tags)

@@ -193,7 +193,7 @@ static void fr_select(orc_pt *p, int64_t left, int64_t right, int64_t m) {
             const double sz = 0.5 * exp(2.0 * z / 3.0);
             /* the reference's ptrdiff_t test (kdtree_selection.cpp:340) */
             const double sd = 0.5 * sqrt(z * sz * (n - sz) / n) * (ii < ni / 2 ? -1.0 : 1.0);
-            /* static_cast<ptrdiff_t>: truncation toward zero (:343-344) */
+            /* static_cast<ptrdiff_t>: truncation toward zero (kdtree_selection.cpp:343-344) */
             int64_t nl = (int64_t)((double)m - i * sz / n + sd);
             int64_t nr = (int64_t)((double)m + (n - i) * sz / n + sd);
             if (nl < left) nl = left;

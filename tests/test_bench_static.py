@@ -67,6 +67,27 @@ def test_gpus_n_without_launcher_starts_n_ranks():
     assert lines[0]["n_gpus"] == 2 and lines[0]["ranks"] == [0, 1]
 
 
+def test_n_gt_1_line_reports_rccl_errors_and_per_rank_numbers():
+    """an N > 1 line is readable on its own.  A forced RCCL
+    failure on rank 1 reaches the line as halo.rccl_error (every rank falls
+    back to gloo, so the line is marked degraded), and each rank's numbers come
+    back as lists over the ranks; without a failure there is no error and the
+    line is not degraded."""
+    rc, lines, err = _run_bench(["--gpus", "2", "--launch-probe", "--probe-rccl-fail", "1"])
+    assert rc == 0, err[-2000:]
+    h = lines[0]["halo"]
+    assert h["degraded"] is True
+    assert len(h["rccl_error"]) == 1 and h["rccl_error"][0].startswith("rank 1: RCCL unavailable")
+    assert "forced RCCL failure" in h["rccl_error"][0]
+    assert h["per_rank"]["step_ms"] == [1.0, 2.0]
+    assert h["per_rank"]["halo_transport"] == ["gloo-staged", "gloo-staged"]
+    rc, lines, err = _run_bench(["--gpus", "2", "--launch-probe"])
+    assert rc == 0, err[-2000:]
+    h = lines[0]["halo"]
+    assert h["degraded"] is False and h["rccl_error"] is None
+    assert h["per_rank"]["collect_ms"] == [0.5, 1.5]
+
+
 def test_gpus_n_with_fewer_gpus_fails_cleanly():
     """Fewer visible GPUs than --gpus (none here): a non-zero exit and no JSON
     line, never an n_gpus: 1 line for an N = 2 request."""

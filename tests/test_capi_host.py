@@ -166,3 +166,17 @@ def test_build_ext_and_kth_out_arguments_rejected():
         assert capi.get_tuning("self_order") == 0.0
     finally:
         capi.set_tuning("self_order", old)
+
+
+def test_reference_build_never_travels():
+    """no reference source, object or bytecode travels to the GPU
+    box.  oracle/_ref (the reference compiled here, the checker's checker) must
+    stay listed in .gpurunignore (round 5 had dropped the entry)."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with open(os.path.join(root, ".gpurunignore")) as f:
+        pats = {ln.strip() for ln in f if ln.strip() and not ln.startswith("#")}
+    assert "./oracle/_ref" in pats
+    # and the bench (which runs on the box) names nothing there; build() in
+    # __graft_entry__.py compiles it in this container only
+    with open(os.path.join(root, "bench.py")) as f:
+        assert "oracle/_ref" not in f.read()

@@ -13,6 +13,11 @@ SCAN = ["oracle", "nbodyhpc_amd", "include", "tests", "nbodyhpc", "DESIGN.md", "
         "bench.py", "README.md", "BASELINE.md", "__graft_entry__.py"]
 EXT = (".py", ".c", ".cpp", ".h", ".hpp", ".hip", ".md", ".pyi")
 CITE = re.compile(r"([A-Za-z0-9_./-]+\.(?:cpp|hpp|h|py|asm|pyi|txt|vert|frag)):(\d+)(?:-(\d+))?")
+# bare continuations of a citation: "file.hpp:52-61, :111-120" or "file.cpp:90 and :128"
+MORE = re.compile(r"\s*(?:,|;|and|&)?\s*:(\d+)(?:-(\d+))?")
+# a bare ":NNN" on a line of its own (no file before it on that line) names no file:
+# such lines are flagged, since the reader cannot tell which file they cite
+BARE = re.compile(r"\(\s*:(\d+)(?:-(\d+))?(?:\s*,\s*:(\d+)(?:-(\d+))?)*\s*\)")
 
 
 def _ref_files():
@@ -48,16 +53,30 @@ def test_reference_citations_resolve():
                 continue
             txt = open(fp, encoding="utf-8", errors="replace").read()
             for m in CITE.finditer(txt):
-                name, a, b = m.group(1), int(m.group(2)), int(m.group(3) or m.group(2))
+                name = m.group(1)
                 cands = [by_path[name]] if name in by_path else [
                     p for p in by_name.get(os.path.basename(name), []) if p.endswith(name)]
                 if not cands:
                     continue  # not a reference file
-                checked += 1
+                ranges = [(int(m.group(2)), int(m.group(3) or m.group(2)))]
+                pos = m.end()
+                while True:  # ", :111-120" continuations cite the same file
+                    c = MORE.match(txt, pos)
+                    if not c:
+                        break
+                    ranges.append((int(c.group(1)), int(c.group(2) or c.group(1))))
+                    pos = c.end()
                 # an ambiguous bare name (pybind.cpp in kdtree/ and rasterization/)
                 # must fit at least one of the files it may name
                 ns = [_lines(c) for c in cands]
-                if not any(1 <= a <= b <= n for n in ns):
-                    bad.append(f"{os.path.relpath(fp, ROOT)}: {m.group(0)} (files have {ns} lines)")
+                for a, b in ranges:
+                    checked += 1
+                    if not any(1 <= a <= b <= n for n in ns):
+                        bad.append(f"{os.path.relpath(fp, ROOT)}: {name}:{a}-{b} (files have {ns} lines)")
+            for m in BARE.finditer(txt):
+                # a parenthesised bare line number with no file: resolvable only by the reader's guess
+                line = txt[:m.start()].rsplit("\n", 1)[-1]
+                if not CITE.search(line):
+                    bad.append(f"{os.path.relpath(fp, ROOT)}: bare citation {m.group(0)}")
     assert checked > 100
     assert not bad, "\n".join(bad[:40])

@@ -180,3 +180,25 @@ def test_stats_sum_over_host_batches(gpu, small_host_batch):
     assert host["packets"] >= m // 64 and dev["packets"] >= m // 64
     assert abs(host["candidates"] - dev["candidates"]) < 0.1 * dev["candidates"]
     t.close()
+
+
+def test_pageable_streaming_when_pinning_is_refused(gpu, oracle, small_host_batch):
+    """a host-buffer call whose pinned staging would pass the
+    process cap ("pinned_bytes"), or whose hipHostMalloc fails, streams
+    between the caller's pageable arrays and the device instead of failing
+    with NBKD_ENOMEM: same rows, k-th distances and counts."""
+    from nbodyhpc_amd import synth
+    pts = synth.uniform(200_000, 65, 1.0)
+    q = synth.uniform(30_000 + 77, 66, 1.0)
+    o = oracle.tree(pts, 64, 1.0)
+    dr, ir = o.query(q, 16, workers=16)
+    try:
+        gpu.set_tuning("pinned_bytes", 1)  # nothing may be pinned
+        t = gpu.Tree(pts, leafsize=64, boxsize=1.0)
+        d, i = t.query(q, 16)
+        assert_knn_equal(d, i, dr, ir, pts, q, 1.0)
+        c = t.ball_count(q, 0.02)
+        assert np.array_equal(c, oracle.ball_count(o, q, 0.02))
+        t.close()
+    finally:
+        gpu.set_tuning("pinned_bytes", 0)

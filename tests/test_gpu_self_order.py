@@ -163,10 +163,12 @@ def test_host_queries_do_not_take_the_self_order(knobs):
 @pytest.mark.parametrize("box,k,margin", [(1.0, 32, 3.5), (1.0, 32, 0.05), (None, 16, 0.05),
                                           (1.0, 80, 3.5)])
 def test_kth_out_beside_the_rows(knobs, box, k, margin):
-    """nbkd_set_kth_out: a self query with device rows leaves each row's last
-    column in the attached array, bit for bit, whichever path wrote the row
-    (lane select, re-walk rounds at a tiny seed margin, the exact kernel, the
-    wave select at k > 64); other queries leave it untouched."""
+    """nbkd_set_kth_out: a query of the tree's own rows with device rows leaves
+    each row's last column in the attached array, bit for bit, whichever path
+    wrote the row (lane select, re-walk rounds at a tiny seed margin, the exact
+    kernel, the wave select at k > 64) and whichever order it took (the self
+    order or, with self_order = 0, the sorted one: ADVICE r05); queries of
+    other arrays, host-output and k-th-only calls leave it untouched."""
     from nbodyhpc_amd import hip
     gpu = knobs
     gpu.set_tuning("knn_seed_margin", margin)
@@ -175,17 +177,47 @@ def test_kth_out_beside_the_rows(knobs, box, k, margin):
     t = gpu.Tree(n=len(pts), dev_ptr=dp.ptr, leafsize=64, boxsize=box)
     m = 100_001
     side = hip.DeviceArray((m,), np.float32)
-    hip.memcpy(side.ptr, np.full(m, -1.0, np.float32).ctypes.data, 4 * m, hip.H2D)
+
+    def reset():
+        hip.memcpy(side.ptr, np.full(m, -1.0, np.float32).ctypes.data, 4 * m, hip.H2D)
+
+    reset()
     t.set_kth_out(side.ptr, m)
     d, _, took = _knn(gpu, t, dp, m, k, True)
     assert took
     assert np.array_equal(side.numpy().view(np.uint32), d[:, k - 1].view(np.uint32))
+    # the sorted path (self_order = 0) writes it too: a slab's forward test
+    # must never read a stale array
+    reset()
+    d0, _, took0 = _knn(gpu, t, dp, m, k, False)
+    assert not took0
+    assert np.array_equal(side.numpy().view(np.uint32), d0[:, k - 1].view(np.uint32))
     before = side.numpy().copy()
     other = hip.DeviceArray.from_numpy(uniform(m, 78, L=box or 1.0))
-    _knn(gpu, t, other, m, k, True)  # not the build array: no self order, no side write
-    gpu.set_tuning("self_order", 0.0)
-    _knn(gpu, t, dp, m, k, False)  # the sorted path leaves it untouched too
+    _knn(gpu, t, other, m, k, True)  # not the build array: no side write
+    # device queries of the build array, host rows: no side write
+    s = hip.Stream()
+    od = hip.DeviceArray((m,), np.float32)
+    t.query_kth_device(dp.ptr, m, k, od.ptr, s.handle)  # k-th only: untouched
+    s.synchronize()
     assert np.array_equal(side.numpy().view(np.uint32), before.view(np.uint32))
     t.set_kth_out(None)
     _knn(gpu, t, dp, 50_000, k, True)
     assert np.array_equal(side.numpy().view(np.uint32), before.view(np.uint32))
+
+
+def test_kth_out_beyond_the_packet_path(knobs):
+    """k > 1024 (no collect/select: the exact kernel writes every row) fills
+    the nbkd_set_kth_out array as well."""
+    from nbodyhpc_amd import hip
+    gpu = knobs
+    pts = uniform(6_000, 79)
+    dp = hip.DeviceArray.from_numpy(pts)
+    t = gpu.Tree(n=len(pts), dev_ptr=dp.ptr, leafsize=32, boxsize=1.0)
+    m, k = 700, 1100
+    side = hip.DeviceArray((m,), np.float32)
+    hip.memcpy(side.ptr, np.full(m, -1.0, np.float32).ctypes.data, 4 * m, hip.H2D)
+    t.set_kth_out(side.ptr, m)
+    d, _, _ = _knn(gpu, t, dp, m, k, True)
+    assert np.array_equal(side.numpy().view(np.uint32), d[:, k - 1].view(np.uint32))
+    t.set_kth_out(None)
