@@ -68,6 +68,7 @@ enum {
 #define NBKD_ACCUMULATE 0x4u    /* nbkd_deposit: add into `out` instead of overwriting it */
 #define NBKD_SQUARED 0x8u       /* nbkd_query_knn / _kth: output d2 (no sqrtf), the values
                                    the reference sorts by (kdtree.cpp:149-151) */
+#define NBKD_SORTED 0x10u       /* nbkd_query_ball_csr: each row sorted ascending (on the device) */
 
 typedef struct nbkd_tree nbkd_tree;
 
@@ -140,10 +141,17 @@ nbkd_status nbkd_query_ball_count(const nbkd_tree *tree, const float *q, uint64_
 /*
  * NEW: neighbour lists within r in CSR form.  out_offsets is (m+1,) uint64
  * (always host memory); out_idx receives offsets[m] original point indices,
- * each row in tree traversal order (unsorted; sort per row if needed).  Call with out_idx == NULL first to get
- * offsets[m] (the required capacity), then again with a buffer of that size.
- * Not batched: the call holds the m queries, their counts and the offsets[m]
- * indices in device scratch at once (split a very large m into several calls).
+ * each row in tree traversal order, or ascending with NBKD_SORTED (a per-row
+ * sort on the device).  Call with out_idx == NULL first to get offsets[m]
+ * (the required capacity), then again with a buffer of that size.
+ * Batched (round 6): the counts stream through the host-buffer pipeline; the
+ * fill runs in batches of at most ~64 M ids (a row longer than that is a batch
+ * of its own) whose ids are sorted and copied out while the next batch is
+ * computed, so device scratch is bounded by the batch, not by m or offsets[m]
+ * (the reference streams any m its host memory holds, pybind.cpp:103-104,164-172).
+ * Queries and out_idx may be host or device memory (NBKD_INPUT_DEVICE /
+ * NBKD_OUTPUT_DEVICE); the call returns when out_idx is complete.  Between
+ * batches it runs the thread's interrupt check.
  */
 nbkd_status nbkd_query_ball_csr(const nbkd_tree *tree, const float *q, uint64_t m, float r,
                                 uint64_t *out_offsets, uint32_t *out_idx, uint64_t capacity,

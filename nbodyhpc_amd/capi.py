@@ -20,6 +20,7 @@ NBKD_INPUT_DEVICE = 0x1
 NBKD_OUTPUT_DEVICE = 0x2
 NBKD_ACCUMULATE = 0x4
 NBKD_SQUARED = 0x8
+NBKD_SORTED = 0x10
 
 NODE_DTYPE = np.dtype([("dim", "<i4"), ("split", "<f4"), ("left", "<u4"), ("right", "<u4")])
 
@@ -225,17 +226,28 @@ class Tree:
         _check(lib().nbkd_query_ball_count(self.h, q_ptr, int(m), float(r), out_ptr,
                                            NBKD_INPUT_DEVICE | NBKD_OUTPUT_DEVICE, stream))
 
-    def ball_csr(self, q, r):
+    def ball_csr(self, q, r, sorted=False):
+        """CSR radius query of host queries: (offsets (m + 1,) uint64, ids);
+        sorted=True: each row ascending (NBKD_SORTED, sorted on the device)."""
         q = _host_f32(q)
         m = q.shape[0]
+        fl = NBKD_SORTED if sorted else 0
         off = np.empty(m + 1, np.uint64)
         _check(lib().nbkd_query_ball_csr(self.h, q.ctypes.data, m, float(r), off.ctypes.data,
-                                         None, 0, 0, None))
+                                         None, 0, fl, None))
         idx = np.empty(int(off[-1]), np.uint32)
         _check(lib().nbkd_query_ball_csr(self.h, q.ctypes.data, m, float(r), off.ctypes.data,
-                                         idx.ctypes.data if idx.size else None, idx.size, 0,
+                                         idx.ctypes.data if idx.size else None, idx.size, fl,
                                          None))
         return off, idx
+
+    def ball_csr_device(self, q_ptr, m, r, off, idx_ptr, capacity, sorted=False, stream=None):
+        """Device queries and device ids (offsets in host memory `off`,
+        (m + 1,) uint64); idx_ptr None: the counts pass only."""
+        fl = NBKD_INPUT_DEVICE | NBKD_OUTPUT_DEVICE | (NBKD_SORTED if sorted else 0)
+        _check(lib().nbkd_query_ball_csr(self.h, q_ptr, int(m), float(r), off.ctypes.data,
+                                         idx_ptr, int(capacity), fl, stream))
+        return off
 
 
 def deposit(xyz, weight, radius, grid, ppu, period=(-1.0, -1.0, -1.0), subsample=4, mode=0,

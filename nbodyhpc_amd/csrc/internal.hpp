@@ -390,6 +390,13 @@ void launch_ball_outside(const Tree &t, const float *q, const uint32_t *list, ui
                          float r2, uint32_t *out_count, uint32_t *fill,
                          const uint64_t *row_offsets, uint32_t *out_idx, hipStream_t s);
 
+// per-row sort of a CSR batch (row offsets `off`, nrows + 1 entries, device):
+// rows of up to csr_sort_row_cap() ids in place; longer rows are appended to
+// long_rows (count in *nlong, zeroed by the caller) for the caller to sort
+void launch_csr_sort_rows(const uint64_t *off, uint32_t *ids, uint32_t nrows, uint32_t *long_rows,
+                          uint32_t *nlong, hipStream_t s);
+uint32_t csr_sort_row_cap();
+
 // query.hip
 nbkd_status query_knn(const Tree &t, const float *q, uint64_t m, int k, float *out_d,
                       uint32_t *out_i, uint32_t flags, hipStream_t s);

@@ -161,27 +161,36 @@ class PyKDTree {
         return out;
     }
 
-    std::pair<py::array_t<uint64_t>, py::array_t<uint32_t>> query_ball_csr(farray points,
-                                                                           float r) {
+    // rows sorted ascending on the device unless sorted=false (NBKD_SORTED);
+    // both passes stream in batches and poll Ctrl-C between them
+    std::pair<py::array_t<uint64_t>, py::array_t<uint32_t>> query_ball_csr(farray points, float r,
+                                                                           bool sorted) {
         check_shape(points);
         const py::ssize_t m = points.shape(0);
         py::array_t<uint64_t> off(m + 1);
         const float *q = points.data();
         uint64_t *o = off.mutable_data();
+        const uint32_t fl = sorted ? NBKD_SORTED : 0u;
         nbkd_status st;
         {
-            py::gil_scoped_release nogil;
-            st = nbkd_query_ball_csr(h_, q, (uint64_t)m, r, o, nullptr, 0, 0u, nullptr);
+            Interruptible intr;
+            {
+                py::gil_scoped_release nogil;
+                st = nbkd_query_ball_csr(h_, q, (uint64_t)m, r, o, nullptr, 0, fl, nullptr);
+            }
+            intr.finish(st);
         }
-        check(st);
         const uint64_t nnz = o[m];
         py::array_t<uint32_t> idx((py::ssize_t)nnz);
         uint32_t *ip = idx.mutable_data();
         {
-            py::gil_scoped_release nogil;
-            st = nbkd_query_ball_csr(h_, q, (uint64_t)m, r, o, ip, nnz, 0u, nullptr);
+            Interruptible intr;
+            {
+                py::gil_scoped_release nogil;
+                st = nbkd_query_ball_csr(h_, q, (uint64_t)m, r, o, ip, nnz, fl, nullptr);
+            }
+            intr.finish(st);
         }
-        check(st);
         return {off, idx};
     }
 
@@ -210,7 +219,8 @@ PYBIND11_MODULE(_impl, m) {
              py::arg("workers") = 1)
         .def("query_kth", &PyKDTree::query_kth, py::arg("points"), py::arg("k"))
         .def("query_ball_count", &PyKDTree::query_ball_count, py::arg("points"), py::arg("r"))
-        .def("query_ball_csr", &PyKDTree::query_ball_csr, py::arg("points"), py::arg("r"))
+        .def("query_ball_csr", &PyKDTree::query_ball_csr, py::arg("points"), py::arg("r"),
+             py::arg("sorted") = true)
         .def("export", &PyKDTree::export_tree)
         .def_property_readonly("n", &PyKDTree::num_points)
         .def_property_readonly("size", &PyKDTree::num_nodes)

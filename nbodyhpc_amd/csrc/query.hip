@@ -1638,17 +1638,15 @@ nbkd_status query_kth(const Tree &t, const float *q, uint64_t m, int k, float *o
                          }, s);
 }
 
+// the radius count of m device queries (count into out_count: device memory
+// when NBKD_OUTPUT_DEVICE, else staged)
 static nbkd_status ball_common(const Tree &t, Workspace &ws, const float *q, uint64_t m, float r,
-                               uint32_t *out_count, uint64_t *offsets, uint32_t *out_idx,
-                               uint64_t capacity, uint32_t flags, hipStream_t s) {
+                               uint32_t *out_count, uint32_t flags, hipStream_t s) {
     if (m >= (1ull << 32)) {
         set_error("more than 2^32 - 1 queries per call are not supported");
         return NBKD_EINVAL;
     }
-    if (m == 0) {
-        if (offsets) offsets[0] = 0;
-        return NBKD_OK;
-    }
+    if (m == 0) return NBKD_OK;
     const uint32_t mm = (uint32_t)m;
     const float *dq = nullptr;
     nbkd_status rc = stage_queries(ws, q, m, flags, dq, s);
@@ -1658,46 +1656,32 @@ static nbkd_status ball_common(const Tree &t, Workspace &ws, const float *q, uin
                                     : sort_queries(t, ws, dq, mm, ord, s);
     if (rc) return rc;
     const float r2 = r * r;
-    // periodic queries outside [0, L]^3: listed, every point tested for them.
-    // Count mode reads the list's length on the device; the CSR fill (host
-    // offsets anyway) reads it here
-    uint32_t *list = nullptr, nout = 0;
-    const bool count_only = offsets == nullptr;
+    // periodic queries outside [0, L]^3: listed (their count stays in device
+    // memory), every point tested for them
+    uint32_t *list = nullptr;
     if (t.periodic) {
         list = (uint32_t *)ws.get(WS_LIST, (size_t)mm * 8 + 16, s);
         if (!list) return NBKD_ENOMEM;
         NBKD_HIP(hipMemsetAsync(list + mm, 0, 4, s));
         outside_box_kernel<<<(mm + TB - 1) / TB, TB, 0, s>>>(dq, mm, t.box, list, list + mm);
-        if (!count_only) {
-            NBKD_HIP(hipMemcpyAsync(&nout, list + mm, 4, hipMemcpyDeviceToHost, s));
-            NBKD_HIP(hipStreamSynchronize(s));
-        }
     }
     unsigned long long *stats = nullptr;
-    if (count_only && stats_enabled()) {
+    if (stats_enabled()) {
         stats = (unsigned long long *)ws.get(WS_STATS, NBKD_NSTATS * 8, s);
         if (!stats) return NBKD_ENOMEM;
         NBKD_HIP(hipMemsetAsync(stats, 0, NBKD_NSTATS * 8, s));
     }
-    auto run = [&](uint32_t *c, const uint64_t *off, uint32_t *idx) -> nbkd_status {
-        launch_ball_packet(t, dq, ord, mm, r2, c, off, idx, idx ? nullptr : stats, s);
-        if (count_only && list)
-            launch_ball_outside_dev(t, dq, list, list + mm, r2, c, s);
-        else
-            launch_ball_outside(t, dq, list, nout, r2, c, list + mm + 4, off, idx, s);
-        NBKD_HIP(hipGetLastError());
-        return NBKD_OK;
-    };
     uint32_t *cnt = out_count;
     const bool dev_out = flags & NBKD_OUTPUT_DEVICE;
-    if (!cnt || !dev_out) {
+    if (!dev_out) {
         cnt = (uint32_t *)ws.get(WS_COUNT, m * 4, s);
         if (!cnt) return NBKD_ENOMEM;
     }
     {
         TimedScope ts("ball_count", s);
-        rc = run(cnt, nullptr, nullptr);
-        if (rc) return rc;
+        launch_ball_packet(t, dq, ord, mm, r2, cnt, nullptr, nullptr, stats, s);
+        if (list) launch_ball_outside_dev(t, dq, list, list + mm, r2, cnt, s);
+        NBKD_HIP(hipGetLastError());
     }
     if (stats) {
         uint64_t h[NBKD_NSTATS];
@@ -1705,42 +1689,10 @@ static nbkd_status ball_common(const Tree &t, Workspace &ws, const float *q, uin
         NBKD_HIP(hipStreamSynchronize(s));
         stats_add(h);
     }
-    if (!offsets) { // count-only
-        if (!dev_out) {
-            NBKD_HIP(hipMemcpyAsync(out_count, cnt, m * 4, hipMemcpyDeviceToHost, s));
-            NBKD_HIP(hipStreamSynchronize(s));
-        }
-        return NBKD_OK;
-    }
-    // CSR: offsets on the host
-    std::vector<uint32_t> hc(m);
-    NBKD_HIP(hipMemcpyAsync(hc.data(), cnt, m * 4, hipMemcpyDeviceToHost, s));
-    NBKD_HIP(hipStreamSynchronize(s));
-    offsets[0] = 0;
-    for (uint64_t i = 0; i < m; ++i) offsets[i + 1] = offsets[i] + hc[i];
-    if (!out_idx) return NBKD_OK;
-    if (capacity < offsets[m]) {
-        set_error("query_ball_csr: capacity smaller than the number of neighbours");
-        return NBKD_EINVAL;
-    }
-    uint64_t *doff = (uint64_t *)ws.get(WS_OFF, (m + 1) * 8, s);
-    if (!doff) return NBKD_ENOMEM;
-    NBKD_HIP(hipMemcpyAsync(doff, offsets, (m + 1) * 8, hipMemcpyHostToDevice, s));
-    NBKD_HIP(hipStreamSynchronize(s));
-    uint32_t *di = out_idx;
     if (!dev_out) {
-        di = (uint32_t *)ws.get(WS_IDX, std::max<uint64_t>(offsets[m], 1) * 4, s);
-        if (!di) return NBKD_ENOMEM;
+        NBKD_HIP(hipMemcpyAsync(out_count, cnt, m * 4, hipMemcpyDeviceToHost, s));
+        NBKD_HIP(hipStreamSynchronize(s));
     }
-    {
-        TimedScope ts("ball_fill", s);
-        rc = run(nullptr, doff, di);
-        if (rc) return rc;
-    }
-    if (!dev_out) {
-        NBKD_HIP(hipMemcpyAsync(out_idx, di, offsets[m] * 4, hipMemcpyDeviceToHost, s));
-    }
-    NBKD_HIP(hipStreamSynchronize(s));
     return NBKD_OK;
 }
 
@@ -1757,16 +1709,99 @@ nbkd_status query_ball_count(const Tree &t, const float *q, uint64_t m, float r,
     NBKD_HIP(call.err);
     const uint32_t dev_io = NBKD_INPUT_DEVICE | NBKD_OUTPUT_DEVICE;
     if ((flags & dev_io) == dev_io)
-        return ball_common(t, ws, q, m, r, out_count, nullptr, nullptr, 0, flags, s);
+        return ball_common(t, ws, q, m, r, out_count, flags, s);
     const size_t ob[1] = {4};
     void *const outs[1] = {out_count};
     return host_pipeline(ws, q, m, flags, 1, ob, outs, 40,
                          [&](const float *dq, uint64_t nb, void *const *o, hipStream_t st) {
-                             return ball_common(t, ws, dq, nb, r, (uint32_t *)o[0], nullptr,
-                                                nullptr, 0, flags | dev_io, st);
+                             return ball_common(t, ws, dq, nb, r, (uint32_t *)o[0], flags | dev_io,
+                                                st);
                          }, s);
 }
 
+namespace {
+
+// The CSR fill of one batch: nb device queries, their rows at the device
+// offsets doff (nb + 1, relative to the batch), ids into di
+nbkd_status ball_fill_batch(const Tree &t, Workspace &ws, const float *dq, uint32_t nb, float r,
+                            const uint64_t *doff, uint32_t *di, hipStream_t s) {
+    uint32_t *ord = nullptr;
+    nbkd_status rc = self_query(t, dq, nb, NBKD_INPUT_DEVICE) ? self_order(t, ws, nb, ord, s)
+                                                               : sort_queries(t, ws, dq, nb, ord, s);
+    if (rc) return rc;
+    const float r2 = r * r;
+    uint32_t *list = nullptr, nout = 0;
+    if (t.periodic) { // periodic queries outside [0, L]^3: every point tested for them
+        list = (uint32_t *)ws.get(WS_LIST, (size_t)nb * 8 + 16, s);
+        if (!list) return NBKD_ENOMEM;
+        NBKD_HIP(hipMemsetAsync(list + nb, 0, 4, s));
+        outside_box_kernel<<<(nb + TB - 1) / TB, TB, 0, s>>>(dq, nb, t.box, list, list + nb);
+        NBKD_HIP(hipMemcpyAsync(&nout, list + nb, 4, hipMemcpyDeviceToHost, s));
+        NBKD_HIP(hipStreamSynchronize(s));
+    }
+    TimedScope ts("ball_fill", s);
+    launch_ball_packet(t, dq, ord, nb, r2, nullptr, doff, di, nullptr, s);
+    launch_ball_outside(t, dq, list, nout, r2, nullptr, list ? list + nb + 4 : nullptr, doff, di,
+                        s);
+    NBKD_HIP(hipGetLastError());
+    return NBKD_OK;
+}
+
+// NBKD_SORTED: every row of a batch ascending, on the device.  Rows of up to
+// csr_sort_row_cap() ids are sorted in LDS by one wave each (ball.hip); the
+// longer ones, listed by that kernel, one by one by the LSD radix sort
+// (values = keys)
+nbkd_status sort_csr_batch(Workspace &ws, const uint64_t *doff, uint32_t *di, uint32_t nb,
+                           const uint64_t *hrel, hipStream_t s) {
+    uint32_t *lr = (uint32_t *)ws.get(WS_LIST2, (size_t)nb * 4 + 64, s);
+    if (!lr) return NBKD_ENOMEM;
+    uint32_t *nl = lr + nb;
+    NBKD_HIP(hipMemsetAsync(nl, 0, 4, s));
+    {
+        TimedScope ts("csr_sort", s);
+        launch_csr_sort_rows(doff, di, nb, lr, nl, s);
+        NBKD_HIP(hipGetLastError());
+    }
+    uint32_t nlong = 0;
+    NBKD_HIP(hipMemcpyAsync(&nlong, nl, 4, hipMemcpyDeviceToHost, s));
+    NBKD_HIP(hipStreamSynchronize(s));
+    if (nlong == 0) return NBKD_OK;
+    std::vector<uint32_t> rows(nlong);
+    NBKD_HIP(hipMemcpyAsync(rows.data(), lr, (size_t)nlong * 4, hipMemcpyDeviceToHost, s));
+    NBKD_HIP(hipStreamSynchronize(s));
+    for (uint32_t row : rows) {
+        const uint64_t a = hrel[row], len = hrel[row + 1] - a;
+        if (len >= (1ull << 32)) {
+            set_error("query_ball_csr: a row of 2^32 or more neighbours cannot be sorted");
+            return NBKD_EINVAL;
+        }
+        const size_t bytes = (size_t)len * 4;
+        uint32_t *k0 = (uint32_t *)ws.get(WS_KTHD, bytes, s);
+        uint32_t *v0 = (uint32_t *)ws.get(WS_KTHI, bytes, s);
+        uint32_t *k1 = (uint32_t *)ws.get(WS_RSORT, bytes, s);
+        uint32_t *v1 = (uint32_t *)ws.get(WS_CCOUNT, bytes, s);
+        if (!k0 || !v0 || !k1 || !v1) return NBKD_ENOMEM;
+        NBKD_HIP(hipMemcpyAsync(k0, di + a, bytes, hipMemcpyDeviceToDevice, s));
+        NBKD_HIP(hipMemcpyAsync(v0, di + a, bytes, hipMemcpyDeviceToDevice, s));
+        uint32_t *vout = nullptr;
+        nbkd_status rc = radix_sort(ws, k0, v0, k1, v1, (uint32_t)len, 32, s, &vout);
+        if (rc) return rc;
+        NBKD_HIP(hipMemcpyAsync(di + a, vout, bytes, hipMemcpyDeviceToDevice, s));
+    }
+    return NBKD_OK;
+}
+
+// ids per fill batch (device scratch ~4 B each, twice for the two slots, plus
+// the pinned staging of the same size)
+constexpr uint64_t CSR_BATCH_IDS = 1ull << 26;
+
+} // namespace
+
+// Round 6: counts through the host-buffer pipeline (any m),
+// then the fill in batches bounded by CSR_BATCH_IDS ids and host_batch
+// queries, each batch sorted per row on the device (NBKD_SORTED) and copied
+// out through two pinned slots while the next batch is filled.  Until round 5
+// the call held every query, count and id in device scratch at once.
 nbkd_status query_ball_csr(const Tree &t, const float *q, uint64_t m, float r, uint64_t *offsets,
                            uint32_t *out_idx, uint64_t capacity, uint32_t flags, hipStream_t s) {
     if (m >= (1ull << 32)) {
@@ -1780,7 +1815,132 @@ nbkd_status query_ball_csr(const Tree &t, const float *q, uint64_t m, float r, u
     Workspace &ws = acquire_ws(t);
     WsCall call(ws, s, std::adopt_lock);
     NBKD_HIP(call.err);
-    return ball_common(t, ws, q, m, r, nullptr, offsets, out_idx, capacity, flags, s);
+    const uint32_t dev_io = NBKD_INPUT_DEVICE | NBKD_OUTPUT_DEVICE;
+    const bool in_dev = (flags & NBKD_INPUT_DEVICE) != 0, out_dev = (flags & NBKD_OUTPUT_DEVICE) != 0;
+    const uint32_t cflags = flags & (NBKD_INPUT_DEVICE | NBKD_OUTPUT_DEVICE);
+    nbkd_status rc;
+    {
+        // 1. every query's count, streamed into host memory
+        std::vector<uint32_t> hc(m);
+        const size_t ob[1] = {4};
+        void *const outs[1] = {hc.data()};
+        rc = host_pipeline(ws, q, m, cflags & ~NBKD_OUTPUT_DEVICE, 1, ob, outs, 40,
+                           [&](const float *dq, uint64_t nb, void *const *o, hipStream_t st) {
+                               return ball_common(t, ws, dq, nb, r, (uint32_t *)o[0],
+                                                  cflags | dev_io, st);
+                           }, s);
+        if (rc) return rc;
+        offsets[0] = 0;
+        for (uint64_t i = 0; i < m; ++i) offsets[i + 1] = offsets[i] + hc[i];
+    }
+    if (!out_idx) return NBKD_OK;
+    if (capacity < offsets[m]) {
+        set_error("query_ball_csr: capacity smaller than the number of neighbours");
+        return NBKD_EINVAL;
+    }
+    if (offsets[m] == 0) return NBKD_OK;
+    // 2. the fill, batch by batch
+    const uint64_t qcap = host_batch(12 + 8 + 40, m);
+    NBKD_HIP(ws.pipe_init());
+    hipStream_t cp = ws.copy;
+    hipEvent_t *ev_comp = ws.pev + 2, *ev_out = ws.pev + 4;
+    if (ws.used && ws.done) NBKD_HIP(hipStreamWaitEvent(cp, ws.done, 0));
+    bool out_rec[2] = {false, false};
+    uint64_t prev_b0 = 0, prev_nnz = 0;
+    int prev_slot = -1;
+    char *hp[2] = {nullptr, nullptr};
+    bool pageable = out_dev;
+    std::vector<uint64_t> rel;
+    auto drain_prev = [&]() -> nbkd_status { // batch i-1's ids: pinned -> the caller's array
+        if (prev_slot < 0 || out_dev) return NBKD_OK;
+        NBKD_HIP(hipEventSynchronize(ev_out[prev_slot]));
+        if (hp[prev_slot]) host_copy(out_idx + offsets[prev_b0], hp[prev_slot], prev_nnz * 4);
+        prev_slot = -1;
+        return NBKD_OK;
+    };
+    int it = 0;
+    for (uint64_t b0 = 0, b1; b0 < m; b0 = b1, ++it) {
+        if (b0 > 0 && interrupted()) {
+            set_error("interrupted");
+            rc = NBKD_EINTR;
+            break;
+        }
+        // the longest run of queries from b0 holding at most CSR_BATCH_IDS ids
+        // (at least one query) and qcap queries
+        const uint64_t lim = std::min<uint64_t>(m, b0 + qcap);
+        b1 = (uint64_t)(std::upper_bound(offsets + b0 + 1, offsets + lim + 1,
+                                         offsets[b0] + CSR_BATCH_IDS) - offsets) - 1;
+        b1 = std::max<uint64_t>(b1, b0 + 1);
+        const uint32_t nb = (uint32_t)(b1 - b0);
+        const uint64_t nnz = offsets[b1] - offsets[b0];
+        const int b = it & 1;
+        const float *dq = nullptr;
+        rc = stage_queries(ws, q + 3 * b0, nb, cflags, dq, s);
+        if (rc) break;
+        rel.resize(nb + 1);
+        for (uint32_t i = 0; i <= nb; ++i) rel[i] = offsets[b0 + i] - offsets[b0];
+        uint64_t *doff = (uint64_t *)ws.get(WS_OFF, (size_t)(nb + 1) * 8, s);
+        if (!doff) {
+            rc = NBKD_ENOMEM;
+            break;
+        }
+        NBKD_HIP(hipMemcpyAsync(doff, rel.data(), (size_t)(nb + 1) * 8, hipMemcpyHostToDevice, s));
+        uint32_t *di = out_idx + offsets[b0];
+        if (!out_dev) {
+            // device slot b is free once batch i-2's ids left it
+            if (out_rec[b]) NBKD_HIP(hipStreamWaitEvent(s, ev_out[b], 0));
+            di = (uint32_t *)ws.get(b == 0 ? WS_IDX : WS_HO11, std::max<uint64_t>(nnz, 1) * 4, s);
+            if (!di) {
+                rc = NBKD_ENOMEM;
+                break;
+            }
+        }
+        if (nnz) {
+            rc = ball_fill_batch(t, ws, dq, nb, r, doff, di, s);
+            if (rc) break;
+            if (flags & NBKD_SORTED) {
+                rc = sort_csr_batch(ws, doff, di, nb, rel.data(), s);
+                if (rc) break;
+            }
+        }
+        // the host copy of batch i-1 (its D2H overlapped this batch's fill)
+        rc = drain_prev();
+        if (rc) break;
+        if (!out_dev && nnz) {
+            NBKD_HIP(hipEventRecord(ev_comp[b], s));
+            NBKD_HIP(hipStreamWaitEvent(cp, ev_comp[b], 0));
+            // pinned slot b (kept by the workspace); refused pinning, or a
+            // batch of one row longer than the slot: straight to the caller
+            hp[b] = nullptr;
+            if (!pageable && nnz <= CSR_BATCH_IDS) {
+                hp[b] = (char *)ws.host_pinned(b, CSR_BATCH_IDS * 4);
+                if (!hp[b]) pageable = true;
+            }
+            if (hp[b]) {
+                NBKD_HIP(hipMemcpyAsync(hp[b], di, nnz * 4, hipMemcpyDeviceToHost, cp));
+                NBKD_HIP(hipEventRecord(ev_out[b], cp));
+                out_rec[b] = true;
+                prev_slot = b;
+                prev_b0 = b0;
+                prev_nnz = nnz;
+            } else {
+                NBKD_HIP(hipMemcpyAsync(out_idx + offsets[b0], di, nnz * 4, hipMemcpyDeviceToHost, cp));
+                NBKD_HIP(hipEventRecord(ev_out[b], cp));
+                out_rec[b] = true;
+                NBKD_HIP(hipEventSynchronize(ev_out[b]));
+            }
+        }
+    }
+    if (rc) {
+        (void)hipStreamSynchronize(s);
+        (void)hipStreamSynchronize(cp);
+        return rc;
+    }
+    rc = drain_prev();
+    if (rc) return rc;
+    NBKD_HIP(hipStreamSynchronize(s));
+    NBKD_HIP(hipStreamSynchronize(cp));
+    return NBKD_OK;
 }
 
 } // namespace nbkd

@@ -88,8 +88,9 @@ class KDTree(cKDTree):
 
         return_length=True -> uint32 counts, shape points.shape[:-1].
         return_csr=True -> (offsets uint64 (M + 1,), indices uint32): row i is
-        indices[offsets[i]:offsets[i + 1]] (each row sorted unless
-        return_sorted=False); no per-row Python objects, for large batches.
+        indices[offsets[i]:offsets[i + 1]] (each row sorted on the device
+        unless return_sorted=False); no per-row Python work, any M (the call
+        streams in batches).
         Otherwise an object array of uint32 index arrays (sorted ascending
         unless return_sorted=False), like scipy's query_ball_point.
         """
@@ -99,17 +100,16 @@ class KDTree(cKDTree):
         out_shape = tuple(shape[:-1]) if shape is not None else (np.asarray(points).shape[0],)
         if return_length:
             return super().query_ball_count(points, float(r)).reshape(out_shape)
-        off, idx = super().query_ball_csr(points, float(r))
-        m = len(off) - 1
+        # rows sorted on the device (NBKD_SORTED), both passes streamed in batches
+        off, idx = super().query_ball_csr(points, float(r), bool(return_sorted))
         if return_csr:
-            if return_sorted:
-                for i in range(m):  # in place, row by row (cache-resident rows)
-                    idx[off[i]:off[i + 1]].sort()
             return off, idx
+        # scipy's object-array form: one array view per row (the rows
+        # themselves are already sorted)
+        m = len(off) - 1
         rows = np.empty(m, dtype=object)
-        for i in range(m):
-            row = idx[off[i]:off[i + 1]]
-            rows[i] = np.sort(row) if return_sorted else row
+        for i, row in enumerate(np.split(idx, off[1:-1].astype(np.int64)) if m else ()):
+            rows[i] = row
         return rows.reshape(out_shape)
 
     def kth_distance(self, points: np.ndarray, k: int):
