@@ -185,9 +185,23 @@ constexpr int BALL_NST = 13;
 // transposed steps and the per-lane loop -- stays what it was.  The packet's
 // balls cover a region only ~1.3x the volume of a 64-query packet's, so far
 // fewer than twice the nodes and leaves are visited.
+// NBKD_BALL_PAIRS (round 6; 0 = round 5's loop, A/B): a leaf's partial
+// queries of both sets are compacted into pair-interleaved records, so the
+// transposed loop runs over a uniform counter, two queries a step whose
+// coordinates load as packed pairs, and writes counts into lane (rank) of two
+// registers that one ds_bpermute per set maps back
+#ifndef NBKD_BALL_PAIRS
+#define NBKD_BALL_PAIRS 1
+#endif
+
 struct alignas(16) BallLds2 {
     float4 p4[CHUNK]; // the staged points
+#if NBKD_BALL_PAIRS
+    // the partial queries by rank r: record r / 2 = {x[2], y[2], z[2], -, -}
+    float pq[64 * 8];
+#else
     float4 qs[128];   // the packet's query coordinates (A at lane, B at 64 + lane)
+#endif
 };
 
 // one internal node with split axis D for both query sets (NBKD_GSTEP's logic)
@@ -315,6 +329,41 @@ __device__ __forceinline__ uint32_t ball_tcount(uint64_t rem, const float4 *qs, 
     return tc;
 }
 
+#if NBKD_BALL_PAIRS
+// two v_writelane_b32 (lane selects in M0: one SGPR operand per VALU
+// instruction), values and lanes written by SALU
+__device__ __forceinline__ uint32_t write_lanes2(uint32_t old, int v0, int l0, int v1, int l1) {
+    asm volatile("s_mov_b32 m0, %2\n\ts_nop 1\n\tv_writelane_b32 %0, %1, m0\n\t"
+                 "s_mov_b32 m0, %4\n\ts_nop 1\n\tv_writelane_b32 %0, %3, m0"
+                 : "+v"(old) : "s"(v0), "s"(l0), "s"(v1), "s"(l1) : "m0");
+    return old;
+}
+
+// the partial queries of ranks [i0, i1) (pair-interleaved records in pq,
+// compacted by rank; i0 even, i1 - i0 <= 64) against the staged points (lanes
+// past the chunk hold FLT_MAX): two queries a step; the count of rank r lands
+// in lane r - i0 of the result
+template <bool M>
+__device__ __forceinline__ uint32_t ball_tcount_pairs(uint32_t i0, uint32_t i1, const float *pq,
+                                                      float ux, float uy, float uz, float r2,
+                                                      float L) {
+    uint32_t tc = 0;
+#pragma unroll 1
+    for (uint32_t i = i0; i < i1; i += 2) {
+        const float4 xy = *reinterpret_cast<const float4 *>(pq + 4 * i); // x0 x1 y0 y1
+        const float2 zz = *reinterpret_cast<const float2 *>(pq + 4 * i + 4);
+        const float d0 = point_d2_fast<M>(xy.x, xy.z, zz.x, ux, uy, uz, L);
+        const float d1 = point_d2_fast<M>(xy.y, xy.w, zz.y, ux, uy, uz, L);
+        const int c0 = __popcll(__ballot(d0 <= r2));
+        const int c1 = __popcll(__ballot(d1 <= r2));
+        // (uniform; readfirstlane keeps the compiler from a VGPR copy of i)
+        const int iu = __builtin_amdgcn_readfirstlane((int)(i - i0));
+        tc = write_lanes2(tc, c0, iu, c1, iu + 1);
+    }
+    return tc;
+}
+#endif
+
 template <bool PER, bool M, bool STATS>
 __device__ __forceinline__ void ball_walk2(const DevTree &t, const uint32_t *__restrict__ linfo,
                                            float r2, const PadLeaves &pad, uint32_t tnum,
@@ -379,11 +428,15 @@ __device__ __forceinline__ void ball_walk2(const DevTree &t, const uint32_t *__r
         }
         NBKD_BPH(1);
         if ((pmA | pmB) == 0) continue;
-        const uint32_t np = (uint32_t)(__popcll(pmA) + __popcll(pmB));
+        const uint32_t nA = (uint32_t)__popcll(pmA);
+        const uint32_t np = nA + (uint32_t)__popcll(pmB);
         // the plain d2 where no partial query wraps around (wrap_free)
         const bool plain_leaf =
             !M || (plain_ok && __all((!partA || wrap_free(ax, ay, az, tb, L)) &&
                                      (!partB || wrap_free(bx_, by, bz, tb, L))));
+#if NBKD_BALL_PAIRS
+        bool pq_written = false;
+#endif
         for (uint32_t c0 = lpos; c0 < lend; c0 += CHUNK) {
             const uint32_t cn = min((uint32_t)CHUNK, lend - c0);
             wave_sync();
@@ -397,6 +450,40 @@ __device__ __forceinline__ void ball_walk2(const DevTree &t, const uint32_t *__r
                 const float4 pl = W.p4[lane];
                 const float ux = pv ? pl.x : FLT_MAX, uy = pv ? pl.y : FLT_MAX,
                             uz = pv ? pl.z : FLT_MAX;
+#if NBKD_BALL_PAIRS
+                // each partial query's rank: set A first, then set B
+                if (!pq_written) { // once per leaf: the partial queries by rank
+                    pq_written = true;
+                    if (partA) {
+                        const uint32_t r = mbcnt64(pmA);
+                        float *r_ = W.pq + 8 * (r >> 1) + (r & 1);
+                        r_[0] = ax;
+                        r_[2] = ay;
+                        r_[4] = az;
+                    }
+                    if (partB) {
+                        const uint32_t r = nA + mbcnt64(pmB);
+                        float *r_ = W.pq + 8 * (r >> 1) + (r & 1);
+                        r_[0] = bx_;
+                        r_[2] = by;
+                        r_[4] = bz;
+                    }
+                    wave_sync();
+                }
+                // ranks 0..63 (all of A's), then 64..127; each batch's counts
+                // go back to their queries by one ds_bpermute per set
+                for (uint32_t i0 = 0; i0 < np; i0 += 64) {
+                    const uint32_t i1 = min(np, i0 + 64u);
+                    const uint32_t tc = plain_leaf
+                                            ? ball_tcount_pairs<false>(i0, i1, W.pq, ux, uy, uz, r2, L)
+                                            : ball_tcount_pairs<M>(i0, i1, W.pq, ux, uy, uz, r2, L);
+                    const uint32_t rA = mbcnt64(pmA) - i0, rB = nA + mbcnt64(pmB) - i0;
+                    const uint32_t cA = (uint32_t)__shfl((int)tc, (int)(rA & 63u), 64);
+                    const uint32_t cB = (uint32_t)__shfl((int)tc, (int)(rB & 63u), 64);
+                    if (partA && rA < 64u) cntA += cA;
+                    if (partB && rB < 64u) cntB += cB;
+                }
+#else
                 if (plain_leaf) {
                     cntA += ball_tcount<false>(pmA, W.qs, ux, uy, uz, r2, L);
                     cntB += ball_tcount<false>(pmB, W.qs + 64, ux, uy, uz, r2, L);
@@ -404,6 +491,7 @@ __device__ __forceinline__ void ball_walk2(const DevTree &t, const uint32_t *__r
                     cntA += ball_tcount<M>(pmA, W.qs, ux, uy, uz, r2, L);
                     cntB += ball_tcount<M>(pmB, W.qs + 64, ux, uy, uz, r2, L);
                 }
+#endif
                 if constexpr (STATS) {
                     bst[3] += np;
                     bst[1] += np * cn;
@@ -454,8 +542,10 @@ ball_count2_kernel(DevTree t, const uint32_t *__restrict__ linfo, const float *_
     const bool inb = !PER || (bx_ >= 0.0f && bx_ <= L && by >= 0.0f && by <= L && bz >= 0.0f && bz <= L);
     const bool acta = va && ina, actb = vb && inb;
     const float thrA = acta ? r2 : -INFINITY, thrB = actb ? r2 : -INFINITY;
+#if !NBKD_BALL_PAIRS
     W.qs[lane] = make_float4(ax, ay, az, 0.0f);
     W.qs[64 + lane] = make_float4(bx_, by, bz, 0.0f);
+#endif
     bool plain = false;
     if constexpr (PER) {
         const float r1 = sqrtf(fmaxf(r2, 0.0f)) * 1.01f + L * 1e-6f;

@@ -39,6 +39,30 @@ using namespace dev;
 constexpr int TB = 256;
 constexpr int WPB = TB / 64;
 
+// Round-6 scan / column variants (A/B: scripts/build_flags.sh <name> "-DX=0"):
+//   NBKD_COL_ROWMAJOR  a query's candidate column contiguous (slot s of query
+//                      row r at r * capg + s) in every pass; before, the first
+//                      pass's columns were blocked (16-slot blocks of 64 rows),
+//                      whose store address took 5 VALU per hit instead of 2
+//   NBKD_PAIR_PAD      the pair list padded to whole scan steps with pairs of a
+//                      never-hitting slot (bound -inf): no per-step range test
+//   NBKD_PAIR_ATOMIC   one returning LDS atomic per (pair, owner) instead of
+//                      one per hit (VERDICT r05 #1a): collect 40.89 -> 38.07 ms
+//                      per 1e8 queries, same rows (profiles/r06b_scan_ab.txt;
+//                      the two variants above alone: 40.54)
+#ifndef NBKD_COL_ROWMAJOR
+#define NBKD_COL_ROWMAJOR 1
+#endif
+#ifndef NBKD_PAIR_PAD
+#define NBKD_PAIR_PAD 1
+#endif
+#ifndef NBKD_PAIR_ATOMIC
+#define NBKD_PAIR_ATOMIC 1
+#endif
+#ifndef NBKD_PAIR_PREFETCH
+#define NBKD_PAIR_PREFETCH 0 // (with NBKD_PAIR_PAD) the next step's pair entry read one step early
+#endif
+
 constexpr int NB = 16; // distance buckets of the bound histogram
 
 // Bound tightening without a top-k: the seed ball [0, S) is cut into NB
@@ -90,15 +114,21 @@ __device__ __forceinline__ uint32_t d2_bucket(float d, float c) {
 constexpr int GCHUNK = 64; // points staged per step (a multiple of NBKD_GROUP)
 constexpr int GMAX = GCHUNK / NBKD_GROUP;
 
+// pair entries: slot | owner lane << PR_OWNER | group << PR_G (16 bits); with
+// NBKD_PAIR_PAD slot 64 is the padding pairs' query (bound -inf, never a hit)
+constexpr uint32_t PR_OWNER = NBKD_PAIR_PAD ? 7 : 6, PR_G = NBKD_PAIR_PAD ? 13 : 12;
+constexpr uint32_t PR_SLOT = (1u << PR_OWNER) - 1u;
+constexpr uint32_t PAIR_DUMMY = 64u;
+
 struct CollectLdsG {
-    float4 sq[64]; // per lane: query xyz + bound
+    float4 sq[64 + NBKD_PAIR_PAD]; // per lane: query xyz + bound (+ the padding pairs' query)
     float scl[64]; // per lane: bucket factor (d2_bucket)
     uint32_t cnt[64];
     uint32_t hist[NB / 4][65];  // padded rows: one lane's 4 words sit in 4 banks
     float4 p4[GCHUNK];           // the staged points: x, y, z, original id bits
     float gb[6 * GMAX];          // the chunk's group boxes (lo.x, hi.x, lo.y, hi.y, lo.z, hi.z)
     float tb[8];                 // the leaf's tight box (leafinfo words 0..5)
-    uint16_t pairs[64 * GMAX];   // (slot, lane, group) pairs: slot | lane << 6 | group << 12
+    uint16_t pairs[64 * GMAX];   // (slot, lane, group) pairs: slot | lane << PR_OWNER | group << PR_G
     uint8_t slot[64];            // lanes needing the leaf, compacted
 };
 
@@ -250,9 +280,16 @@ __device__ __forceinline__ void grp_packet(const DevTree &t, const float *__rest
                     }
                     const uint64_t hm = __ballot(hit);
                     if (hit)
-                        W.pairs[np + mbcnt64(hm)] = (uint16_t)(sl | (owner << 6) | (g << 12));
+                        W.pairs[np + mbcnt64(hm)] = (uint16_t)(sl | (owner << PR_OWNER) | (g << PR_G));
                     np += (uint32_t)__popcll(hm);
                 }
+                if constexpr (STATS) st[5] += np * NBKD_GROUP; // (pair, point) evaluations
+#if NBKD_PAIR_PAD
+                // whole scan steps: the last one's missing pairs never hit
+                const uint32_t npp = (np + 7u) & ~7u;
+                if ((uint32_t)lane < npp - np) W.pairs[np + lane] = (uint16_t)PAIR_DUMMY;
+                np = npp;
+#endif
                 NBKD_PH(2);
                 wave_sync();
                 // Tried and dropped (r04s): the hit's column slot as the owner's
@@ -263,22 +300,60 @@ __device__ __forceinline__ void grp_packet(const DevTree &t, const float *__rest
                 // arithmetic costs more issue than the atomics' waits.
                 // each pair's 8 points spread over 8 consecutive lanes
                 const uint32_t ntrip = np * NBKD_GROUP;
-                if constexpr (STATS) st[5] += ntrip;
+#if NBKD_PAIR_PAD && NBKD_PAIR_PREFETCH
+                // the next step's pair entry is read while this step computes
+                uint32_t pr_next = ntrip ? W.pairs[(uint32_t)lane >> 3] : 0u;
+#endif
 #pragma unroll 1
                 for (uint32_t t0 = 0; t0 < ntrip; t0 += 64) {
                     if constexpr (STATS) ++st[4];
+#if NBKD_PAIR_PAD
+                    // every lane of every step holds a pair (padding pairs never hit)
+                    {
+#if NBKD_PAIR_PREFETCH
+                        const uint32_t pr = pr_next;
+                        if (t0 + 64 < ntrip) pr_next = W.pairs[((t0 + 64) >> 3) + ((uint32_t)lane >> 3)];
+#else
+                        const uint32_t pr = W.pairs[(t0 >> 3) + ((uint32_t)lane >> 3)];
+#endif
+                        const uint32_t pi = (pr >> PR_G) * NBKD_GROUP + ((uint32_t)lane & 7u);
+#else
                     const uint32_t ti = t0 + lane;
                     if (ti < ntrip) {
                         const uint32_t pr = W.pairs[ti / NBKD_GROUP];
-                        const uint32_t qs = pr & 63u, owner = (pr >> 6) & 63u;
-                        const uint32_t pi = (pr >> 12) * NBKD_GROUP + (ti % NBKD_GROUP);
+                        const uint32_t pi = (pr >> PR_G) * NBKD_GROUP + (ti % NBKD_GROUP);
+#endif
+                        const uint32_t qs = pr & PR_SLOT, owner = (pr >> PR_OWNER) & 63u;
                         const float4 qq = W.sq[qs];
                         const float4 pp = W.p4[pi];
                         const float d = point_d2_fast<M>(qq.x, qq.y, qq.z, pp.x, pp.y, pp.z, L);
+#if NBKD_PAIR_ATOMIC
+                        // the hits of a pair (8 consecutive lanes, one owner):
+                        // ranked by mbcnt inside the 8-lane group, one returning
+                        // atomic by the group's last lane, its base broadcast by
+                        // two DPP moves (quad broadcast of lane 3, half-row mirror)
+                        const bool hit = d < qq.w;
+                        const uint64_t hm = __ballot(hit);
+                        const uint32_t gbits = (uint32_t)(hm >> ((uint32_t)lane & ~7u)) & 0xFFu;
+                        const uint32_t rank = __popc(gbits & ((1u << ((uint32_t)lane & 7u)) - 1u));
+                        uint32_t base = 0;
+                        if (((uint32_t)lane & 7u) == 7u && gbits != 0u)
+                            base = atomicAdd(&W.cnt[owner], (uint32_t)__popc(gbits));
+                        // quad_perm [3,3,3,3]: lanes 0-3 of the group read lane 3, 4-7 lane 7;
+                        // row_half_mirror into banks 0 and 2 only: lanes 0-3 read 7-4
+                        base = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)base, 0xFF, 0xF, 0xF, false);
+                        base = (uint32_t)__builtin_amdgcn_update_dpp((int)base, (int)base, 0x141, 0xF, 0x5,
+                                                                     false);
+                        if (hit) {
+                            const uint32_t j = d2_bucket(d, W.scl[qs]);
+                            atomicAdd(&W.hist[j >> 2][owner], 1u << (8 * (j & 3)));
+                            const uint32_t sl = base + rank;
+#else
                         if (d < qq.w) {
                             const uint32_t j = d2_bucket(d, W.scl[qs]);
                             atomicAdd(&W.hist[j >> 2][owner], 1u << (8 * (j & 3)));
                             const uint32_t sl = atomicAdd(&W.cnt[owner], 1u);
+#endif
                             // a row past capg is a failure whose column is never read (both
                             // selects): its extra hits overwrite its last slot (no branch)
                             const uint32_t sw = min(sl, capg - 1u);
@@ -286,7 +361,11 @@ __device__ __forceinline__ void grp_packet(const DevTree &t, const float *__rest
                             // the selects write it without a gather
                             // a 32-bit byte offset from the packet's (SGPR) column base:
                             // one saddr store, no 64-bit address arithmetic per hit
+#if NBKD_COL_ROWMAJOR
+                            const uint32_t off = (__umul24(owner, capg) + sw) << 3;
+#else
                             const uint32_t off = (((__umul24(sw >> 4, qpp) + owner) << 4) | (sw & 15u)) << 3;
+#endif
                             *reinterpret_cast<uint2 *>(reinterpret_cast<char *>(col) + off) =
                                 make_uint2(__float_as_uint(d), __float_as_uint(pp.w));
                         }
@@ -364,6 +443,9 @@ __device__ __forceinline__ void collect_packet(
     const float nb_over_s = fin ? (float)NB / seed * 1.00000095367431640625f : 0.0f;
 #pragma unroll
     for (int w = 0; w < NB / 4; ++w) W.hist[w][lane] = 0u;
+#if NBKD_PAIR_PAD
+    if (lane == 0) W.sq[PAIR_DUMMY] = make_float4(0.0f, 0.0f, 0.0f, -INFINITY);
+#endif
     uint2 *const col = cand + (size_t)pk * qpp * capg;
     uint32_t cnt = 0;
     // per-packet work counters and phase clocks (STATS only): 32 bits each, so
@@ -470,18 +552,22 @@ __device__ __forceinline__ void mark_failure(float qx, float qy, float qz, float
 // LDS by direct loads, no VGPR staging: LDS piece x = i*64 + lane takes the
 // block's row r = x/8, piece (x%8) ^ (r%8), so row r's piece j sits at
 // r*8 + (j ^ (r & 7)) and the per-row reads are bank-conflict free.
-__device__ __forceinline__ void issue_block(const uint4 *b4, uint4 *lds4, int lane, uint64_t rows) {
+// row_stride4: uint4s between two rows' lines (8: blocked columns; capg / 2:
+// row-major columns, NBKD_COL_ROWMAJOR)
+__device__ __forceinline__ void issue_block(const uint4 *b4, uint4 *lds4, int lane, uint64_t rows,
+                                            uint32_t row_stride4) {
     // rows: bit r set = row r holds candidates in this block; the other rows'
     // 128-B lines are not read (their LDS slots keep stale data, masked by count)
     const uint32_t r0 = (uint32_t)lane >> 3, jj = (uint32_t)lane & 7u;
-    const uint4 *src = b4 + r0 * 8 + (jj ^ r0);
+    const uint4 *src = b4 + r0 * row_stride4 + (jj ^ r0);
     // bits r0, r0+8, .., r0+56 of rows -> bits 0..7 of m
     const uint32_t m = (uint32_t)((((rows >> r0) & 0x0101010101010101ull) * 0x0102040810204080ull) >> 56);
 #pragma unroll
     for (int i = 0; i < 8; ++i)
         if (m & (1u << i))
             // non-temporal (aux 2 = nt): each column line is read once
-            __builtin_amdgcn_global_load_lds((gas_ptr)(src + 64 * i), (las_ptr)(lds4 + 64 * i), 16, 0, 2);
+            __builtin_amdgcn_global_load_lds((gas_ptr)(src + (size_t)(8 * i) * row_stride4),
+                                             (las_ptr)(lds4 + 64 * i), 16, 0, 2);
 }
 
 // One lane per query: the k smallest of its candidate column, sorted, as rows.
@@ -548,7 +634,9 @@ select_block(const DevTree &t, const float *__restrict__ q, const uint32_t *__re
         cand + (whole ? (size_t)(gq >> 6) * 64u * capg : (size_t)gq * capg));
     uint4 *const lds4 = reinterpret_cast<uint4 *>(stage);
     // all_rows: read every row's line (A/B of the per-row masking)
-    if (whole && maxn > 0) issue_block(blk, lds4, lane, __ballot(nn > 0u) | all_rows);
+    // a block's rows: 128 B apart (blocked) or one column apart (row-major)
+    const uint32_t rs4 = NBKD_COL_ROWMAJOR ? capg / 2u : 8u, bs4 = NBKD_COL_ROWMAJOR ? 8u : 512u;
+    if (whole && maxn > 0) issue_block(blk, lds4, lane, __ballot(nn > 0u) | all_rows, rs4);
     for (uint32_t s0 = 0; s0 < maxn; s0 += NS) {
         float bd[NS];
         uint32_t bi[NS];
@@ -582,8 +670,8 @@ select_block(const DevTree &t, const float *__restrict__ q, const uint32_t *__re
             __builtin_amdgcn_s_waitcnt(0xC07F); // lgkmcnt(0)
             wave_sync();
             if (s0 + NS < maxn)
-                issue_block(blk + (size_t)((s0 + NS) >> 4) * 512u, lds4, lane,
-                            __ballot(nn > s0 + NS) | all_rows);
+                issue_block(blk + (size_t)((s0 + NS) >> 4) * bs4, lds4, lane,
+                            __ballot(nn > s0 + NS) | all_rows, rs4);
         }
         // a block with nothing below any lane's current k-th changes nothing
         bool useful = false;
@@ -795,27 +883,35 @@ knn_select_wave_kernel(DevTree t, const float *__restrict__ q, const uint32_t *_
     uint2 *const cl = cl_all[wave_id()];
     const uint32_t m = span_m(span);
     const uint32_t nwaves = gridDim.x * WPB;
-    // software pipeline: the next query's count, bound and first 2K slots are
-    // loaded before this query is sorted (their addresses depend on gq only;
-    // slots past the column are clamped to its last slot and masked by n)
+    // software pipeline, two deep: the next query's bound and first 2K slots
+    // are loaded before this query is sorted, and the count of the query after
+    // it one iteration earlier, so that only the slots below its count are
+    // read (until round 6 every slot up to 2K was read, clamped to the
+    // column's last one: at k = 100 ~1.7 KB per query for ~1 KB of candidates)
     auto slot_ptr = [&](uint32_t g, uint32_t sl) {
         const uint32_t c = min(sl, capg - 1u);
-        return WHOLE ? cand + (size_t)(g >> 6) * 64u * capg + ((c >> 4) * 64u + (g & 63u)) * 16u + (c & 15u)
-                     : cand + (size_t)g * capg + c;
+        return (WHOLE && !NBKD_COL_ROWMAJOR)
+                   ? cand + (size_t)(g >> 6) * 64u * capg + ((c >> 4) * 64u + (g & 63u)) * 16u + (c & 15u)
+                   : cand + (size_t)g * capg + c;
     };
     uint32_t gq = blockIdx.x * WPB + wave_id();
-    uint32_t n_nx = 0, qo_nx = 0;
+    uint32_t n_nx = gq < m ? ccount[gq] : 0u, qo_nx = 0;
+    uint32_t n_nn = gq + nwaves < m ? ccount[gq + nwaves] : 0u; // one query further
     float b_nx = INFINITY;
     uint2 e_nx[2 * R];
-    auto prefetch = [&](uint32_t g) {
+    auto prefetch = [&](uint32_t g, uint32_t ng) {
         if (g >= m) return;
-        n_nx = ccount[g];
         qo_nx = order[g];
         b_nx = kbound ? kbound[g] : INFINITY;
+        // a failed column (fewer than k, or past capg) is never sorted
+        const uint32_t lim = (ng >= (uint32_t)k && ng <= capg) ? ng : 0u;
 #pragma unroll
-        for (int j = 0; j < 2 * R; ++j) e_nx[j] = *slot_ptr(g, (uint32_t)(j * 64 + lane));
+        for (int j = 0; j < 2 * R; ++j) {
+            const uint32_t sl = (uint32_t)(j * 64 + lane);
+            e_nx[j] = sl < lim ? *slot_ptr(g, sl) : make_uint2(0x7F800000u, 0xFFFFFFFFu);
+        }
     };
-    prefetch(gq);
+    prefetch(gq, n_nx);
     uint32_t pend_q = 0xFFFFFFFFu; // the query whose ids are still to be stored
     uint32_t pend_i[R];
     for (; gq < m; gq += nwaves) {
@@ -825,7 +921,9 @@ knn_select_wave_kernel(DevTree t, const float *__restrict__ q, const uint32_t *_
         uint2 e[2 * R];
 #pragma unroll
         for (int j = 0; j < 2 * R; ++j) e[j] = e_nx[j];
-        prefetch(gq + nwaves);
+        n_nx = n_nn;
+        prefetch(gq + nwaves, n_nx);
+        n_nn = gq + 2 * nwaves < m ? ccount[gq + 2 * nwaves] : 0u;
         if (!(n >= (uint32_t)k && n <= capg)) {
             if (lane == 0) {
                 const float qx = q[3 * (size_t)qo], qy = q[3 * (size_t)qo + 1],
@@ -844,7 +942,8 @@ knn_select_wave_kernel(DevTree t, const float *__restrict__ q, const uint32_t *_
             }
             continue;
         }
-        const uint2 *col = WHOLE ? cand + (size_t)(gq >> 6) * 64u * capg : cand + (size_t)gq * capg;
+        constexpr bool BLOCKED = WHOLE && !NBKD_COL_ROWMAJOR;
+        const uint2 *col = BLOCKED ? cand + (size_t)(gq >> 6) * 64u * capg : cand + (size_t)gq * capg;
         const uint32_t row = gq & 63u;
         // at least k candidates lie strictly below the collect kernel's final
         // bound (bnd), so the k smallest are all below it
@@ -896,8 +995,8 @@ knn_select_wave_kernel(DevTree t, const float *__restrict__ q, const uint32_t *_
 #pragma unroll
                 for (int r = 0; r < R; ++r) {
                     const uint32_t sl = c0 + (uint32_t)(r * 64 + lane);
-                    const uint2 e = sl < n ? (WHOLE ? col[((sl >> 4) * 64u + row) * 16u + (sl & 15u)]
-                                                    : col[sl])
+                    const uint2 e = sl < n ? (BLOCKED ? col[((sl >> 4) * 64u + row) * 16u + (sl & 15u)]
+                                                      : col[sl])
                                            : make_uint2(0x7F800000u, 0xFFFFFFFFu);
                     const float d = __uint_as_float(e.x);
                     cd[r] = d < bnd ? d : INFINITY;
