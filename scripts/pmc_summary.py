@@ -1,5 +1,7 @@
-"""Per-kernel mean of every PMC counter in a rocprofv3 csv tree:
-    python scripts/pmc_summary.py gpurun_out/<tag> [kernel-substring]"""
+"""Per-kernel (name, grid) means of every PMC counter in a rocprofv3 csv tree,
+over its dispatches:
+    python scripts/pmc_summary.py gpurun_out/<tag> [kernel-substring] [dir-glob]
+(dir-glob default "pmc*", e.g. "ball_sq*" for the radius-count sets)."""
 import collections
 import csv
 import glob
@@ -7,13 +9,19 @@ import sys
 
 root = sys.argv[1]
 sub = sys.argv[2] if len(sys.argv) > 2 else ""
-for f in sorted(glob.glob(f"{root}/pmc*/run_counter_collection.csv")):
+pat = sys.argv[3] if len(sys.argv) > 3 else "pmc*"
+for f in sorted(glob.glob(f"{root}/{pat}/run_counter_collection.csv")):
     agg = collections.defaultdict(float)
+    disp = collections.defaultdict(set)
     for r in csv.DictReader(open(f)):
         if sub not in r["Kernel_Name"]:
             continue
-        agg[(r["Dispatch_Id"], r["Counter_Name"])] += float(r["Counter_Value"])
-    byc = collections.defaultdict(list)
-    for (_, c), v in agg.items():
-        byc[c].append(v)
-    print(f.split("/")[-2], {c: "%.4g" % (sum(v) / len(v)) for c, v in sorted(byc.items())})
+        key = (r["Kernel_Name"].replace("void nbkd::(anonymous namespace)::", "").split("(")[0],
+               r.get("Grid_Size", "?"))
+        agg[key + (r["Counter_Name"],)] += float(r["Counter_Value"])
+        disp[key].add(r["Dispatch_Id"])
+    rows = collections.defaultdict(dict)
+    for (k, g, c), v in agg.items():
+        rows[(k, g)][c] = "%.4g" % (v / len(disp[(k, g)]))
+    for (k, g), cs in sorted(rows.items()):
+        print(f.split("/")[-2], k, "grid", g, "dispatches", len(disp[(k, g)]), dict(sorted(cs.items())))
