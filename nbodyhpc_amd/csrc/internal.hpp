@@ -22,7 +22,7 @@ namespace nbkd {
 enum WsSlot {
     WS_Q = 0, WS_KEYS, WS_KEYS2, WS_ORDER, WS_TMP, WS_HIST, WS_SUMS, WS_OUTD, WS_OUTI,
     WS_COUNT, WS_OFF, WS_IDX, WS_STATS, WS_LIST, WS_LT, WS_TG, WS_CAND, WS_CCOUNT,
-    WS_LIST2, WS_RSORT, WS_KTHD, WS_KTHI, WS_KB, WS_ANCH,
+    WS_LIST2, WS_RSORT, WS_KTHD, WS_KTHI, WS_KB, WS_ANCH, WS_PAIR,
     // host-buffer pipeline (query.hip host_pipeline): two slots of queries and
     // of up to two result arrays
     WS_HQ0, WS_HQ1, WS_HO00, WS_HO01, WS_HO10, WS_HO11, WS_NSLOTS
@@ -360,7 +360,7 @@ nbkd_status launch_knn_collect(const Tree &t, const float *q, const uint32_t *or
                                uint32_t *fail_list, uint32_t *fail_count, uint32_t *fail_bits,
                                uint32_t pos_base, bool retry, bool fix_seed, bool sq, float *kb,
                                unsigned long long *stats, hipStream_t s,
-                               float *kth_side = nullptr);
+                               float *kth_side = nullptr, uint32_t *pair_scratch = nullptr);
 
 // the same pass as its two halves
 nbkd_status launch_collect_pass(const Tree &t, const float *q, const uint32_t *order, QSpan span,
@@ -372,7 +372,10 @@ nbkd_status launch_select_pass(const Tree &t, const float *q, const uint32_t *or
                                uint32_t capg, const uint32_t *ccount, float *od, uint32_t *oi,
                                uint32_t *fail_list, uint32_t *fail_count, uint32_t *fail_bits,
                                uint32_t pos_base, bool retry, bool fix_seed, bool sq, float *kb,
-                               hipStream_t s, float *kth_side = nullptr);
+                               hipStream_t s, float *kth_side = nullptr,
+                               uint32_t *pair_scratch = nullptr);
+// pair_scratch (64 < k <= 128, first pass): m + 16 words; the wave select then
+// runs two queries per wave where it can (knn_select_wave_pair_kernel)
 
 // ball.hip: radius count (out_idx == nullptr) or CSR fill over m kd-ordered
 // queries (periodic queries outside [0, L]^3 are skipped: query.hip answers them)

@@ -59,6 +59,9 @@ constexpr int WPB = TB / 64;
 #ifndef NBKD_PAIR_ATOMIC
 #define NBKD_PAIR_ATOMIC 1
 #endif
+#ifndef NBKD_WAVE_PAIR
+#define NBKD_WAVE_PAIR 4 // 64 < k <= 128: queries per wave in the first pass's wave select (0: one)
+#endif
 #ifndef NBKD_PAIR_PREFETCH
 #define NBKD_PAIR_PREFETCH 0 // (with NBKD_PAIR_PAD) the next step's pair entry read one step early
 #endif
@@ -867,6 +870,107 @@ __device__ __forceinline__ void wave_sort_stages(float (&d)[R], uint32_t (&p)[R]
     if constexpr (SIZE < 64 * R) wave_sort_stages<R, SIZE * 2, DESC>(d, p, lane);
 }
 
+// the bitonic sort stages of sizes SIZE..MAXSIZE only: with MAXSIZE < 64 R the
+// register blocks of MAXSIZE elements are sorted independently, alternately
+// ascending and descending
+template <int R, int SIZE, int MAXSIZE, bool DESC>
+__device__ __forceinline__ void wave_sort_upto(float (&d)[R], uint32_t (&p)[R], int lane) {
+    wave_merge_stages<R, SIZE, SIZE / 2, DESC>(d, p, lane);
+    if constexpr (SIZE < MAXSIZE) wave_sort_upto<R, SIZE * 2, MAXSIZE, DESC>(d, p, lane);
+}
+
+// 64 < k <= 128, a first pass (round 6): TWO queries per wave, sorted in one
+// network of four registers (positions p and p + 1 of the pass: registers 0-1
+// hold the first, ascending; 2-3 the second, descending), so every stage has
+// two independent exchange chains.  The one-query wave select issues each
+// stage's DPP exchange, ballot compare, scalar mask logic and select as one
+// dependent chain; its counters at k = 100 (profiles/r06f_pmc_select_wave.txt)
+// show more issue-stall than issuing cycles.  Only the common case runs here:
+// both columns complete (k <= n <= capg, n <= 256) and at most 128 candidates
+// below the collect kernel's final bound; any other position of the pair is
+// appended to `leftover` for the one-query kernel (pos_list), which also
+// marks the failures.
+template <bool PER, int NQ>
+__global__ void __launch_bounds__(TB)
+knn_select_wave_pair_kernel(const uint32_t *__restrict__ order, QSpan span, int k,
+                            const uint2 *__restrict__ cand, uint32_t capg,
+                            const uint32_t *__restrict__ ccount, float *__restrict__ out_d,
+                            uint32_t *__restrict__ out_i, bool sq,
+                            const float *__restrict__ kbound, uint32_t *__restrict__ leftover,
+                            uint32_t *__restrict__ nleft) {
+    constexpr int K = 128, NS = 2 * K; // sorted per query; slots read per query
+    constexpr int RR = 2 * NQ;         // registers: query j in 2j, 2j + 1
+    __shared__ uint2 cl_all[WPB][NQ][K];
+    const int lane = threadIdx.x & 63;
+    const int w = wave_id();
+    const uint32_t m = span_m(span);
+    const uint32_t ngroups = (m + NQ - 1) / NQ;
+    for (uint32_t gi = blockIdx.x * WPB + w; gi < ngroups; gi += gridDim.x * WPB) {
+        float td[RR];
+        uint32_t tp[RR];
+        bool fast[NQ];
+        uint32_t qo[NQ];
+        bool any = false;
+#pragma unroll
+        for (int s2 = 0; s2 < NQ; ++s2) {
+            const uint32_t g = NQ * gi + s2;
+            const bool valid = g < m;
+            const uint32_t n = valid ? ccount[g] : 0u;
+            const bool ok = valid && n >= (uint32_t)k && n <= capg && n <= (uint32_t)NS;
+            qo[s2] = valid ? order[g] : 0u;
+            const float bnd = (valid && kbound) ? kbound[g] : INFINITY;
+            const uint2 *col = cand + (size_t)g * capg;
+            uint2 e[NS / 64];
+#pragma unroll
+            for (int j = 0; j < NS / 64; ++j) {
+                const uint32_t sl = (uint32_t)(j * 64 + lane);
+                e[j] = (ok && sl < n) ? col[sl] : make_uint2(0x7F800000u, 0xFFFFFFFFu);
+            }
+            uint32_t c = 0;
+#pragma unroll
+            for (int j = 0; j < NS / 64; ++j) {
+                const bool v = __uint_as_float(e[j].x) < bnd;
+                const uint64_t bal = __ballot(v);
+                const uint32_t at = c + mbcnt64(bal);
+                if (v && at < (uint32_t)K) cl_all[w][s2][at] = e[j];
+                c += (uint32_t)__popcll(bal);
+            }
+            fast[s2] = ok && c <= (uint32_t)K;
+            any |= fast[s2];
+            if (valid && !fast[s2] && lane == 0) leftover[atomicAdd(nleft, 1u)] = g;
+            // the entries past the compacted ones read as +inf
+            if ((uint32_t)lane >= c) cl_all[w][s2][lane] = make_uint2(0x7F800000u, 0xFFFFFFFFu);
+            if ((uint32_t)(lane + 64) >= c)
+                cl_all[w][s2][lane + 64] = make_uint2(0x7F800000u, 0xFFFFFFFFu);
+        }
+        if (!any) continue;
+        wave_sync();
+#pragma unroll
+        for (int r = 0; r < RR; ++r) {
+            const uint2 v = cl_all[w][r >> 1][(r & 1) * 64 + lane];
+            td[r] = __uint_as_float(v.x);
+            tp[r] = v.y;
+        }
+        // one network for all NQ queries: blocks of 128 alternately ascending
+        // and descending
+        wave_sort_upto<RR, 2, K, false>(td, tp, lane);
+        wave_sync(); // the LDS reads are done before the next group's writes
+#pragma unroll
+        for (int r = 0; r < RR; ++r) {
+            const int s2 = r >> 1, rr = (r & 1) * 64 + lane;
+            const int e = (s2 & 1) == 0 ? rr : 127 - rr; // odd blocks descending
+            if (!fast[s2] || e >= k) continue;
+            const float dv = sq ? td[r] : sqrtf(td[r]);
+            if (out_i == nullptr) { // k-th distance only
+                if (e == k - 1) out_d[qo[s2]] = dv;
+                continue;
+            }
+            out_d[(size_t)qo[s2] * k + e] = dv;
+            out_i[(size_t)qo[s2] * k + e] = tp[r];
+        }
+    }
+}
+
 template <int R, bool PER, bool WHOLE>
 __global__ void __launch_bounds__(TB)
 knn_select_wave_kernel(DevTree t, const float *__restrict__ q, const uint32_t *__restrict__ order,
@@ -875,13 +979,17 @@ knn_select_wave_kernel(DevTree t, const float *__restrict__ q, const uint32_t *_
                        uint32_t *__restrict__ out_i, uint32_t *__restrict__ fail_list,
                        uint32_t *__restrict__ fail_count, uint32_t pos_base,
                        float *__restrict__ tg_fix, float mu, bool sq,
-                       const float *__restrict__ kbound, uint32_t *__restrict__ fail_bits) {
+                       const float *__restrict__ kbound, uint32_t *__restrict__ fail_bits,
+                       const uint32_t *__restrict__ pos_list) {
     constexpr int K = 64 * R;
     // per wave: the query's candidates below its final bound, compacted
     __shared__ uint2 cl_all[WPB][2 * K];
     const int lane = threadIdx.x & 63;
     uint2 *const cl = cl_all[wave_id()];
     const uint32_t m = span_m(span);
+    // pos_list (the pair kernel's leftovers): entry i of this pass is the
+    // pass position pos_list[i]; else entry i is position i
+    auto pos = [&](uint32_t i) { return pos_list ? pos_list[i] : i; };
     const uint32_t nwaves = gridDim.x * WPB;
     // software pipeline, two deep: the next query's bound and first 2K slots
     // are loaded before this query is sorted, and the count of the query after
@@ -895,12 +1003,13 @@ knn_select_wave_kernel(DevTree t, const float *__restrict__ q, const uint32_t *_
                    : cand + (size_t)g * capg + c;
     };
     uint32_t gq = blockIdx.x * WPB + wave_id();
-    uint32_t n_nx = gq < m ? ccount[gq] : 0u, qo_nx = 0;
-    uint32_t n_nn = gq + nwaves < m ? ccount[gq + nwaves] : 0u; // one query further
+    uint32_t n_nx = gq < m ? ccount[pos(gq)] : 0u, qo_nx = 0;
+    uint32_t n_nn = gq + nwaves < m ? ccount[pos(gq + nwaves)] : 0u; // one query further
     float b_nx = INFINITY;
     uint2 e_nx[2 * R];
-    auto prefetch = [&](uint32_t g, uint32_t ng) {
-        if (g >= m) return;
+    auto prefetch = [&](uint32_t gi, uint32_t ng) {
+        if (gi >= m) return;
+        const uint32_t g = pos(gi);
         qo_nx = order[g];
         b_nx = kbound ? kbound[g] : INFINITY;
         // a failed column (fewer than k, or past capg) is never sorted
@@ -923,12 +1032,13 @@ knn_select_wave_kernel(DevTree t, const float *__restrict__ q, const uint32_t *_
         for (int j = 0; j < 2 * R; ++j) e[j] = e_nx[j];
         n_nx = n_nn;
         prefetch(gq + nwaves, n_nx);
-        n_nn = gq + 2 * nwaves < m ? ccount[gq + 2 * nwaves] : 0u;
+        n_nn = gq + 2 * nwaves < m ? ccount[pos(gq + 2 * nwaves)] : 0u;
+        const uint32_t gp = pos(gq); // this query's position in the pass
         if (!(n >= (uint32_t)k && n <= capg)) {
             if (lane == 0) {
                 const float qx = q[3 * (size_t)qo], qy = q[3 * (size_t)qo + 1],
                             qz = q[3 * (size_t)qo + 2];
-                mark_failure<PER>(qx, qy, qz, t.box, pos_base == 0xFFFFFFFFu ? qo : pos_base + gq,
+                mark_failure<PER>(qx, qy, qz, t.box, pos_base == 0xFFFFFFFFu ? qo : pos_base + gp,
                                   fail_list, fail_count, fail_bits);
                 if (tg_fix) { // the retry's seed, as knn_select_kernel
                     float fv;
@@ -936,15 +1046,15 @@ knn_select_wave_kernel(DevTree t, const float *__restrict__ q, const uint32_t *_
                         fv = fminf(8.0f, fmaxf(2.0f, 1.5f * mu / fmaxf((float)n, 0.5f)));
                     else
                         fv = fminf(1.0f, 4.0f * (float)capg / (float)n);
-                    const uint32_t ti = span.tg_pos ? gq : qo;
+                    const uint32_t ti = span.tg_pos ? gp : qo;
                     tg_fix[ti] = fminf(tg_fix[ti] * cbrtf(fv * fv), FLT_MAX);
                 }
             }
             continue;
         }
         constexpr bool BLOCKED = WHOLE && !NBKD_COL_ROWMAJOR;
-        const uint2 *col = BLOCKED ? cand + (size_t)(gq >> 6) * 64u * capg : cand + (size_t)gq * capg;
-        const uint32_t row = gq & 63u;
+        const uint2 *col = BLOCKED ? cand + (size_t)(gp >> 6) * 64u * capg : cand + (size_t)gp * capg;
+        const uint32_t row = gp & 63u;
         // at least k candidates lie strictly below the collect kernel's final
         // bound (bnd), so the k smallest are all below it
         float td[R], cd[R];
@@ -1138,14 +1248,42 @@ void launch_select_wave(const Tree &t, const float *q, const uint32_t *order, QS
                         uint32_t qpp, const uint2 *cand, uint32_t capg, const uint32_t *ccount,
                         float *od, uint32_t *oi, uint32_t *fail_list, uint32_t *fail_count,
                         uint32_t *fail_bits, uint32_t pos_base, float *tg_fix, float mu, bool sq,
-                        const float *kbound, hipStream_t s) {
+                        const float *kbound, hipStream_t s, uint32_t *pair_scratch) {
+    const uint32_t *pos_list = nullptr;
+    if constexpr (R == 2 && NBKD_COL_ROWMAJOR && NBKD_WAVE_PAIR > 0) {
+        if (pair_scratch && !span.count && kbound) {
+            // two queries per wave for the common case; the rest (failures, long
+            // columns, more than 128 below the bound) by the one-query kernel
+            uint32_t *nleft = pair_scratch + ((size_t)span.m + 15) / 16 * 16;
+            if (hipMemsetAsync(nleft, 0, 4, s) != hipSuccess) goto one_query; // every query below
+            {
+            constexpr int NQ = NBKD_WAVE_PAIR;
+            const unsigned pblocks = (unsigned)std::min<uint64_t>(
+                (((uint64_t)span.m + NQ - 1) / NQ + WPB - 1) / WPB, 32768u);
+            if (t.periodic)
+                knn_select_wave_pair_kernel<true, NQ><<<pblocks, TB, 0, s>>>(
+                    order, span, k, cand, capg, ccount, od, oi, sq, kbound, pair_scratch, nleft);
+            else
+                knn_select_wave_pair_kernel<false, NQ><<<pblocks, TB, 0, s>>>(
+                    order, span, k, cand, capg, ccount, od, oi, sq, kbound, pair_scratch, nleft);
+            QSpan lsp = span;
+            lsp.count = nleft;
+            lsp.base = 0;
+            lsp.mode = 0;
+            lsp.capped = true;
+            span = lsp;
+            pos_list = pair_scratch;
+            }
+        }
+    }
+one_query:
     const unsigned blocks = (unsigned)std::min<uint64_t>(((uint64_t)span.m + WPB - 1) / WPB,
                                                          span.count ? resident_blocks() : 32768u);
 #define NBKD_SELW(PER, WH)                                                                         \
     knn_select_wave_kernel<R, PER, WH><<<blocks, TB, 0, s>>>(view(t), q, order, span, k, cand,     \
                                                             capg, ccount, od, oi, fail_list,       \
                                                             fail_count, pos_base, tg_fix, mu, sq,  \
-                                                            kbound, fail_bits)
+                                                            kbound, fail_bits, pos_list)
     if (t.periodic) {
         if (qpp == 64) NBKD_SELW(true, true); else NBKD_SELW(true, false);
     } else {
@@ -1217,13 +1355,14 @@ nbkd_status launch_knn_collect(const Tree &t, const float *q, const uint32_t *or
                                uint32_t capg, uint32_t *ccount, float *od, uint32_t *oi,
                                uint32_t *fail_list, uint32_t *fail_count, uint32_t *fail_bits,
                                uint32_t pos_base, bool retry, bool fix_seed, bool sq, float *kb,
-                               unsigned long long *stats, hipStream_t s, float *kth_side) {
+                               unsigned long long *stats, hipStream_t s, float *kth_side,
+                               uint32_t *pair_scratch) {
     nbkd_status rc = launch_collect_pass(t, q, order, span, k, tg, seed_mul, qpp, cand, capg,
                                          ccount, retry, kb, stats, s);
     if (rc) return rc;
     return launch_select_pass(t, q, order, span, k, tg, qpp, cand, capg, ccount, od, oi,
                               fail_list, fail_count, fail_bits, pos_base, retry, fix_seed, sq, kb,
-                              s, kth_side);
+                              s, kth_side, pair_scratch);
 }
 
 nbkd_status launch_collect_pass(const Tree &t, const float *q, const uint32_t *order, QSpan span,
@@ -1248,7 +1387,7 @@ nbkd_status launch_select_pass(const Tree &t, const float *q, const uint32_t *or
                                uint32_t capg, const uint32_t *ccount, float *od, uint32_t *oi,
                                uint32_t *fail_list, uint32_t *fail_count, uint32_t *fail_bits,
                                uint32_t pos_base, bool retry, bool fix_seed, bool sq, float *kb,
-                               hipStream_t s, float *kth_side) {
+                               hipStream_t s, float *kth_side, uint32_t *pair_scratch) {
     if (span.m == 0) return NBKD_OK;
     float *kbound = k > 64 ? kb : nullptr;
     {
@@ -1267,16 +1406,20 @@ nbkd_status launch_select_pass(const Tree &t, const float *q, const uint32_t *or
                               fail_count, fail_bits, pos_base, tg_fix, mu, sq, s, kth_side);
         else if (k <= 128)
             launch_select_wave<2>(t, q, order, span, k, qpp, cand, capg, ccount, od, oi,
-                                  fail_list, fail_count, fail_bits, pos_base, tg_fix, mu, sq, kbound, s);
+                                  fail_list, fail_count, fail_bits, pos_base, tg_fix, mu, sq, kbound, s,
+                                  pair_scratch);
         else if (k <= 256)
             launch_select_wave<4>(t, q, order, span, k, qpp, cand, capg, ccount, od, oi,
-                                  fail_list, fail_count, fail_bits, pos_base, tg_fix, mu, sq, kbound, s);
+                                  fail_list, fail_count, fail_bits, pos_base, tg_fix, mu, sq, kbound, s,
+                                   nullptr);
         else if (k <= 512)
             launch_select_wave<8>(t, q, order, span, k, qpp, cand, capg, ccount, od, oi,
-                                  fail_list, fail_count, fail_bits, pos_base, tg_fix, mu, sq, kbound, s);
+                                  fail_list, fail_count, fail_bits, pos_base, tg_fix, mu, sq, kbound, s,
+                                   nullptr);
         else
             launch_select_wave<16>(t, q, order, span, k, qpp, cand, capg, ccount, od, oi,
-                                   fail_list, fail_count, fail_bits, pos_base, tg_fix, mu, sq, kbound, s);
+                                   fail_list, fail_count, fail_bits, pos_base, tg_fix, mu, sq, kbound, s,
+                                   nullptr);
         NBKD_HIP(hipGetLastError());
     }
     return NBKD_OK;

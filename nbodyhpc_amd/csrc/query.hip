@@ -1278,6 +1278,13 @@ nbkd_status knn_locked(const Tree &t, Workspace &ws, const float *q, uint64_t m,
                 kb = (float *)ws.get(WS_KB, std::max<uint64_t>(batch, (uint64_t)mm) * 4u, s);
                 if (!kb) return NBKD_ENOMEM;
             }
+            // 64 < k <= 128: the first pass's wave select takes two queries
+            // per wave where it can; the leftover positions list here
+            uint32_t *pair_scratch = nullptr;
+            if (k > 64 && k <= 128) {
+                pair_scratch = (uint32_t *)ws.get(WS_PAIR, (batch + 32) * 4u, s);
+                if (!pair_scratch) return NBKD_ENOMEM;
+            }
             // Seed failures (fewer than k points in the seed ball, or more than
             // the column holds) are re-walked without the host reading how many
             // there are: the first pass marks them in a bitmap over the sorted
@@ -1304,7 +1311,8 @@ nbkd_status knn_locked(const Tree &t, Workspace &ws, const float *q, uint64_t m,
                     sp1.tg_pos = self; // seeds (and the first pass's rewritten ones) per position
                     rc = launch_knn_collect(t, dq, ord + b0, sp1, k, self ? tgp + b0 : tg, 1.0f, 64u,
                                             cand, capg, ccount, dd, di, nullptr, nullptr, bits,
-                                            (uint32_t)b0, false, adaptive, sq, kb, stats, s, ks);
+                                            (uint32_t)b0, false, adaptive, sq, kb, stats, s, ks,
+                                            pair_scratch);
                     if (rc) return rc;
                 }
             }

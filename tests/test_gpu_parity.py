@@ -615,3 +615,30 @@ def test_ball_count_wide_radius_periodic_images(gpu, oracle, box, r):
     t = gpu.Tree(pts, leafsize=64, boxsize=box)
     c = t.ball_count(q, r)
     assert np.array_equal(c, oracle.ball_count_brute(pts, q, r, box))
+
+
+@pytest.mark.parametrize("k,box", [(65, 1.0), (100, None), (127, 1.0), (128, 1.0)])
+def test_wave_select_pairs_vs_oracle(gpu, oracle, k, box):
+    """64 < k <= 128 (round 6): the first pass's wave select takes two queries
+    per wave; an odd query count leaves the last one unpaired, and columns it
+    cannot take (failures, more than 128 below the bound) go to the one-query
+    kernel.  Rows and the k-th distance against the oracle, plain and with a
+    seed margin that fails most first passes."""
+    pts = uniform(80_000, 900 + k, L=box or 1.0)
+    rng = np.random.Generator(np.random.PCG64(k))
+    q = np.concatenate([pts[:2001], rng.uniform(0, box or 1.0, (1000, 3)).astype(np.float32)])
+    t = gpu.Tree(pts, leafsize=64, boxsize=box)
+    o = oracle.tree(pts, 64, box)
+    dr, ir = o.query(q, k)
+    d, i = t.query(q, k)
+    assert_knn_equal(d, i, dr, ir, pts, q, box)
+    kth = t.query_kth(q, k)
+    assert np.array_equal(kth.view(np.uint32), dr[:, k - 1].view(np.uint32))
+    saved = gpu.get_tuning("knn_seed_margin")
+    try:
+        gpu.set_tuning("knn_seed_margin", 0.3)
+        d, i = t.query(q, k)
+        assert_knn_equal(d, i, dr, ir, pts, q, box)
+    finally:
+        gpu.set_tuning("knn_seed_margin", saved)
+    t.close()
