@@ -104,7 +104,9 @@ nbkd_status nbkd_build(const float *xyz, uint64_t n, int32_t leaf_size, int32_t 
  * leaves are not flat: an x-slab of 1/8 of the box took 35 % more leaves
  * per query with depth % 3.  Same median rule, leaves and padding; the node
  * table differs from the reference's when the schedule does (extent (1, 1, 1)
- * gives depth % 3); every query result is the same, exactly. */
+ * gives depth % 3).  Query results: distances identical; indices identical up
+ * to exact-distance ties (the traversal order differs, so which member of a
+ * tied group a row holds may too). */
 nbkd_status nbkd_build_ext(const float *xyz, uint64_t n, int32_t leaf_size, int32_t periodic,
                            float box_size, const float *extent, int32_t device, uint32_t flags,
                            void *stream, nbkd_tree **out);
@@ -246,7 +248,9 @@ nbkd_status nbkd_set_ids(nbkd_tree *tree, const uint32_t *ids, uint32_t flags, v
  * every row's last column (its k-th distance, as the row holds it) to
  * kth[row].  A slab's exactness test then reads 4 B per row instead of a
  * row's last line (nbkd_slab_forward_async with dist = kth, k = 1).  kth =
- * NULL or capacity = 0 detaches it; other calls leave it untouched. */
+ * NULL or capacity = 0 detaches it; other calls leave it untouched.  The call
+ * waits for every kNN of the tree already enqueued (on any stream), so the
+ * previously attached array may be freed once it returns. */
 nbkd_status nbkd_set_kth_out(nbkd_tree *tree, float *kth, uint64_t capacity);
 
 /* Stable compaction of the points with lo <= x < hi into out_xyz / out_ids

@@ -312,6 +312,14 @@ nbkd_status nbkd_set_kth_out(nbkd_tree *tree, float *kth, uint64_t capacity) {
     Tree &t = tree->t;
     DevGuard g(t.device);
     AllWs all(t, nullptr); // no query of this tree runs while the target changes
+    // a kNN already queued on another stream may still write the
+    // old array; the host waits for every workspace's last call, so the
+    // caller may free the old array once this returns
+    auto drain = [](Workspace &w) {
+        if (w.used && w.done) (void)hipEventSynchronize(w.done);
+    };
+    drain(t.ws);
+    for (auto &w : t.ws_extra) drain(*w);
     t.kth_side = capacity ? kth : nullptr;
     t.kth_side_cap = kth ? capacity : 0;
     return NBKD_OK;

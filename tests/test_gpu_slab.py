@@ -531,3 +531,23 @@ def test_extent_axes_slab_tree(gpu, oracle, box):
     dr, ir = oracle.tree(pts, 32, box).query(q, k, workers=8)
     assert_knn_equal(d1, i1, dr, ir, pts, q, box)
     assert np.array_equal(t_ext.ball_count(pts, 0.01), t_ref.ball_count(pts, 0.01))
+
+
+def test_extent_tree_rows_on_tie_heavy_lattice(gpu, oracle):
+    """an extent-scheduled tree and the depth % 3 tree give
+    identical distances on a lattice full of exact-distance ties; indices may
+    differ only inside tied groups (assert_knn_equal checks them as sets)."""
+    from tests.parity import assert_knn_equal
+    g = np.arange(24, dtype=np.float32) / np.float32(24.0)
+    xs, ys, zs = np.meshgrid(g * np.float32(0.25), g, g, indexing="ij")
+    pts = np.stack([xs.ravel(), ys.ravel(), zs.ravel()], 1).astype(np.float32)
+    k = 27
+    t_ref = gpu.Tree(pts, leafsize=32, boxsize=1.0)
+    t_ext = gpu.Tree(pts, leafsize=32, boxsize=1.0, extent=(0.25, 1.0, 1.0))
+    q = pts[::7]
+    d0, i0 = t_ref.query(q, k)
+    d1, i1 = t_ext.query(q, k)
+    assert np.array_equal(d1.view(np.uint32), d0.view(np.uint32))
+    assert_knn_equal(d1, i1, d0, i0, pts, q, 1.0)
+    dr, ir = oracle.tree(pts, 32, 1.0).query(q, k, workers=8)
+    assert_knn_equal(d1, i1, dr, ir, pts, q, 1.0)
