@@ -62,6 +62,18 @@ constexpr int WPB = TB / 64;
 #ifndef NBKD_WAVE_PAIR
 #define NBKD_WAVE_PAIR 4 // 64 < k <= 128: queries per wave in the first pass's wave select (0: one)
 #endif
+// a short first-pass column (n < k points in the seed ball): the retry's seed
+// volume grows to hold NBKD_RETRY_GROW mu points at the density n measured,
+// at least NBKD_RETRY_MINV x and at most 8 x
+#ifndef NBKD_LOOP_AHEAD
+#define NBKD_LOOP_AHEAD 1 // the re-walk rounds' (LOOP) collect with the first pass's look-ahead
+#endif
+#ifndef NBKD_RETRY_GROW
+#define NBKD_RETRY_GROW 1.0f
+#endif
+#ifndef NBKD_RETRY_MINV
+#define NBKD_RETRY_MINV 2.0f
+#endif
 #ifndef NBKD_PAIR_PREFETCH
 #define NBKD_PAIR_PREFETCH 0 // (with NBKD_PAIR_PAD) the next step's pair entry read one step early
 #endif
@@ -605,13 +617,15 @@ select_block(const DevTree &t, const float *__restrict__ q, const uint32_t *__re
                           fail_list, fail_count, fail_bits);
         // the retry's seed (tg_fix: first pass only); n counted every point
         // inside the seed ball, so it measured the local density.  n < k:
-        // grow the volume to hold ~1.5 mu at that density (2x..8x).  An
+        // grow the volume to hold ~mu at that density (2x..8x; 1.5 mu until
+        // round 6: log-normal 1e8 re-walks 9.48 -> 9.09 ms,
+        // profiles/r06l_retry_ab.txt).  An
         // overflowing column (n > capg): the retry's column is 8 capg, so keep
         // the seed while n fits half of it, else shrink it to that.
         if (tg_fix) {
             float fv;
             if (n < (uint32_t)k)
-                fv = fminf(8.0f, fmaxf(2.0f, 1.5f * mu / fmaxf((float)n, 0.5f)));
+                fv = fminf(8.0f, fmaxf(NBKD_RETRY_MINV, NBKD_RETRY_GROW * mu / fmaxf((float)n, 0.5f)));
             else
                 fv = fminf(1.0f, 4.0f * (float)capg / (float)n);
             const uint32_t ti = tg_pos ? gq : qo;
@@ -1043,7 +1057,7 @@ knn_select_wave_kernel(DevTree t, const float *__restrict__ q, const uint32_t *_
                 if (tg_fix) { // the retry's seed, as knn_select_kernel
                     float fv;
                     if (n < (uint32_t)k)
-                        fv = fminf(8.0f, fmaxf(2.0f, 1.5f * mu / fmaxf((float)n, 0.5f)));
+                        fv = fminf(8.0f, fmaxf(NBKD_RETRY_MINV, NBKD_RETRY_GROW * mu / fmaxf((float)n, 0.5f)));
                     else
                         fv = fminf(1.0f, 4.0f * (float)capg / (float)n);
                     const uint32_t ti = span.tg_pos ? gp : qo;
@@ -1228,7 +1242,7 @@ void launch_collect(const Tree &t, const float *q, const uint32_t *order, QSpan 
         view(t), t.ginfo, t.leafinfo, t.hinfo, q, order, span, k, tg, seed_mul, qpp, cand, capg,   \
         ccount, STP, XCD, kbound)
         if (span.count)
-            NBKD_GRP(false, true, false, nullptr, false);
+            NBKD_GRP(false, true, NBKD_LOOP_AHEAD != 0, nullptr, false);
         else if (collect_ahead()) {
             if (stats)
                 NBKD_GRP(true, false, true, stats, xcd);
@@ -1346,7 +1360,8 @@ uint32_t collect_capacity(int k) {
     // seed balls hold mu = k + 4 sqrt(k) + 4 points on average; the column
     // takes mu + 5 sqrt(mu), rounded up to a multiple of 16
     const double mu = k + 4.0 * std::sqrt((double)k) + 4.0;
-    const double c = mu + 5.0 * std::sqrt(mu);
+    double c = mu + 5.0 * std::sqrt(mu);
+    if (const char *e = knob("NBKD_KNN_CAP")) c *= std::max(0.25, atof(e)); // experiments only
     return (uint32_t)((c + 15.0) / 16.0) * 16u;
 }
 
