@@ -220,30 +220,66 @@ __device__ __forceinline__ void seed_turn(SeedPath &w, bool right, int o, uint64
     }
 }
 
-// anch[c] = (first position, seed bits) of the anchor holding position 64c
+// anch[c] = (first position, boundary, seed bits below it, seed bits at or
+// past it) of the anchor holding position 64c.  The boundary splits the
+// anchor into its two halves (its children; child_th != 0 and the anchor not
+// a leaf): a half sparser than the anchor as a whole -- its seed above
+// child_th times the anchor's -- gives its positions max(anchor seed,
+// child_s x its own).  On log-normal 1e8 (k = 32) 6.3 % of the self queries
+// found fewer than k points in the anchor's seed ball; with child_th = 1.1
+// the re-walks drop 7.07 M -> 4.32 M and the step 62.98 -> 61.39 ms, while
+// uniform data (whose halves' volumes differ by ~12 %) moves by noise
+// (82 k -> 64 k re-walks, 52.49 -> 52.32 ms).  1.0 re-walks 4.03 M
+// log-normal but costs uniform +0.4 ms; each half its own seed (-1) 6.09 M,
+// and at x1.1 3.89 M but +0.9 ms uniform (profiles/r06l_retry_ab.txt).
 // (tried and dropped: the anchor's tight span from its 8-point group boxes
 // where the cell reaches through empty space -- the same seed failures on
 // slab trees and log-normal data, +0.13 ms per 1e8; profiles/r05s_ab.txt)
 __global__ void __launch_bounds__(TB)
 anchor_chunk_kernel(const float *__restrict__ hf, int o, uint32_t n8, uint32_t stop,
-                    uint32_t nchunks, uint2 *__restrict__ anch, float mu_c, float3 box_lo,
-                    float3 box_hi, uint64_t axes) {
+                    uint32_t nchunks, uint4 *__restrict__ anch, float mu_c, float3 box_lo,
+                    float3 box_hi, uint64_t axes, uint32_t leaf, float child_th, float child_s) {
     const uint32_t c = blockIdx.x * TB + threadIdx.x;
     if (c >= nchunks) return;
     const uint32_t p = c * 64u;
     SeedPath w{0u, n8, 0u, 0u, 1u, 0u, o, 0, 0u, 0u, 0u, 0u, 0u, 0u};
     while (w.count > stop) seed_turn(w, p >= w.left + (w.count / 2) / 8 * 8, o, axes);
-    const float lo[3] = {w.lo0 ? hf[w.lo0 - 1] : box_lo.x, w.lo1 ? hf[w.lo1 - 1] : box_lo.y,
-                         w.lo2 ? hf[w.lo2 - 1] : box_lo.z};
-    const float hi[3] = {w.hi0 ? hf[w.hi0 - 1] : box_hi.x, w.hi1 ? hf[w.hi1 - 1] : box_hi.y,
-                         w.hi2 ? hf[w.hi2 - 1] : box_hi.z};
-    anch[c] = make_uint2(w.left, __float_as_uint(guess_r2(w.count, lo, hi, mu_c)));
+    float lo[3] = {w.lo0 ? hf[w.lo0 - 1] : box_lo.x, w.lo1 ? hf[w.lo1 - 1] : box_lo.y,
+                   w.lo2 ? hf[w.lo2 - 1] : box_lo.z};
+    float hi[3] = {w.hi0 ? hf[w.hi0 - 1] : box_hi.x, w.hi1 ? hf[w.hi1 - 1] : box_hi.y,
+                   w.hi2 ? hf[w.hi2 - 1] : box_hi.z};
+    const float ra = guess_r2(w.count, lo, hi, mu_c);
+    uint32_t bnd = w.left + w.count;
+    float r0 = ra, r1 = ra;
+    if (child_th != 0.0f && w.count > leaf && w.count >= 64u && ra < FLT_MAX) {
+        // the anchor's own split: heap index + 1 as seed_turn computes it
+        const uint32_t at = 16u * w.b + (1u << w.l) + w.lp;
+        const float sv = hf[at - 1];
+        const int dim = axis_at(axes, w.depth);
+        const uint32_t mm = (w.count / 2) / 8 * 8;
+        bnd = w.left + mm;
+        const float keep_hi = hi[dim], keep_lo = lo[dim];
+        hi[dim] = sv;
+        const float rl = guess_r2(mm, lo, hi, mu_c);
+        hi[dim] = keep_hi;
+        lo[dim] = sv;
+        const float rr = guess_r2(w.count - mm, lo, hi, mu_c);
+        lo[dim] = keep_lo;
+        if (child_th < 0.0f) { // experiments: each half its own seed
+            r0 = rl < FLT_MAX ? rl * child_s : ra;
+            r1 = rr < FLT_MAX ? rr * child_s : ra;
+        } else {
+            if (rl < FLT_MAX && rl > child_th * ra) r0 = fmaxf(ra, rl * child_s);
+            if (rr < FLT_MAX && rr > child_th * ra) r1 = fmaxf(ra, rr * child_s);
+        }
+    }
+    anch[c] = make_uint4(w.left, bnd, __float_as_uint(r0), __float_as_uint(r1));
 }
 
 // tgp[i] = the seed of position pos[i] (pos nullptr: i); with pos, also
 // order[i] = perm[pos[i]]; tgp nullptr: the order alone
 __global__ void __launch_bounds__(TB)
-self_seed_kernel(const uint2 *__restrict__ anch, uint32_t nchunks,
+self_seed_kernel(const uint4 *__restrict__ anch, uint32_t nchunks,
                  const uint32_t *__restrict__ pos, const uint32_t *__restrict__ perm, uint32_t m,
                  uint32_t *__restrict__ order, float *__restrict__ tgp) {
     for (uint32_t i = blockIdx.x * TB + threadIdx.x; i < m; i += gridDim.x * TB) {
@@ -251,9 +287,12 @@ self_seed_kernel(const uint2 *__restrict__ anch, uint32_t nchunks,
         if (pos) order[i] = perm[p];
         if (!tgp) continue;
         const uint32_t c = p >> 6;
-        const uint2 a = anch[c];
-        const uint2 b = c + 1 < nchunks ? anch[c + 1] : a;
-        tgp[i] = __uint_as_float(p >= b.x ? b.y : a.y);
+        uint4 a = anch[c];
+        if (c + 1 < nchunks) {
+            const uint4 b = anch[c + 1];
+            if (p >= b.x) a = b;
+        }
+        tgp[i] = __uint_as_float(p < a.y ? a.z : a.w);
     }
 }
 
@@ -944,10 +983,17 @@ constexpr int KNN_PACKET_KMAX = 1024;
 // and kth_locked's k > 1024 rows go to scratch; neither may touch it)
 constexpr uint32_t KNN_SIDE_OK = 0x80000000u;
 
+#ifndef NBKD_KNN_CHILD_TH
+#define NBKD_KNN_CHILD_TH 1.1f
+#endif
+#ifndef NBKD_KNN_CHILD_S
+#define NBKD_KNN_CHILD_S 1.0f
+#endif
 struct SeedParams {
     bool on;
     float mu_c;
     uint32_t anchor;
+    float child_th, child_s; // self seeds: a sparse anchor half's own seed (anchor_chunk_kernel)
 };
 SeedParams seed_params(const Tree &t, int k) {
     // a = 3.0 (round 5, with the self order, profiles/r05ab_seed_margin_ab.txt,
@@ -972,6 +1018,10 @@ SeedParams seed_params(const Tree &t, int k) {
     // much: log-normal 1e8 retried 5.7 M queries)
     const char *ea = knob("NBKD_KNN_ANCHOR"); // tuning only: anchor in points
     p.anchor = std::max<uint32_t>((uint32_t)t.leaf, ea ? (uint32_t)std::max(1, atoi(ea)) : 128u);
+    const char *ec = knob("NBKD_KNN_CHILD"); // tuning only: 0 = the anchor's seed everywhere
+    p.child_th = ec ? (float)atof(ec) : NBKD_KNN_CHILD_TH;
+    const char *es = knob("NBKD_KNN_CHILD_S");
+    p.child_s = es ? (float)atof(es) : NBKD_KNN_CHILD_S;
     return p;
 }
 
@@ -1066,16 +1116,16 @@ nbkd_status self_order(const Tree &t, Workspace &ws, uint32_t m, uint32_t *&orde
     }
     if (!pos && !tgp) return NBKD_OK;
     const uint32_t nchunks = (uint32_t)((t.n8 + 63) / 64);
-    uint2 *anch = nullptr;
+    uint4 *anch = nullptr;
     if (tgp) {
-        anch = (uint2 *)ws.get(WS_ANCH, (size_t)nchunks * 8, s);
+        anch = (uint4 *)ws.get(WS_ANCH, (size_t)nchunks * 16, s);
         if (!anch) return NBKD_ENOMEM;
         const float3 lo = seed_lo(t), hi = seed_hi(t);
         // an anchor below 64 points would break the two-anchors-per-chunk rule
         const uint32_t stop = std::max<uint32_t>({sp->anchor, (uint32_t)t.leaf, 128u});
         anchor_chunk_kernel<<<(nchunks + TB - 1) / TB, TB, 0, s>>>(
             t.hsplit, hblk_offset(t.depth), (uint32_t)t.n8, stop, nchunks, anch, sp->mu_c, lo, hi,
-            t.axes);
+            t.axes, (uint32_t)t.leaf, sp->child_th, sp->child_s);
         NBKD_HIP(hipGetLastError());
     }
     const unsigned blocks = (unsigned)std::min<uint64_t>(((uint64_t)m + TB - 1) / TB, 65536);
@@ -1824,7 +1874,7 @@ nbkd_status query_ball_csr(const Tree &t, const float *q, uint64_t m, float r, u
     WsCall call(ws, s, std::adopt_lock);
     NBKD_HIP(call.err);
     const uint32_t dev_io = NBKD_INPUT_DEVICE | NBKD_OUTPUT_DEVICE;
-    const bool in_dev = (flags & NBKD_INPUT_DEVICE) != 0, out_dev = (flags & NBKD_OUTPUT_DEVICE) != 0;
+    const bool out_dev = (flags & NBKD_OUTPUT_DEVICE) != 0;
     const uint32_t cflags = flags & (NBKD_INPUT_DEVICE | NBKD_OUTPUT_DEVICE);
     nbkd_status rc;
     {
