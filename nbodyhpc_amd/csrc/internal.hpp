@@ -333,6 +333,10 @@ struct QSpan {
     // tg is indexed by the position in this pass's order (self queries: the
     // seed per tree position), not by query id
     bool tg_pos = false;
+    // first pass, periodic trees: the collect appends the queries outside
+    // [0, L]^3 to out_list (count at out_count) for the exact kernel
+    uint32_t *out_list = nullptr;
+    uint32_t *out_count = nullptr;
 };
 __host__ __device__ inline QSpan static_span(uint32_t m) { return QSpan{m, nullptr, 0u, 0u, 0}; }
 __device__ __forceinline__ uint32_t span_m(const QSpan &s) {

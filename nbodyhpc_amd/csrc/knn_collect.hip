@@ -445,13 +445,22 @@ __device__ __forceinline__ void collect_packet(
     uint32_t m, int kq, const float *__restrict__ tg, bool tg_pos, float seed_mul, uint32_t qpp,
     uint2 *__restrict__ cand, uint32_t capg, uint32_t *__restrict__ ccount,
     unsigned long long *__restrict__ stats, float *__restrict__ kbound, CollectLdsG &W, int lane,
-    uint32_t pk) {
+    uint32_t pk, uint32_t *__restrict__ out_list, uint32_t *__restrict__ out_count) {
     const uint32_t gq = pk * qpp + lane;
     const bool valid = (uint32_t)lane < qpp && gq < m;
     const uint32_t qo = valid ? order[gq] : 0u;
     const float qx = valid ? q[3 * (size_t)qo] : 0.0f;
     const float qy = valid ? q[3 * (size_t)qo + 1] : 0.0f;
     const float qz = valid ? q[3 * (size_t)qo + 2] : 0.0f;
+    // the first pass lists the periodic queries outside [0, L]^3 for the
+    // exact kernel (QSpan::out_list; until round 6 a separate outside_box_kernel
+    // pass re-read every query); the packet still walks them, and their
+    // select skips them as failures (mark_failure)
+    if constexpr (PER) {
+        if (out_list && valid &&
+            !(qx >= 0.0f && qx <= t.box && qy >= 0.0f && qy <= t.box && qz >= 0.0f && qz <= t.box))
+            out_list[atomicAdd(out_count, 1u)] = qo;
+    }
     const float seed = valid ? fminf(tg[tg_pos ? gq : qo] * seed_mul, FLT_MAX) : -INFINITY;
     const bool fin = seed < FLT_MAX && seed >= 1e-30f;
     const float s_over_nb = fin ? seed * (1.0f / NB) : (seed > 0.0f ? INFINITY : 0.0f);
@@ -536,14 +545,14 @@ knn_collect_grp_kernel(DevTree t, const float *__restrict__ ginfo,
             wave_sync(); // the previous packet's LDS reads are done
             collect_packet<PER, STATS, AHEAD>(t, ginfo, linfo, hinfo, q, order, m, kq, tg, span.tg_pos,
                                               seed_mul, qpp, cand, capg, ccount, stats, kbound,
-                                              W, lane, pk);
+                                              W, lane, pk, span.out_list, span.out_count);
         }
     } else {
         const uint32_t pk = bid * WPB + wave;
         if (pk < npk)
             collect_packet<PER, STATS, AHEAD>(t, ginfo, linfo, hinfo, q, order, m, kq, tg, span.tg_pos,
                                               seed_mul, qpp, cand, capg, ccount, stats, kbound,
-                                              W, lane, pk);
+                                              W, lane, pk, span.out_list, span.out_count);
     }
 }
 

@@ -296,6 +296,32 @@ self_seed_kernel(const uint4 *__restrict__ anch, uint32_t nchunks,
     }
 }
 
+// the same for the identity order (pos nullptr): four positions per thread,
+// one 16-B store, one pass over the grid (the grid-stride form above spent
+// 0.24 ms per 1e8 positions, latency-bound)
+__global__ void __launch_bounds__(TB)
+self_seed4_kernel(const uint4 *__restrict__ anch, uint32_t nchunks, uint32_t m,
+                  float *__restrict__ tgp) {
+    const uint32_t p0 = (blockIdx.x * TB + threadIdx.x) * 4u;
+    if (p0 >= m) return;
+    const uint32_t c = p0 >> 6; // the four positions share a chunk (64 = 16 x 4)
+    const uint4 a = anch[c];
+    const uint4 b = c + 1 < nchunks ? anch[c + 1] : a;
+    float v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint32_t p = p0 + j;
+        const uint4 e = p >= b.x ? b : a;
+        v[j] = __uint_as_float(p < e.y ? e.z : e.w);
+    }
+    if (p0 + 4 <= m) { // tgp is a 256-B aligned workspace buffer
+        *reinterpret_cast<float4 *>(tgp + p0) = make_float4(v[0], v[1], v[2], v[3]);
+    } else {
+        for (int j = 0; j < 4; ++j)
+            if (p0 + j < m) tgp[p0 + j] = v[j];
+    }
+}
+
 // bits[p / 32] bit p % 32 = perm[p] < m: the tree positions of the first m
 // input rows (self queries over a prefix of the build input, e.g. a slab's
 // owned particles ahead of its halo)
@@ -1128,8 +1154,13 @@ nbkd_status self_order(const Tree &t, Workspace &ws, uint32_t m, uint32_t *&orde
             t.axes, (uint32_t)t.leaf, sp->child_th, sp->child_s);
         NBKD_HIP(hipGetLastError());
     }
-    const unsigned blocks = (unsigned)std::min<uint64_t>(((uint64_t)m + TB - 1) / TB, 65536);
-    self_seed_kernel<<<blocks, TB, 0, s>>>(anch, nchunks, pos, perm, m, order, tgp);
+    if (!pos) {
+        const uint64_t th = ((uint64_t)m + 3) / 4;
+        self_seed4_kernel<<<(unsigned)((th + TB - 1) / TB), TB, 0, s>>>(anch, nchunks, m, tgp);
+    } else {
+        const unsigned blocks = (unsigned)std::min<uint64_t>(((uint64_t)m + TB - 1) / TB, 65536);
+        self_seed_kernel<<<blocks, TB, 0, s>>>(anch, nchunks, pos, perm, m, order, tgp);
+    }
     NBKD_HIP(hipGetLastError());
     return NBKD_OK;
 }
@@ -1256,7 +1287,8 @@ nbkd_status knn_locked(const Tree &t, Workspace &ws, const float *q, uint64_t m,
         if (!list) return NBKD_ENOMEM;
         count = list + mm;
         NBKD_HIP(hipMemsetAsync(count, 0, 4, s));
-        if (t.periodic) {
+        // the collect / select path lists them in its first pass (QSpan::out_list)
+        if (t.periodic && !(tg && !collect_disabled())) {
             TimedScope ts("knn_outside_box", s);
             outside_box_kernel<<<(mm + TB - 1) / TB, TB, 0, s>>>(dq, mm, t.box, list, count);
             NBKD_HIP(hipGetLastError());
@@ -1359,6 +1391,10 @@ nbkd_status knn_locked(const Tree &t, Workspace &ws, const float *q, uint64_t m,
                     const uint32_t nb = (uint32_t)std::min<uint64_t>(batch, mm - b0);
                     QSpan sp1 = static_span(nb);
                     sp1.tg_pos = self; // seeds (and the first pass's rewritten ones) per position
+                    if (t.periodic) {
+                        sp1.out_list = list;
+                        sp1.out_count = count;
+                    }
                     rc = launch_knn_collect(t, dq, ord + b0, sp1, k, self ? tgp + b0 : tg, 1.0f, 64u,
                                             cand, capg, ccount, dd, di, nullptr, nullptr, bits,
                                             (uint32_t)b0, false, adaptive, sq, kb, stats, s, ks,
