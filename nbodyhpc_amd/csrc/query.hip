@@ -105,7 +105,7 @@ __global__ void __launch_bounds__(TB)
 leaf_key3_kernel(const float4 *__restrict__ hb, int o, uint32_t n8, uint32_t leaf,
                  const float *__restrict__ q, uint32_t m, uint32_t *__restrict__ keys,
                  uint32_t *__restrict__ vals, float *__restrict__ tg, float mu_c, uint32_t anchor,
-                 float3 box_lo, float3 box_hi, uint64_t axes) {
+                 float3 box_lo, float3 box_hi, uint64_t axes, float child_th, float child_s) {
     for (uint32_t i = blockIdx.x * TB + threadIdx.x; i < m; i += gridDim.x * TB) {
         const float p[3] = {q[3 * (size_t)i], q[3 * (size_t)i + 1], q[3 * (size_t)i + 2]};
         uint32_t left = 0, count = n8;
@@ -113,6 +113,7 @@ leaf_key3_kernel(const float4 *__restrict__ hb, int o, uint32_t n8, uint32_t lea
         float lo[3] = {box_lo.x, box_lo.y, box_lo.z}, hi[3] = {box_hi.x, box_hi.y, box_hi.z};
         float r2 = FLT_MAX;
         bool have_r2 = tg == nullptr;
+        bool half = false; // the anchor's half the query falls in is next (anchor_chunk_kernel's rule)
         // line b of block level j (level start `base`, `nb` lines); first level l0
         uint32_t b = 0, base = 0, nb = 1;
         int l0 = o;
@@ -127,6 +128,7 @@ leaf_key3_kernel(const float4 *__restrict__ hb, int o, uint32_t n8, uint32_t lea
                 if (!have_r2 && count <= anchor) {
                     r2 = guess_r2(count, lo, hi, mu_c);
                     have_r2 = true;
+                    half = child_th > 0.0f && count >= 64u && r2 < FLT_MAX;
                 }
                 float s;
                 if (l == 0)
@@ -152,6 +154,11 @@ leaf_key3_kernel(const float4 *__restrict__ hb, int o, uint32_t n8, uint32_t lea
                     count = mm;
                 }
                 pos = 2 * pos + (right ? 1u : 0u);
+                if (half) {
+                    const float rc = guess_r2(count, lo, hi, mu_c);
+                    if (rc < FLT_MAX && rc > child_th * r2) r2 = fmaxf(r2, child_s * rc);
+                    half = false;
+                }
             }
             if (count <= leaf) break;
             // pos = child index 0..15 of the next line
@@ -1078,7 +1085,8 @@ nbkd_status sort_queries(const Tree &t, Workspace &ws, const float *dq, uint32_t
             leaf_key3_kernel<<<blocks, TB, 0, s>>>((const float4 *)t.hsplit, hblk_offset(t.depth),
                                                    (uint32_t)t.n8, (uint32_t)t.leaf, dq, m,
                                                    keys, order, tg, sp ? sp->mu_c : 0.0f,
-                                                   sp ? sp->anchor : 0u, lo, hi, t.axes);
+                                                   sp ? sp->anchor : 0u, lo, hi, t.axes,
+                                                   sp ? sp->child_th : 0.0f, sp ? sp->child_s : 1.0f);
         } else if (t.shape_len <= SHAPE_MAX) {
             const unsigned blocks = (unsigned)std::min<uint64_t>((m + TB - 1) / TB, 8192);
             const float3 lo = seed_lo(t), hi = seed_hi(t);

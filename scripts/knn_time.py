@@ -1,7 +1,7 @@
 """One library build, one workload: per-phase kNN times (HIP events on the
 launch stream) and a SHA of the full distance and id arrays, as one JSON line.
 The library is the one NBKD_LIB names (A/B runs: scripts/lib_ab.py).
-python scripts/knn_time.py --n 1e8 --k 32 --leaf 64 [--lognormal] [--indep]
+python scripts/knn_time.py --n 1e8 --k 32 --leaf 64 [--lognormal]
 
 --slab-world W --slab-rank r [--scaling strong|weak]: rank r's part of the
 bench's W-GPU run, alone on this GPU (scripts/slab_traffic.sh profiles it):
