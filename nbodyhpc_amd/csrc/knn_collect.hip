@@ -59,6 +59,22 @@ constexpr int WPB = TB / 64;
 #ifndef NBKD_PAIR_ATOMIC
 #define NBKD_PAIR_ATOMIC 1
 #endif
+//   NBKD_SEL_FIRST     lane-per-query select, k == KC: the first 16-candidate
+//                      block, sorted, IS the top-k state (the rest FLT_MAX),
+//                      so it is copied in without the take and the 32-wide
+//                      merge (80 compare-exchanges per query fewer), in its
+//                      own instance (one instance for both: 54 VGPRs spilled,
+//                      select 14.1 -> 24.0 ms; split: 14.59 -> 13.47 ms per
+//                      1e8 queries, profiles/r06s_select_first_ab.txt)
+#ifndef NBKD_SEL_FIRST
+#define NBKD_SEL_FIRST 1
+#endif
+//   NBKD_WAVE_KEY64    wave selects (k > 64): a lane-exchange stage compares
+//                      (d2, id) as one 64-bit key (one compare, no equal-key
+//                      case) instead of two float compares
+#ifndef NBKD_WAVE_KEY64
+#define NBKD_WAVE_KEY64 0
+#endif
 #ifndef NBKD_WAVE_PAIR
 #define NBKD_WAVE_PAIR 4 // 64 < k <= 128: queries per wave in the first pass's wave select (0: one)
 #endif
@@ -600,7 +616,7 @@ template <int KC> constexpr int select_stage_words() {
 }
 
 // the 64 queries of wave-block wb (m: the pass's query count)
-template <int KC, bool PER, bool WHOLE>
+template <int KC, bool PER, bool WHOLE, bool EX = false>
 __device__ __forceinline__ void
 select_block(const DevTree &t, const float *__restrict__ q, const uint32_t *__restrict__ order,
              uint32_t m, uint32_t wb, int k, const uint2 *__restrict__ cand, uint32_t capg,
@@ -663,9 +679,8 @@ select_block(const DevTree &t, const float *__restrict__ q, const uint32_t *__re
     // a block's rows: 128 B apart (blocked) or one column apart (row-major)
     const uint32_t rs4 = NBKD_COL_ROWMAJOR ? capg / 2u : 8u, bs4 = NBKD_COL_ROWMAJOR ? 8u : 512u;
     if (whole && maxn > 0) issue_block(blk, lds4, lane, __ballot(nn > 0u) | all_rows, rs4);
-    for (uint32_t s0 = 0; s0 < maxn; s0 += NS) {
-        float bd[NS];
-        uint32_t bi[NS];
+    // block s0/16 into (bd, bi); the whole-packet path also issues block s0/16 + 1
+    auto read_block = [&](uint32_t s0, float (&bd)[NS], uint32_t (&bi)[NS]) {
         // block s0/16: 8 KB contiguous -> LDS (row r, 16-B piece j at r*8 + (j ^ (r&7)))
         if constexpr (!whole) { // scattered packets: each lane reads its own row directly
 #pragma unroll
@@ -699,6 +714,30 @@ select_block(const DevTree &t, const float *__restrict__ q, const uint32_t *__re
                 issue_block(blk + (size_t)((s0 + NS) >> 4) * bs4, lds4, lane,
                             __ballot(nn > s0 + NS) | all_rows, rs4);
         }
+    };
+    uint32_t s_first = 0;
+    if constexpr (EX && KC > NS) {
+        // EX: k == KC (no -inf placeholders): td is all FLT_MAX, so the take
+        // and the merge of the first block would leave [block ascending,
+        // FLT_MAX ...]; it is copied in instead (empty slots, INFINITY, stay
+        // FLT_MAX; maxn == 0 reads nothing: every slot is empty)
+        {
+            float bd[NS];
+            uint32_t bi[NS];
+            read_block(0u, bd, bi);
+            bitonic_sort<NS>(bd, bi);
+#pragma unroll
+            for (int s = 0; s < NS; ++s) {
+                td[s] = fminf(bd[s], FLT_MAX);
+                ti[s] = bi[s];
+            }
+            s_first = NS;
+        }
+    }
+    for (uint32_t s0 = s_first; s0 < maxn; s0 += NS) {
+        float bd[NS];
+        uint32_t bi[NS];
+        read_block(s0, bd, bi);
         // a block with nothing below any lane's current k-th changes nothing
         bool useful = false;
 #pragma unroll
@@ -776,10 +815,16 @@ knn_select_kernel(DevTree t, const float *__restrict__ q, const uint32_t *__rest
     } else {
         const uint32_t wb = blockIdx.x * WPB + wave;
         if (wb * 64u >= m) return;
-        select_block<KC, PER, WHOLE>(t, q, order, m, wb, k, cand, capg, ccount, out_d, out_i,
-                                     fail_list, fail_count, pos_base, all_rows, tg_fix,
-                                     span.tg_pos, mu, sq, fail_bits, stage, rowq, lane,
-                                     kth_side);
+        if (NBKD_SEL_FIRST && k == KC) // a separate instance: no join of the two td states
+            select_block<KC, PER, WHOLE, true>(t, q, order, m, wb, k, cand, capg, ccount, out_d,
+                                               out_i, fail_list, fail_count, pos_base, all_rows,
+                                               tg_fix, span.tg_pos, mu, sq, fail_bits, stage,
+                                               rowq, lane, kth_side);
+        else
+            select_block<KC, PER, WHOLE>(t, q, order, m, wb, k, cand, capg, ccount, out_d, out_i,
+                                         fail_list, fail_count, pos_base, all_rows, tg_fix,
+                                         span.tg_pos, mu, sq, fail_bits, stage, rowq, lane,
+                                         kth_side);
     }
 }
 
@@ -872,8 +917,17 @@ __device__ __forceinline__ void wave_cx(float (&d)[R], uint32_t (&p)[R], int lan
             const uint64_t asc_m = SIZE >= 64 ? ((((r * 64) & SIZE) == 0) ? ones : 0ull)
                                               : lanes_bit_clear(SIZE);
             const uint64_t M = ~(lower ^ (DESC ? ~asc_m : asc_m)); // lower == ascending
+#if NBKD_WAVE_KEY64
+            // (d2 bits, id) as one unsigned 64-bit key: d2 >= 0, so the bits
+            // order as the values, and the ids of one column are distinct, so
+            // partners differ unless both are padding (equal: either way)
+            const uint64_t ko = ((uint64_t)__float_as_uint(od[r]) << 32) | op[r];
+            const uint64_t kw = ((uint64_t)__float_as_uint(d[r]) << 32) | p[r];
+            const uint64_t take = ~(M ^ __ballot(ko < kw));
+#else
             const uint64_t lt = __ballot(od[r] < d[r]), gt = __ballot(od[r] > d[r]);
             const uint64_t take = (M & lt) | (~M & gt);
+#endif
             d[r] = lane_set(d[r], od[r], take);
             p[r] = lane_set(p[r], op[r], take);
         }
