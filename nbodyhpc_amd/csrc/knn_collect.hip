@@ -71,9 +71,11 @@ constexpr int WPB = TB / 64;
 #endif
 //   NBKD_WAVE_KEY64    wave selects (k > 64): a lane-exchange stage compares
 //                      (d2, id) as one 64-bit key (one compare, no equal-key
-//                      case) instead of two float compares
+//                      case) instead of two float compares: k = 100 select
+//                      74.50 -> 69.07 ms per 1e8 queries, same distances, ties
+//                      now by id (profiles/r06u_wave_key64_ab.txt)
 #ifndef NBKD_WAVE_KEY64
-#define NBKD_WAVE_KEY64 0
+#define NBKD_WAVE_KEY64 1
 #endif
 #ifndef NBKD_WAVE_PAIR
 #define NBKD_WAVE_PAIR 4 // 64 < k <= 128: queries per wave in the first pass's wave select (0: one)
